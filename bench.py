@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c3_64k|c4]
+  torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
+
+A step = one pass of the hot path over one batch resident in HBM:
+  c1 (default, the metric's config): 256K x 1500 B frames, raw pico_checksum per frame
+  c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
+  c3: 256K x 9000 B jumbo frames;  c3_64k: 16K x 64 KiB reassembled buffers
+  c4: 4M x 1500 B frames sharded over the ranks (strong scaling)
+c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame batches
+are independent shards; no collective touches the data path -- RCCL only carries the
+barrier and the max-over-ranks timing).
+
+Rank 0 prints ONE JSON line.  `roofline` is the checksum kernel's achieved algorithmic HBM
+bandwidth (HIP events around every launch on the launch stream) against the 8.0 TB/s
+HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch from profiles/ (gfx950
+FETCH_SIZE x2 correction, rocprofv3 separate passes) when recorded for this config;
+`cpu_baseline` times the reference's own pico_checksum (compiled from stack/pico_frame.c,
+oracle/_ref) on the host cores over a bounded sample of the same frames.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from picotcp_amd import batch, synth  # noqa: E402
+from picotcp_amd.shard import shard_range  # noqa: E402
+
+METRIC = "device-resident checksummed GiB/s, 1500B-frame batches, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+
+CONFIGS = {
+    "c1": dict(kind="uniform", frames=262144, frame_bytes=1500,
+               workload="C1: 256K x 1500 B (Ethernet MTU) frames, raw pico_checksum per frame, packed stride 1500"),
+    "c2": dict(kind="ipv4", frames=262144,
+               workload="C2: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams (14 B Ethernet header in front), "
+                        "fused IPv4 header + TCP pseudo-header RX verify"),
+    "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
+               workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
+    "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
+                   workload="C3: 16K x 64 KiB reassembled-fragment buffers, raw pico_checksum per buffer"),
+    "c4": dict(kind="uniform", frames=4194304, frame_bytes=1500, strong=True,
+               workload="C4: 4M x 1500 B frames sharded contiguously over the ranks (strong scaling)"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    p.add_argument("--rotate", type=int, default=0, help="rotating batch copies (0 = enough for >= 1 GiB)")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU-baseline wall per leg")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--shape", default="", help="G,CPL,FPW launch override (sweeps)")
+    return p.parse_args()
+
+
+def make_uniform(n, ln, device, seed):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    nbytes = n * ln
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=device, generator=g)
+
+
+def make_c2(n, device, seed):
+    lens = synth.imix_lengths(n, seed)
+    buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
+    desc = batch.make_desc(net, avail)
+    d_buf = torch.from_numpy(buf).to(device)
+    d_desc = batch.desc_to_device(desc, device)
+    # make every datagram valid with the TX kernel (untimed setup), so RX verify accepts
+    batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize(device)
+    return d_buf, d_desc, int(lens.sum())
+
+
+def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
+    """The reference's pico_checksum (oracle/_ref, -O3 = reference PERF=1) over a bounded
+    sample of the same frames: 1 thread and all usable host cores (<= 16 on the box)."""
+    from oracle import oracle as O
+    kind = "reference" if O.ref_available() else "port"
+    n = sample.size // ln
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    res = {}
+    for t in (1, threads):
+        secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind)   # first pass: page-in / warm
+        reps = max(1, int(target_s / max(secs, 1e-3)))
+        tot = 0.0
+        for _ in range(reps):
+            secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind)
+            tot += secs
+        res[t] = (n * ln * reps / tot / GIB, reps)
+    return {
+        "value": round(res[threads][0], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "single_core_value": round(res[1][0], 3),
+        "sample": f"{n} x {ln} B frames ({n * ln / 2**20:.0f} MiB, DRAM-resident), reference stack/pico_frame.c "
+                  f"pico_checksum built -O3, pthreads over contiguous frame ranges; {res[threads][1]} passes on "
+                  f"{threads} threads, {res[1][1]} on 1 thread; host {os.uname().machine}, {cores} usable cores",
+    }
+
+
+def e2e_rate(n, ln):
+    """Host-resident path (pinned host -> H2D -> kernel -> D2H, chunked, 2 streams)."""
+    host = torch.randint(0, 256, (n * ln,), dtype=torch.uint8).pin_memory()
+    hb = batch.HostBatch(torch.cuda.current_device(), staging_bytes=64 << 20)
+    out = np.empty(n, dtype=np.uint16)
+    try:
+        hb.checksum_uniform(host, ln, ln, n, out=out)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            hb.checksum_uniform(host, ln, ln, n, out=out)
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        hb.close()
+    return {"value": round(n * ln / dt / GIB, 3), "unit": "GiB/s",
+            "path": "pico_checksum_batch_uniform_host: pinned host frames -> H2D -> kernel -> D2H results, "
+                    "64 MiB chunks double-buffered on 2 streams"}
+
+
+def load_traffic(config: str):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(config)
+        return None if rec is None else rec.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if a.shape:
+        batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
+    cfg = CONFIGS[a.config]
+
+    # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)
+    if cfg["kind"] == "uniform":
+        ln = cfg["frame_bytes"]
+        if cfg.get("strong"):
+            first, n = shard_range(cfg["frames"], rank, world)
+        else:
+            first, n = rank * cfg["frames"], cfg["frames"]
+        per = n * ln
+        rot = a.rotate or max(2, -(-(1 << 30) // per))
+        bufs = [make_uniform(n, ln, dev, 1000 + 17 * rank + i) for i in range(rot)]
+        outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
+
+        def step(i):
+            batch.checksum_uniform(bufs[i % rot], ln, ln, n, out=outs[i % rot])
+        frame_bytes = per
+        algo_bytes = per + 2 * n                            # frames read + uint16 results written
+    else:
+        n = cfg["frames"]
+        ln = 0
+        rot = max(2, a.rotate)
+        sets = [make_c2(n, dev, 500 + 13 * rank + i) for i in range(rot)]
+
+        def step(i):
+            b, d, _ = sets[i % rot]
+            batch.ipv4_checksum_batch(b, d, n)
+        frame_bytes = sets[0][2]
+        algo_bytes = frame_bytes + 16 * n + 5 * n           # datagrams + descriptors + (2+2+1) B results
+
+    stream = torch.cuda.current_stream(dev)
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+
+    # per-launch HIP events on the launch stream (kernel duration) ...
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    # ... and whole-job time = max over ranks
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_max_ms = float(t[0]), float(t[1])
+    ms_per_step = wall / a.steps * 1e3
+    total_bytes = frame_bytes * (world if not cfg.get("strong") else 1)
+    if cfg.get("strong"):
+        tb = torch.tensor([float(frame_bytes)], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tb)
+        total_bytes = float(tb[0])
+    value = total_bytes / (ms_per_step / 1e3) / GIB
+
+    achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+            "scaling": "strong" if cfg.get("strong") else "weak", "vs_baseline": None, "dtype": "u16",
+            "data": "synthetic (seeded random frame bytes; C2: valid IPv4/TCP headers written by the TX kernel)",
+            "config": {"workload": cfg["workload"], "frames_per_gpu": n, "frame_bytes": ln or "imix",
+                       "batch_bytes_per_gpu": frame_bytes, "rotating_batches": rot,
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(a.config),
+                         "kernel_avg_us": round(kern_ms * 1e3, 2), "kernel_avg_us_max_rank": round(kern_max_ms * 1e3, 2),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+        }
+    if rank == 0 and world == 1 and cfg["kind"] == "uniform":
+        if not a.no_cpu:
+            sample_frames = min(n, 262144)
+            sample = bufs[0][: sample_frames * ln].cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(sample, ln, a.cpu_seconds)
+        if not a.no_e2e:
+            out["e2e_host_to_host"] = e2e_rate(n, ln)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * pico_csum.h -- C ABI of libpicocsum, the MI355X-native drop-in for picoTCP's
+ * Internet-checksum path (RFC 1071 one's-complement sum, stack/pico_frame.c).
+ *
+ * Plain C: no torch, no HIP types in any signature.  Device pointers are
+ * plain `void *` / `T *`; a HIP stream is passed as an opaque `void *`
+ * (NULL = the device's default stream).
+ *
+ * Three layers:
+ *
+ *  1. Scalar drop-in (replaces the two strong symbols of the reference's
+ *     stack/pico_frame.o; callers keep compiling against
+ *     include/pico_frame.h unchanged):
+ *       pico_checksum            ref: include/pico_frame.h:106, stack/pico_frame.c:312-318
+ *       pico_dualbuffer_checksum ref: include/pico_frame.h:107, stack/pico_frame.c:320-328
+ *     The reference calls these inline, once per frame, from a single-threaded
+ *     tick loop on host pointers.  A GPU launch costs ~10 us
+ *     against ~100 ns of work, so these two stay synchronous host code with
+ *     bit-identical results; the accelerated path is layer 2.
+ *
+ *  2. Batched device API (the MI355X hot path; the reference has no batch
+ *     entry -- each function below is the batch form of the per-frame calls
+ *     cited on it).  Buffers are device-resident; calls are asynchronous on
+ *     `stream`; they never fall back to host code: when no HIP device or
+ *     kernel image is usable they return -PICO_ERR_ENODEV and set
+ *     pico_csum_last_error().
+ *
+ *  3. Host-resident batch API: H2D -> kernel -> D2H, chunked and overlapped on
+ *     two streams (the path starts and ends in host memory: a pico_device /
+ *     TAP buffer, modules/pico_dev_tap.c:53-79).
+ *
+ * Return convention of every checksum value (device and host alike) is the
+ * reference's: ret = short_be((uint16_t)~fold(sum)); a caller stores
+ * hdr->crc = short_be(ret), and a region that already carries its correct
+ * checksum yields 0 (pico_ipv4.c:249, pico_socket.c:1927).
+ *
+ * Error codes: 0 on success, otherwise the negated picoTCP pico_err value
+ * (include/pico_protocol.h:21-65).
+ */
+#ifndef PICO_CSUM_H
+#define PICO_CSUM_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PICO_CSUM_ABI_VERSION 1
+
+/* picoTCP pico_err values used here (include/pico_protocol.h:27,31,38 + ENODEV) */
+#define PICO_CSUM_EIO     5
+#define PICO_CSUM_ENOMEM 12
+#define PICO_CSUM_EINVAL 22
+#define PICO_CSUM_ENODEV 19
+
+/* One frame region of a batch: 16 bytes, naturally aligned. */
+#ifndef PICO_CSUM_DESC_DEFINED
+#define PICO_CSUM_DESC_DEFINED
+struct pico_csum_desc {
+    uint64_t off;   /* byte offset of the region from the batch base (any alignment) */
+    uint32_t len;   /* RAW: region length (the `len` of pico_checksum);
+                       IPV4: bytes available from the IPv4 header to the end of
+                       the frame buffer = f->buffer_len - (f->net_hdr - f->buffer) */
+    uint32_t seed;  /* RAW: initial pico_checksum_adder accumulator, e.g. a
+                       pseudo-header partial from pico_ipv4_pseudo_partial()
+                       (TX: from socket state, pico_tcp.c:429-433); 0 for a
+                       plain pico_checksum.  IPV4: must be 0 (reserved). */
+};
+#endif
+
+/* flags */
+#define PICO_CSUM_F_WRITE 0x1u  /* store short_be(ret) into the frame's crc field (in place, device memory) */
+#define PICO_CSUM_F_TX    0x2u  /* IPV4 batch: compute (TX) mode -- crc fields read as zero */
+
+/* IPV4 batch verdict byte */
+#define PICO_CSUM_V_ACCEPT    1u  /* frame passes every check the reference makes */
+#define PICO_CSUM_V_NET_BAD   2u  /* pico_ipv4_crc_check would discard (pico_ipv4.c:249-253) */
+#define PICO_CSUM_V_L4_BAD    4u  /* pico_transport_crc_check would discard (pico_socket.c:1929,1953) */
+#define PICO_CSUM_V_MALFORMED 8u  /* infeasible length (pico_ipv4.c:402-405) or a region past the buffer */
+
+/* ---------------------------------------------------------------- layer 1 */
+
+/* ref: stack/pico_frame.c:312-318 */
+uint16_t pico_checksum(void *inbuf, uint32_t len);
+/* ref: stack/pico_frame.c:320-328 (len1 must be even, as in the reference) */
+uint16_t pico_dualbuffer_checksum(void *inbuf1, uint32_t len1, void *inbuf2, uint32_t len2);
+
+/* The reference's accumulator step, exported so a caller can build a
+ * descriptor seed: ref stack/pico_frame.c:279-299 pico_checksum_adder. */
+uint32_t pico_checksum_partial(uint32_t sum, const void *buf, uint32_t len);
+/* Accumulator value of the 12-byte struct pico_ipv4_pseudo_hdr
+ * (modules/pico_ipv4.h:46-53) as pico_tcp_checksum_ipv4 / pico_udp_checksum_ipv4
+ * build it (pico_tcp.c:428-443, pico_udp.c:42-57).  src/dst as stored in
+ * struct pico_ip4 (network byte order). */
+uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t proto, uint16_t transport_len);
+
+/* ---------------------------------------------------------------- layer 2 */
+
+/* Batch of pico_checksum / pico_dualbuffer_checksum calls:
+ *   d_out[i] = finalize(adder(desc[i].seed, d_base + desc[i].off, desc[i].len))
+ * crc_off >= 0 (even): the 2 bytes at off+crc_off read as zero when they lie
+ * inside the region ("hdr->crc = 0" before computing: pico_ipv4.c:237,
+ * pico_icmp4.c:38, pico_tcp.c:980); with PICO_CSUM_F_WRITE the result is
+ * stored there (pico_ipv4.c:238, pico_icmp4.c:39, pico_tcp.c:981).
+ * crc_off < 0: no crc field.  Regions may not overlap when F_WRITE is set. */
+int pico_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
+                            int32_t crc_off, uint32_t flags, uint16_t *d_out, void *stream);
+
+/* Uniform batch (no descriptors): frame i = d_base + i*stride, len bytes,
+ * seed added to every frame.  The layout of a packed frame ring. */
+int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len, uint32_t n,
+                                    uint32_t seed, uint16_t *d_out, void *stream);
+
+/* Fused IPv4 header + transport batch, one IPv4 datagram per descriptor
+ * (desc.off -> IPv4 header, desc.len = bytes available).
+ * RX (flags without F_TX): the checks of pico_ipv4_process_in
+ *   (pico_ipv4.c:381-420) + pico_ipv4_crc_check (:243-257) +
+ *   pico_transport_crc_check (pico_socket.c:1916-1968): TCP always, UDP when
+ *   its crc field != 0, pseudo header from the IP header.
+ *   d_out_net = pico_checksum(hdr, net_len), d_out_transport = the TCP/UDP
+ *   checksum (0 = valid; 0 when none is computed), d_verdict = PICO_CSUM_V_*.
+ * TX (F_TX): crc fields read as zero; d_out_* are the values to store
+ *   (IPv4 header; TCP with pseudo header; ICMPv4 without; UDP 0 as
+ *   pico_udp.c:123).  F_WRITE stores them into accepted frames in place.
+ * Any output pointer may be NULL. */
+int pico_ipv4_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
+                                 uint32_t flags, uint16_t *d_out_net, uint16_t *d_out_transport,
+                                 uint8_t *d_verdict, void *stream);
+
+/* ---------------------------------------------------------------- layer 3 */
+
+struct pico_csum_ctx;   /* device, two streams, double-buffered staging */
+
+struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes);
+void pico_csum_ctx_destroy(struct pico_csum_ctx *ctx);
+
+/* Host-resident uniform batch: frames in host memory (pinned for full PCIe
+ * rate, see pico_csum_host_register), results to host memory; returns when
+ * d2h of every result has completed. */
+int pico_checksum_batch_uniform_host(struct pico_csum_ctx *ctx, const void *base, uint64_t stride,
+                                     uint32_t len, uint32_t n, uint32_t seed, uint16_t *out);
+int pico_csum_host_register(void *ptr, uint64_t bytes);
+int pico_csum_host_unregister(void *ptr);
+
+/* ---------------------------------------------------------------- misc */
+
+int pico_csum_abi_version(void);
+const char *pico_csum_last_error(void);   /* thread-local, "" when none */
+
+/* Launch-shape override for tests and bench sweeps (0 = automatic choice).
+ * group = lanes per frame (4..64, power of 2), cpl = 16-byte chunks per lane
+ * per pass (1,2,4,8), fpw = frames per wave (multiple of 64/group, <= 64). */
+int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t fpw);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PICO_CSUM_H */

@@ -1,0 +1,163 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes access to the CPU oracle.
+
+  liboracle.so       -- C restatement (oracle/pico_csum_oracle.c), the checker.
+  _ref/libpicoref.so -- the reference's own stack/pico_frame.c compiled from
+                        /root/reference by oracle/Makefile (present here and,
+                        prebuilt, on the GPU box).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product (picotcp_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libpicoref.so")
+REF_OS_SO = os.path.join(HERE, "_ref", "libpicoref_Os.so")
+
+DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+ORACLE_IPV4_TX = 1
+
+_vp = ctypes.c_void_p
+_u16, _u32, _u64, _i32 = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+
+
+def build() -> None:
+    """Compile liboracle.so (and oracle/_ref when /root/reference is present)."""
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+    if os.path.isdir("/root/reference/stack"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+_olib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _olib
+    if _olib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = ctypes.CDLL(ORACLE_SO)
+        L.oracle_checksum_adder.restype = _u32
+        L.oracle_checksum_adder.argtypes = [_u32, _vp, _u32]
+        L.oracle_checksum_finalize.restype = _u16
+        L.oracle_checksum_finalize.argtypes = [_u32]
+        L.oracle_checksum.restype = _u16
+        L.oracle_checksum.argtypes = [_vp, _u32]
+        L.oracle_dualbuffer_checksum.restype = _u16
+        L.oracle_dualbuffer_checksum.argtypes = [_vp, _u32, _vp, _u32]
+        L.oracle_ipv4_pseudo_sum.restype = _u32
+        L.oracle_ipv4_pseudo_sum.argtypes = [_vp, _vp, ctypes.c_uint8, ctypes.c_uint16]
+        L.oracle_batch_raw.restype = None
+        L.oracle_batch_raw.argtypes = [_vp, _vp, _u32, _vp, _i32]
+        L.oracle_batch_uniform.restype = None
+        L.oracle_batch_uniform.argtypes = [_vp, _u64, _u32, _u32, _u32, _vp]
+        L.oracle_batch_ipv4.restype = None
+        L.oracle_batch_ipv4.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _u32]
+        L.oracle_uniform_mt.restype = ctypes.c_double
+        L.oracle_uniform_mt.argtypes = [_vp, _vp, _u64, _u32, _u32, _vp, _u32]
+        _olib = L
+    return _olib
+
+
+def _p(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _buf(b) -> np.ndarray:
+    return np.ascontiguousarray(np.frombuffer(bytes(b), dtype=np.uint8) if isinstance(b, (bytes, bytearray))
+                                else b, dtype=np.uint8)
+
+
+def checksum(b) -> int:
+    a = _buf(b)
+    return lib().oracle_checksum(_p(a), a.size)
+
+
+def dualbuffer_checksum(b1, b2) -> int:
+    a1, a2 = _buf(b1), _buf(b2)
+    return lib().oracle_dualbuffer_checksum(_p(a1), a1.size, _p(a2), a2.size)
+
+
+def adder(s: int, b) -> int:
+    a = _buf(b)
+    return lib().oracle_checksum_adder(s & 0xFFFFFFFF, _p(a), a.size)
+
+
+def ipv4_pseudo_sum(src: bytes, dst: bytes, proto: int, tl: int) -> int:
+    s, d = _buf(src), _buf(dst)
+    return lib().oracle_ipv4_pseudo_sum(_p(s), _p(d), proto, tl)
+
+
+def batch_raw(base: np.ndarray, desc: np.ndarray, crc_off: int = -1) -> np.ndarray:
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    out = np.zeros(desc.shape[0], dtype=np.uint16)
+    lib().oracle_batch_raw(_p(base), _p(desc), desc.shape[0], _p(out), crc_off)
+    return out
+
+
+def batch_uniform(base: np.ndarray, stride: int, length: int, n: int, seed: int = 0) -> np.ndarray:
+    out = np.zeros(n, dtype=np.uint16)
+    lib().oracle_batch_uniform(_p(base), stride, length, n, seed & 0xFFFFFFFF, _p(out))
+    return out
+
+
+def batch_ipv4(base: np.ndarray, desc: np.ndarray, tx: bool = False):
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    n = desc.shape[0]
+    on, ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8)
+    lib().oracle_batch_ipv4(_p(base), _p(desc), n, _p(on), _p(ol), _p(v), ORACLE_IPV4_TX if tx else 0)
+    return on, ol, v
+
+
+# ---------------------------------------------------------------- reference
+
+_rlibs: dict = {}
+
+
+def ref_available(os_flags: bool = False) -> bool:
+    return os.path.exists(REF_OS_SO if os_flags else REF_SO)
+
+
+def ref_lib(os_flags: bool = False) -> ctypes.CDLL:
+    path = REF_OS_SO if os_flags else REF_SO
+    if path not in _rlibs:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle ref` where /root/reference exists")
+        L = ctypes.CDLL(path)
+        L.pico_checksum.restype = _u16
+        L.pico_checksum.argtypes = [_vp, _u32]
+        L.pico_dualbuffer_checksum.restype = _u16
+        L.pico_dualbuffer_checksum.argtypes = [_vp, _u32, _vp, _u32]
+        _rlibs[path] = L
+    return _rlibs[path]
+
+
+def ref_checksum(b) -> int:
+    a = _buf(b)
+    return ref_lib().pico_checksum(_p(a), a.size)
+
+
+def ref_dualbuffer_checksum(b1, b2) -> int:
+    a1, a2 = _buf(b1), _buf(b2)
+    return ref_lib().pico_dualbuffer_checksum(_p(a1), a1.size, _p(a2), a2.size)
+
+
+def uniform_mt(base: np.ndarray, stride: int, length: int, n: int, nthreads: int,
+               kind: str = "reference", os_flags: bool = False):
+    """Time `n` uniform frames through pico_checksum on `nthreads` pthreads.
+    kind="reference": the compiled reference pico_frame.c; "port": the restatement.
+    Returns (seconds, out)."""
+    out = np.zeros(n, dtype=np.uint16)
+    if kind == "reference":
+        fn = ctypes.cast(ref_lib(os_flags).pico_checksum, ctypes.c_void_p)
+    else:
+        fn = ctypes.cast(lib().oracle_checksum, ctypes.c_void_p)
+    secs = lib().oracle_uniform_mt(fn, _p(base), stride, length, n, _p(out), nthreads)
+    return secs, out

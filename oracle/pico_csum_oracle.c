@@ -1,0 +1,271 @@
+/*
+ * pico_csum_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of picoTCP's Internet-checksum path, used as the parity
+ * checker (tests/, __graft_entry__.smoke()) and as the CPU baseline leg of
+ * bench.py.  Nothing in the product library (picotcp_amd/) links, loads or
+ * calls this file; the product's batched path is the HIP kernel and it fails
+ * loudly when that is unavailable.
+ *
+ * Parity is PINNED: every function below is checked bit-for-bit against
+ * (1) oracle/_ref/libpicoref.so, built by oracle/Makefile from the unmodified
+ *     reference source /root/reference/stack/pico_frame.c, and
+ * (2) the golden vectors in tests/golden/ (reference KATs from
+ *     test/unit/unit_socket.c:418-435, test/unit/unit_icmp4.c:225-230 and
+ *     RFC/rfc1071.txt:246-268, plus seeded random frames whose expected
+ *     outputs were produced by oracle/_ref).
+ *
+ * Semantics restated (little-endian host, the reference's default build):
+ *   S   = sum over i < floor(n/2) of (b[2i] | b[2i+1] << 8)  + (n odd ? b[n-1] : 0)
+ *   s   = S mod 2^32            (uint32_t accumulator, no carry fold in the loop)
+ *   fold s to 16 bits with end-around carry, complement, byte-swap.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+
+#include "pico_csum_oracle.h"
+
+/* stack/pico_frame.c:279-299 pico_checksum_adder (LE branch at :289). */
+uint32_t oracle_checksum_adder(uint32_t sum, const void *data, uint32_t len)
+{
+    const uint8_t *p = (const uint8_t *)data;
+    uint32_t i;
+
+    if (len & 1u) {
+        --len;
+        sum += p[len];                      /* odd trailing byte is the LOW byte */
+    }
+    for (i = 0; i < len; i += 2) {
+        uint16_t w;
+        memcpy(&w, p + i, 2);               /* native (LE) 16-bit word, any alignment */
+        sum += w;                           /* uint32 wrap, as the reference */
+    }
+    return sum;
+}
+
+/* stack/pico_frame.c:301-307 pico_checksum_finalize; short_be = bswap16
+ * (include/pico_config.h:156-159). */
+uint16_t oracle_checksum_finalize(uint32_t sum)
+{
+    uint16_t r;
+    while (sum >> 16)
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+    r = (uint16_t)~sum;
+    return (uint16_t)((r >> 8) | (r << 8));
+}
+
+/* stack/pico_frame.c:312-318 */
+uint16_t oracle_checksum(const void *buf, uint32_t len)
+{
+    return oracle_checksum_finalize(oracle_checksum_adder(0, buf, len));
+}
+
+/* stack/pico_frame.c:320-328 */
+uint16_t oracle_dualbuffer_checksum(const void *b1, uint32_t len1, const void *b2, uint32_t len2)
+{
+    uint32_t sum = oracle_checksum_adder(0, b1, len1);
+    sum = oracle_checksum_adder(sum, b2, len2);
+    return oracle_checksum_finalize(sum);
+}
+
+/* modules/pico_ipv4.h:46-53 pseudo header {src, dst, zeros, proto, len_be}
+ * summed by pico_checksum_adder, i.e. as it would be in
+ * pico_tcp.c:422-446 / pico_udp.c:36-60 (the 12-byte buffer 1 of
+ * pico_dualbuffer_checksum). src/dst are in network byte order as stored. */
+uint32_t oracle_ipv4_pseudo_sum(const uint8_t src[4], const uint8_t dst[4], uint8_t proto, uint16_t transport_len)
+{
+    uint8_t ph[12];
+    memcpy(ph, src, 4);
+    memcpy(ph + 4, dst, 4);
+    ph[8] = 0;
+    ph[9] = proto;
+    ph[10] = (uint8_t)(transport_len >> 8);   /* short_be(transport_len) stored LE */
+    ph[11] = (uint8_t)(transport_len & 0xFF);
+    return oracle_checksum_adder(0, ph, 12);
+}
+
+/* Batched restatement of the RAW path: out[i] = finalize(adder(seed_i, base+off_i, len_i)).
+ * crc_off >= 0: the two bytes at off_i+crc_off are read as zero (the
+ * "hdr->crc = 0" the callers do before computing: pico_ipv4.c:237,
+ * pico_icmp4.c:38, pico_tcp.c:980). */
+void oracle_batch_raw(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                      uint16_t *out, int32_t crc_off)
+{
+    uint32_t i;
+    for (i = 0; i < n; i++) {
+        const uint8_t *p = base + d[i].off;
+        uint32_t len = d[i].len;
+        uint32_t sum = oracle_checksum_adder(d[i].seed, p, len);
+        if (crc_off >= 0 && (uint32_t)crc_off + 2u <= len) {
+            uint16_t w;                     /* crc_off is even (API contract) */
+            memcpy(&w, p + crc_off, 2);
+            sum -= w;
+        }
+        out[i] = oracle_checksum_finalize(sum);
+    }
+}
+
+void oracle_batch_uniform(const uint8_t *base, uint64_t stride, uint32_t len, uint32_t n,
+                          uint32_t seed, uint16_t *out)
+{
+    uint32_t i;
+    for (i = 0; i < n; i++)
+        out[i] = oracle_checksum_finalize(oracle_checksum_adder(seed, base + (uint64_t)i * stride, len));
+}
+
+/*
+ * Fused IPv4 RX/TX restatement, one frame per descriptor.  desc.off points at
+ * the IPv4 header (f->net_hdr); desc.len = bytes available from net_hdr to the
+ * end of the frame buffer (f->buffer_len - (f->net_hdr - f->buffer)).
+ *
+ * RX (flags & ORACLE_IPV4_TX == 0):
+ *   lengths + feasibility bound   pico_ipv4_process_in  modules/pico_ipv4.c:381-405
+ *   header check                  pico_ipv4_crc_check   modules/pico_ipv4.c:243-257
+ *   transport check               pico_transport_crc_check stack/pico_socket.c:1916-1968
+ *     TCP: pico_tcp_checksum_ipv4 modules/pico_tcp.c:422-446 (pseudo from IP hdr, f->sock NULL)
+ *     UDP: only when the stored crc != 0 (pico_socket.c:1941), pico_udp.c:36-60
+ *   out_net = pico_checksum(hdr, net_len)                        (0 when valid)
+ *   out_l4  = transport checksum with the IPv4 pseudo header       (0 when valid;
+ *             0 when the reference computes none)
+ *   verdict = PICO_CSUM_V_ACCEPT, or the OR of the failure bits.
+ *   Frames where the reference would read past desc.len (header or
+ *   transport beyond the buffer: reference UB) are PICO_CSUM_V_MALFORMED.
+ * TX (ORACLE_IPV4_TX): the header is complete; crc fields read as zero
+ *   (hdr->crc = 0 at pico_ipv4.c:237, pico_tcp.c:980, pico_icmp4.c:38); out_*
+ *   are the values the reference stores with short_be() (pico_ipv4.c:238,
+ *   pico_tcp.c:981, pico_icmp4.c:39).  UDP over IPv4 sends crc 0
+ *   (pico_udp.c:123); other protocols get none.  TCP needs a 20-byte and ICMP
+ *   an 8-byte header inside transport_len, else MALFORMED.
+ */
+void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                       uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
+{
+    uint32_t i;
+    int tx = (flags & ORACLE_IPV4_TX) != 0;
+    for (i = 0; i < n; i++) {
+        const uint8_t *h = base + d[i].off;
+        const uint8_t *t;
+        uint32_t avail = d[i].len;
+        uint32_t option_len = 0, net_len, s;
+        uint16_t tot, transport_len, max_allowed;
+        uint16_t net_cs, l4_cs = 0;
+        uint8_t proto, v = 0;
+
+        out_net[i] = 0; out_l4[i] = 0; verdict[i] = PICO_CSUM_V_MALFORMED;
+        if (avail < 20)
+            continue;
+        if ((h[0] & 0x0F) > 5)
+            option_len = 4u * ((h[0] & 0x0Fu) - 5u);
+        net_len = 20u + option_len;
+        proto = h[9];
+        tot = (uint16_t)((h[2] << 8) | h[3]);
+        transport_len = (uint16_t)(tot - 20u - option_len);    /* uint16 wrap as :395 */
+        max_allowed = (uint16_t)(avail - 20u);                 /* :386 */
+        if (net_len > avail)
+            continue;
+        if (!tx && transport_len > max_allowed)                /* :402-405 discard */
+            continue;
+        if (net_len + (uint32_t)transport_len > avail)         /* reference would overread */
+            continue;
+        t = h + net_len;
+
+        s = oracle_checksum_adder(0, h, net_len);
+        if (tx) s -= (uint32_t)(h[10] | (h[11] << 8));
+        net_cs = oracle_checksum_finalize(s);
+        if (!tx && net_cs != 0)
+            v |= PICO_CSUM_V_NET_BAD;
+
+        if (!tx) {
+            if (proto == 6 || proto == 17) {
+                int check = 1;
+                if (proto == 17) {
+                    if (net_len + 8u > avail) { v |= PICO_CSUM_V_MALFORMED; check = 0; }
+                    else if (t[6] == 0 && t[7] == 0) check = 0;
+                }
+                if (check) {
+                    s = oracle_ipv4_pseudo_sum(h + 12, h + 16, proto, transport_len);
+                    l4_cs = oracle_checksum_finalize(oracle_checksum_adder(s, t, transport_len));
+                    if (l4_cs != 0)
+                        v |= PICO_CSUM_V_L4_BAD;
+                }
+            }
+        } else {
+            if (proto == 6) {
+                if (transport_len < 20) { v |= PICO_CSUM_V_MALFORMED; }
+                else {
+                    s = oracle_ipv4_pseudo_sum(h + 12, h + 16, proto, transport_len);
+                    s = oracle_checksum_adder(s, t, transport_len);
+                    s -= (uint32_t)(t[16] | (t[17] << 8));
+                    l4_cs = oracle_checksum_finalize(s);
+                }
+            } else if (proto == 1) {
+                if (transport_len < 8) { v |= PICO_CSUM_V_MALFORMED; }
+                else {
+                    s = oracle_checksum_adder(0, t, transport_len);
+                    s -= (uint32_t)(t[2] | (t[3] << 8));
+                    l4_cs = oracle_checksum_finalize(s);
+                }
+            }
+        }
+        out_net[i] = net_cs;
+        out_l4[i] = l4_cs;
+        verdict[i] = (uint8_t)(v == 0 ? PICO_CSUM_V_ACCEPT : v);
+    }
+}
+
+/* ---- multi-threaded CPU baseline driver (bench.py cpu_baseline leg) ---- */
+
+struct mt_job {
+    const uint8_t *base;
+    uint64_t stride;
+    uint32_t len, first, count;
+    uint16_t *out;
+    oracle_checksum_fn fn;
+};
+
+static void *mt_worker(void *arg)
+{
+    struct mt_job *j = (struct mt_job *)arg;
+    uint32_t i;
+    for (i = 0; i < j->count; i++) {
+        uint64_t f = (uint64_t)j->first + i;
+        j->out[f] = j->fn((void *)(j->base + f * j->stride), j->len);
+    }
+    return NULL;
+}
+
+/* Runs fn (oracle_checksum, or the reference's own pico_checksum from
+ * oracle/_ref) over n uniform frames on nthreads pthreads, contiguous frame
+ * ranges per thread.  Returns wall seconds. */
+double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
+                         uint32_t n, uint16_t *out, uint32_t nthreads)
+{
+    struct mt_job jobs[256];
+    pthread_t th[256];
+    struct timespec t0, t1;
+    uint32_t t, per, first = 0;
+
+    if (fn == NULL) fn = (oracle_checksum_fn)oracle_checksum;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    per = (n + nthreads - 1) / nthreads;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (t = 0; t < nthreads; t++) {
+        uint32_t c = (first + per <= n) ? per : (n > first ? n - first : 0);
+        jobs[t].base = base; jobs[t].stride = stride; jobs[t].len = len;
+        jobs[t].first = first; jobs[t].count = c; jobs[t].out = out; jobs[t].fn = fn;
+        first += c;
+        if (nthreads == 1)
+            mt_worker(&jobs[t]);
+        else
+            pthread_create(&th[t], NULL, mt_worker, &jobs[t]);
+    }
+    if (nthreads > 1)
+        for (t = 0; t < nthreads; t++)
+            pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,38 @@
+/* TEST INFRASTRUCTURE ONLY -- see pico_csum_oracle.c.  Never linked into the product. */
+#ifndef PICO_CSUM_ORACLE_H
+#define PICO_CSUM_ORACLE_H
+#include <stdint.h>
+
+#ifndef PICO_CSUM_DESC_DEFINED
+#define PICO_CSUM_DESC_DEFINED
+/* Same 16-byte layout as include/pico_csum.h (kept separate on purpose). */
+struct pico_csum_desc {
+    uint64_t off;
+    uint32_t len;
+    uint32_t seed;
+};
+#endif
+
+#define PICO_CSUM_V_ACCEPT    1u
+#define PICO_CSUM_V_NET_BAD   2u
+#define PICO_CSUM_V_L4_BAD    4u
+#define PICO_CSUM_V_MALFORMED 8u
+
+#define ORACLE_IPV4_TX 1u
+
+typedef uint16_t (*oracle_checksum_fn)(void *buf, uint32_t len);
+
+uint32_t oracle_checksum_adder(uint32_t sum, const void *data, uint32_t len);
+uint16_t oracle_checksum_finalize(uint32_t sum);
+uint16_t oracle_checksum(const void *buf, uint32_t len);
+uint16_t oracle_dualbuffer_checksum(const void *b1, uint32_t len1, const void *b2, uint32_t len2);
+uint32_t oracle_ipv4_pseudo_sum(const uint8_t src[4], const uint8_t dst[4], uint8_t proto, uint16_t transport_len);
+void oracle_batch_raw(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                      uint16_t *out, int32_t crc_off);
+void oracle_batch_uniform(const uint8_t *base, uint64_t stride, uint32_t len, uint32_t n,
+                          uint32_t seed, uint16_t *out);
+void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                       uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
+double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
+                         uint32_t n, uint16_t *out, uint32_t nthreads);
+#endif

@@ -1,0 +1,92 @@
+"""ctypes binding of libpicocsum.so (include/pico_csum.h).
+
+The shared library is the product: a C-ABI drop-in for picoTCP's checksum path
+whose batched entry points run HIP kernels on gfx950.  This module only loads
+it and declares argument types.  There is no Python or CPU fallback for the
+batched path: if the library is missing, importing the batch helpers raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpicocsum.so")
+
+# Public symbols declared by include/pico_csum.h (checked by tests/test_abi.py).
+EXPORTED = (
+    "pico_checksum",
+    "pico_dualbuffer_checksum",
+    "pico_checksum_partial",
+    "pico_ipv4_pseudo_partial",
+    "pico_checksum_batch_dev",
+    "pico_checksum_batch_uniform_dev",
+    "pico_ipv4_checksum_batch_dev",
+    "pico_csum_ctx_create",
+    "pico_csum_ctx_destroy",
+    "pico_checksum_batch_uniform_host",
+    "pico_csum_host_register",
+    "pico_csum_host_unregister",
+    "pico_csum_abi_version",
+    "pico_csum_last_error",
+    "pico_csum_set_launch_override",
+)
+
+F_WRITE = 0x1
+F_TX = 0x2
+V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED = 1, 2, 4, 8
+EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12
+
+
+class PicoCsumError(RuntimeError):
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed ({rc}): {msg}")
+        self.rc = rc
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libpicocsum.so once; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make -C picotcp_amd/csrc` "
+            "(or __graft_entry__.build()); the batched checksum path has no fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.c_void_p
+    vp = ctypes.c_void_p
+    u16, u32, u64, i32 = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+
+    def sig(name, res, *args):
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = list(args)
+
+    sig("pico_checksum", u16, vp, u32)
+    sig("pico_dualbuffer_checksum", u16, vp, u32, vp, u32)
+    sig("pico_checksum_partial", u32, u32, vp, u32)
+    sig("pico_ipv4_pseudo_partial", u32, u32, u32, ctypes.c_uint8, ctypes.c_uint16)
+    sig("pico_checksum_batch_dev", ctypes.c_int, vp, vp, u32, i32, u32, vp, vp)
+    sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u32, u32, u32, vp, vp)
+    sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, vp, u32, u32, vp, vp, vp, vp)
+    sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
+    sig("pico_csum_ctx_destroy", None, vp)
+    sig("pico_checksum_batch_uniform_host", ctypes.c_int, vp, vp, u64, u32, u32, u32, vp)
+    sig("pico_csum_host_register", ctypes.c_int, vp, u64)
+    sig("pico_csum_host_unregister", ctypes.c_int, vp)
+    sig("pico_csum_abi_version", ctypes.c_int)
+    sig("pico_csum_last_error", ctypes.c_char_p)
+    sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32)
+    del u8p
+    _lib = lib
+    return lib
+
+
+def check(fn: str, rc: int) -> None:
+    if rc != 0:
+        msg = load().pico_csum_last_error().decode(errors="replace")
+        raise PicoCsumError(fn, rc, msg)

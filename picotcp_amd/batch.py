@@ -1,0 +1,157 @@
+"""Host-side (Python) mirror of the batched checksum API over torch device tensors.
+
+Each function is a thin call into libpicocsum.so (include/pico_csum.h); the
+work happens in the HIP kernels.  Frame buffers are uint8 tensors on a HIP
+device; descriptor arrays are uint8 tensors of n*16 bytes (struct
+pico_csum_desc); results are int16 tensors holding the uint16 checksum bits
+(view them as uint16 with `.cpu().numpy().view(np.uint16)`).
+
+Reference interfaces mirrored (per frame in the reference, per batch here):
+  checksum_uniform / checksum_batch  <- pico_checksum, pico_dualbuffer_checksum
+                                        (stack/pico_frame.c:312-328)
+  ipv4_checksum_batch                <- pico_ipv4_checksum / pico_ipv4_crc_check
+                                        (modules/pico_ipv4.c:231-257),
+                                        pico_tcp_checksum_ipv4 (pico_tcp.c:422),
+                                        pico_udp_checksum_ipv4 (pico_udp.c:36),
+                                        pico_icmp4_checksum (pico_icmp4.c:30),
+                                        pico_transport_crc_check (pico_socket.c:1916)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import F_TX, F_WRITE, V_ACCEPT, V_L4_BAD, V_MALFORMED, V_NET_BAD  # noqa: F401
+
+DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+assert DESC_DTYPE.itemsize == 16
+
+
+def make_desc(offsets, lengths, seeds=None) -> np.ndarray:
+    """Host descriptor array (struct pico_csum_desc[n])."""
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    d = np.zeros(offsets.shape[0], dtype=DESC_DTYPE)
+    d["off"] = offsets
+    d["len"] = np.asarray(lengths, dtype=np.uint32)
+    if seeds is not None:
+        d["seed"] = np.asarray(seeds, dtype=np.uint32)
+    return d
+
+
+def desc_to_device(desc: np.ndarray, device) -> torch.Tensor:
+    """Copy a descriptor array to the device (fresh allocation: 16-B aligned)."""
+    raw = np.ascontiguousarray(desc).view(np.uint8).reshape(-1)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def _stream_handle(stream) -> ctypes.c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def _require_device(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor (the batched path is GPU-only)")
+
+
+def checksum_uniform(base: torch.Tensor, stride: int, length: int, n: int, seed: int = 0,
+                     out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """out[i] = pico_checksum(base + i*stride, length) (+ seed as pico_dualbuffer_checksum's
+    first buffer); device-resident, asynchronous on `stream`."""
+    _require_device(base, "base")
+    if n and (n - 1) * stride + length > base.numel():
+        raise ValueError("frames exceed the base tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=base.device)
+    lib = _lib.load()
+    _lib.check("pico_checksum_batch_uniform_dev",
+               lib.pico_checksum_batch_uniform_dev(_ptr(base), stride, length, n, seed & 0xFFFFFFFF,
+                                                   _ptr(out), _stream_handle(stream)))
+    return out
+
+
+def checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, crc_off: int = -1, flags: int = 0,
+                   out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """out[i] = finalize(adder(desc[i].seed, base + desc[i].off, desc[i].len)); crc field
+    at crc_off read as zero (and written with F_WRITE)."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=base.device)
+    lib = _lib.load()
+    _lib.check("pico_checksum_batch_dev",
+               lib.pico_checksum_batch_dev(_ptr(base), _ptr(desc), n, crc_off, flags, _ptr(out),
+                                           _stream_handle(stream)))
+    return out
+
+
+def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None):
+    """Fused IPv4 header + transport checksums (RX verify, or TX compute with F_TX).
+    Returns (out_net int16[n], out_transport int16[n], verdict uint8[n])."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    dev = base.device
+    out_net = torch.empty(n, dtype=torch.int16, device=dev)
+    out_l4 = torch.empty(n, dtype=torch.int16, device=dev)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    lib = _lib.load()
+    _lib.check("pico_ipv4_checksum_batch_dev",
+               lib.pico_ipv4_checksum_batch_dev(_ptr(base), _ptr(desc), n, flags, _ptr(out_net),
+                                                _ptr(out_l4), _ptr(verdict), _stream_handle(stream)))
+    return out_net, out_l4, verdict
+
+
+def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0) -> None:
+    """Force a kernel launch shape (tests / bench sweeps); all zero = automatic."""
+    _lib.check("pico_csum_set_launch_override", _lib.load().pico_csum_set_launch_override(group, cpl, fpw))
+
+
+class HostBatch:
+    """Host-resident batches through pico_checksum_batch_uniform_host: H2D, kernel and D2H
+    chunked over two streams (staging_bytes per chunk)."""
+
+    def __init__(self, device: int = 0, staging_bytes: int = 64 << 20):
+        self._lib = _lib.load()
+        self._ctx = self._lib.pico_csum_ctx_create(device, staging_bytes)
+        if not self._ctx:
+            raise _lib.PicoCsumError("pico_csum_ctx_create", -1,
+                                     self._lib.pico_csum_last_error().decode(errors="replace"))
+
+    def checksum_uniform(self, frames: np.ndarray | torch.Tensor, stride: int, length: int, n: int,
+                         seed: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+        if out is None:
+            out = np.empty(n, dtype=np.uint16)
+        if isinstance(frames, torch.Tensor):
+            if frames.is_cuda:
+                raise ValueError("HostBatch takes host memory")
+            src = frames.data_ptr()
+        else:
+            src = frames.ctypes.data
+        _lib.check("pico_checksum_batch_uniform_host",
+                   self._lib.pico_checksum_batch_uniform_host(self._ctx, ctypes.c_void_p(src), stride, length, n,
+                                                              seed & 0xFFFFFFFF,
+                                                              ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.pico_csum_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

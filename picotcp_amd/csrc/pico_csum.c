@@ -1,0 +1,367 @@
+/*
+ * pico_csum.c -- host side of libpicocsum, plain C (C99).
+ *
+ * Layer 1: the drop-in scalar symbols pico_checksum / pico_dualbuffer_checksum
+ *          (ref stack/pico_frame.c:279-328) -- synchronous host code, the
+ *          reference calls them inline per frame (see include/pico_csum.h).
+ * Layer 2: argument checking + launch-shape choice for the batched HIP
+ *          kernels (picotcp_amd/csrc/pico_csum_kernels.hip), reached through
+ *          the thin extern "C" launchers declared below.
+ * Layer 3: host-resident batches: pinned staging, two streams, chunked
+ *          H2D -> kernel -> D2H overlap.
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "pico_csum.h"
+
+/* kernels TU (C++/HIP), extern "C" */
+int pico_csum_launch_raw(void *base, const void *desc, uint64_t stride, uint32_t len, uint32_t n,
+                         uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
+                         uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void *stream);
+int pico_csum_launch_ipv4(void *base, const void *desc, uint32_t n, uint32_t flags, uint16_t *out_net,
+                          uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
+                          void *stream);
+
+/* ------------------------------------------------------------------ errors */
+
+static __thread char g_err[256];
+
+static int fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return -code;
+}
+
+const char *pico_csum_last_error(void) { return g_err; }
+int pico_csum_abi_version(void) { return PICO_CSUM_ABI_VERSION; }
+
+/* ------------------------------------------------------------------ layer 1 */
+
+/* Exact S = sum of LE 16-bit words (+ odd trailing byte as the low byte),
+ * 4 words per 8-byte load into a 64-bit accumulator; the caller reduces it
+ * mod 2^32 exactly as the reference's uint32_t accumulator does. */
+static uint64_t word_sum(const uint8_t *p, uint32_t len)
+{
+    uint64_t s = 0;
+    uint32_t i = 0;
+    for (; i + 8 <= len; i += 8) {
+        uint64_t x;
+        memcpy(&x, p + i, 8);
+        s += (x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu) + (x >> 48);
+    }
+    for (; i + 2 <= len; i += 2) {
+        uint16_t w;
+        memcpy(&w, p + i, 2);
+        s += w;
+    }
+    if (len & 1u)
+        s += p[len - 1];
+    return s;
+}
+
+uint32_t pico_checksum_partial(uint32_t sum, const void *buf, uint32_t len)
+{
+    if (len == 0)
+        return sum;
+    return (uint32_t)(sum + word_sum((const uint8_t *)buf, len));
+}
+
+static uint16_t finalize(uint32_t sum)
+{
+    uint16_t c;
+    while (sum >> 16)
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+    c = (uint16_t)~sum;
+    return (uint16_t)((c >> 8) | (c << 8));
+}
+
+uint16_t pico_checksum(void *inbuf, uint32_t len)
+{
+    return finalize(pico_checksum_partial(0, inbuf, len));
+}
+
+uint16_t pico_dualbuffer_checksum(void *inbuf1, uint32_t len1, void *inbuf2, uint32_t len2)
+{
+    return finalize(pico_checksum_partial(pico_checksum_partial(0, inbuf1, len1), inbuf2, len2));
+}
+
+uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t proto, uint16_t transport_len)
+{
+    /* struct pico_ipv4_pseudo_hdr bytes: src(4) dst(4) 0 proto len_be(2) as LE words */
+    uint32_t s = 0;
+    s += (src_addr & 0xFFFFu) + (src_addr >> 16);
+    s += (dst_addr & 0xFFFFu) + (dst_addr >> 16);
+    s += (uint32_t)proto << 8;
+    s += (uint32_t)(uint16_t)((transport_len >> 8) | (transport_len << 8));
+    return s;
+}
+
+/* ------------------------------------------------------------------ layer 2 */
+
+static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_fpw;
+
+int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t fpw)
+{
+    if (group == 0 && cpl == 0 && fpw == 0) {
+        g_ovr_group = g_ovr_cpl = g_ovr_fpw = 0;
+        return 0;
+    }
+    if (!(group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
+        return fail(PICO_CSUM_EINVAL, "group must be 4, 8, 16, 32 or 64");
+    if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
+        return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
+    if (fpw == 0 || fpw > 64 || fpw % (64 / group) != 0)
+        return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
+    g_ovr_group = group; g_ovr_cpl = cpl; g_ovr_fpw = fpw;
+    return 0;
+}
+
+struct shape { uint32_t G, CPL, fpw; };
+
+/* Frames per wave: keep >= ~8192 waves (32 per CU on 256 CUs) in the grid
+ * when the batch allows, at most 64 (one coalesced result store per wave). */
+static uint32_t pick_fpw(uint32_t n, uint32_t G)
+{
+    uint32_t ng = 64u / G, f = n / 8192u;
+    if (f > 64u) f = 64u;
+    f -= f % ng;
+    if (f < ng) f = ng;
+    return f;
+}
+
+static struct shape pick_shape(uint32_t n, uint32_t typical_len)
+{
+    struct shape s;
+    uint32_t chunks = typical_len / 16u + 1u, cpl;
+    if (g_ovr_group) {
+        s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.fpw = g_ovr_fpw;
+        return s;
+    }
+    s.G = chunks >= 48 ? 64 : chunks >= 24 ? 32 : chunks >= 12 ? 16 : chunks >= 6 ? 8 : 4;
+    cpl = (chunks + s.G - 1) / s.G;
+    s.CPL = cpl <= 1 ? 1 : cpl <= 2 ? 2 : cpl <= 4 ? 4 : 8;
+    s.fpw = pick_fpw(n, s.G);
+    return s;
+}
+
+static int g_dev_state; /* 0 unknown, 1 ok, -1 none */
+
+static int need_device(void)
+{
+    int count = 0;
+    if (g_dev_state == 1)
+        return 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        g_dev_state = -1;
+        return fail(PICO_CSUM_ENODEV, "no HIP device: the batched checksum path runs only on the GPU");
+    }
+    g_dev_state = 1;
+    return 0;
+}
+
+static int launch_status(int herr, const char *what)
+{
+    if (herr == (int)hipSuccess)
+        return 0;
+    if (herr == (int)hipErrorInvalidValue)
+        return fail(PICO_CSUM_EINVAL, "%s: invalid launch shape", what);
+    if (herr == (int)hipErrorNoBinaryForGpu || herr == (int)hipErrorInvalidDeviceFunction)
+        return fail(PICO_CSUM_ENODEV, "%s: no gfx950 kernel image for this device (%s)", what,
+                    hipGetErrorString((hipError_t)herr));
+    return fail(PICO_CSUM_EIO, "%s: %s", what, hipGetErrorString((hipError_t)herr));
+}
+
+/* Typical frame length for descriptor batches (unknown on the host without a
+ * sync): tuned for the simple-IMIX mean (354 B) .. MTU range. */
+#define DESC_TYPICAL_LEN 512u
+
+int pico_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
+                            int32_t crc_off, uint32_t flags, uint16_t *d_out, void *stream)
+{
+    struct shape s;
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc || !d_out)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if (crc_off >= 0 && (crc_off & 1))
+        return fail(PICO_CSUM_EINVAL, "crc_off must be even");
+    if (flags & ~PICO_CSUM_F_WRITE)
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+    if ((flags & PICO_CSUM_F_WRITE) && crc_off < 0)
+        return fail(PICO_CSUM_EINVAL, "F_WRITE needs crc_off >= 0");
+    if ((rc = need_device()) != 0)
+        return rc;
+    s = pick_shape(n, DESC_TYPICAL_LEN);
+    return launch_status(pico_csum_launch_raw(d_base, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
+                                              s.G, s.CPL, s.fpw, 0, stream), "pico_checksum_batch_dev");
+}
+
+int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len, uint32_t n,
+                                    uint32_t seed, uint16_t *d_out, void *stream)
+{
+    struct shape s;
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_out)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if ((rc = need_device()) != 0)
+        return rc;
+    s = pick_shape(n, len);
+    return launch_status(pico_csum_launch_raw((void *)d_base, NULL, stride, len, n, seed, -1, 0, d_out,
+                                              s.G, s.CPL, s.fpw, 1, stream), "pico_checksum_batch_uniform_dev");
+}
+
+int pico_ipv4_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
+                                 uint32_t flags, uint16_t *d_out_net, uint16_t *d_out_transport,
+                                 uint8_t *d_verdict, void *stream)
+{
+    struct shape s;
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+    if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
+    if ((rc = need_device()) != 0)
+        return rc;
+    s = pick_shape(n, DESC_TYPICAL_LEN);
+    return launch_status(pico_csum_launch_ipv4(d_base, d_desc, n, flags, d_out_net, d_out_transport,
+                                               d_verdict, s.G, s.CPL, s.fpw, stream),
+                         "pico_ipv4_checksum_batch_dev");
+}
+
+/* ------------------------------------------------------------------ layer 3 */
+
+/* results buffer of a staging slot: one uint16 per frame, up to this many frames per chunk */
+#define CTX_MAX_FRAMES(staging) ((staging) / 16u + 64u)
+
+struct pico_csum_ctx {
+    int device;
+    uint64_t staging;          /* bytes per staging buffer */
+    void *d_buf[2];
+    uint16_t *d_out[2];
+    hipStream_t st[2];
+    hipEvent_t done[2];
+};
+
+struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes)
+{
+    struct pico_csum_ctx *c;
+    int i;
+    if (need_device() != 0)
+        return NULL;
+    if (staging_bytes < (1u << 20))
+        staging_bytes = 1u << 20;
+    c = (struct pico_csum_ctx *)calloc(1, sizeof(*c));
+    if (!c) { fail(PICO_CSUM_ENOMEM, "ctx alloc"); return NULL; }
+    c->device = device;
+    c->staging = staging_bytes;
+    if (hipSetDevice(device) != hipSuccess) { fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", device); free(c); return NULL; }
+    for (i = 0; i < 2; i++) {
+        if (hipMalloc(&c->d_buf[i], staging_bytes) != hipSuccess ||
+            hipMalloc((void **)&c->d_out[i], 2u * CTX_MAX_FRAMES(staging_bytes)) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess) {
+            fail(PICO_CSUM_ENOMEM, "ctx device allocation (%llu B staging)", (unsigned long long)staging_bytes);
+            pico_csum_ctx_destroy(c);
+            return NULL;
+        }
+    }
+    return c;
+}
+
+void pico_csum_ctx_destroy(struct pico_csum_ctx *c)
+{
+    int i;
+    if (!c)
+        return;
+    hipSetDevice(c->device);
+    for (i = 0; i < 2; i++) {
+        if (c->st[i]) hipStreamSynchronize(c->st[i]);
+        if (c->d_buf[i]) hipFree(c->d_buf[i]);
+        if (c->d_out[i]) hipFree(c->d_out[i]);
+        if (c->done[i]) hipEventDestroy(c->done[i]);
+        if (c->st[i]) hipStreamDestroy(c->st[i]);
+    }
+    free(c);
+}
+
+int pico_csum_host_register(void *ptr, uint64_t bytes)
+{
+    hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
+    if (e != hipSuccess)
+        return fail(PICO_CSUM_EIO, "hipHostRegister: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int pico_csum_host_unregister(void *ptr)
+{
+    hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess)
+        return fail(PICO_CSUM_EIO, "hipHostUnregister: %s", hipGetErrorString(e));
+    return 0;
+}
+
+/* Frames [first, first+cnt) go into staging buffer b on stream b: H2D of the
+ * contiguous span they occupy, kernel, D2H of their results.  The two streams
+ * alternate so chunk c+1's H2D overlaps chunk c's kernel and D2H. */
+int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, uint64_t stride,
+                                     uint32_t len, uint32_t n, uint32_t seed, uint16_t *out)
+{
+    uint64_t per;
+    uint32_t first = 0;
+    int b = 0, rc = 0;
+    struct shape s;
+    if (!c || !base || !out)
+        return fail(PICO_CSUM_EINVAL, "NULL argument");
+    if (n == 0)
+        return 0;
+    if (stride < len)
+        return fail(PICO_CSUM_EINVAL, "host batch needs stride >= len (non-overlapping frames)");
+    if (stride == 0 || (uint64_t)len > c->staging)
+        return fail(PICO_CSUM_EINVAL, "frame larger than the staging buffer");
+    per = (c->staging - len) / stride + 1;
+    if (per > CTX_MAX_FRAMES(c->staging)) per = CTX_MAX_FRAMES(c->staging);
+    if (hipSetDevice(c->device) != hipSuccess)
+        return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
+    while (first < n) {
+        uint32_t cnt = (uint32_t)((n - first) < per ? (n - first) : per);
+        uint64_t bytes = (uint64_t)(cnt - 1) * stride + len;
+        const uint8_t *src = (const uint8_t *)base + (uint64_t)first * stride;
+        hipError_t e;
+        /* staging buffer b is free once its previous chunk's D2H is done (same stream: ordered) */
+        e = hipMemcpyAsync(c->d_buf[b], src, bytes, hipMemcpyHostToDevice, c->st[b]);
+        if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "H2D: %s", hipGetErrorString(e)); break; }
+        s = pick_shape(cnt, len);
+        rc = launch_status(pico_csum_launch_raw(c->d_buf[b], NULL, stride, len, cnt, seed, -1, 0,
+                                                c->d_out[b], s.G, s.CPL, s.fpw, 1, c->st[b]),
+                           "pico_checksum_batch_uniform_host");
+        if (rc) break;
+        e = hipMemcpyAsync(out + first, c->d_out[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]);
+        if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "D2H: %s", hipGetErrorString(e)); break; }
+        first += cnt;
+        b ^= 1;
+    }
+    if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
+        if (!rc) rc = fail(PICO_CSUM_EIO, "stream synchronize failed");
+    return rc;
+}

@@ -1,0 +1,454 @@
+// pico_csum_kernels.hip -- CDNA4 (gfx950) kernels for picoTCP's Internet checksum.
+//
+// What is computed (bit-exact with stack/pico_frame.c:279-328):
+//   S = sum_{i<n/2} (b[2i] | b[2i+1]<<8) + (n odd ? b[n-1] : 0)    word pairing relative to the frame start
+//   s = (seed + S) mod 2^32;  ret = bswap16(~fold16(s))
+//
+// How (DESIGN.md "Kernels"):
+//   * S = E + 256*O, E/O = sums of the bytes at even/odd offsets from the frame
+//     start.  A 16-byte-aligned chunk is loaded with one global_load_dwordx4
+//     whatever the frame's alignment; bytes outside the frame (or inside a
+//     crc field) are masked to zero; for an odd frame start v_perm_b32 swaps
+//     the bytes of each 16-bit half so the pairing is frame-relative again;
+//     v_dot2_u32_u16 (x . {1,1}) then adds both halves into a 32-bit
+//     per-lane accumulator -- exact, two VALU ops per dword.  All later
+//     additions are plain 32-bit wrapping adds, which is exactly the
+//     reference's uint32_t accumulator, so the 131076-byte wrap matches too.
+//   * A frame is owned by a lane group of G lanes (G = 4..64): lane l reads
+//     chunks l, l+G, ... (G*16 contiguous bytes per group per load), CPL
+//     chunks per lane per pass are issued back to back.  The group's partial
+//     sums are folded with DPP row ops (quad_perm, row_half_mirror,
+//     row_mirror) and, above 16 lanes, ds_swizzle/bpermute shuffles.
+//   * A wave owns FPW consecutive frames: descriptors are read with one
+//     coalesced load per wave, results are collected one per lane and written
+//     with one coalesced store per wave.
+//   * No MFMA: this is an HBM-bound byte reduction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint32_t SEL_EVEN = 0x03020100u;  // v_perm: identity
+constexpr uint32_t SEL_ODD  = 0x02030001u;  // v_perm: swap bytes inside each 16-bit half
+
+__device__ __forceinline__ uint32_t dot2_add(uint32_t x, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), (u16x2){1, 1}, acc, false);
+}
+
+// 4 mask bits -> 4 byte masks (0x00 / 0xFF); the shifted copies never overlap.
+__device__ __forceinline__ uint32_t nib_to_bytes(uint32_t nib) {
+    return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+
+// Adds the bytes of chunk v selected by the 16-bit mask m16 (bit i = byte i).
+__device__ __forceinline__ uint32_t add_chunk(const uint4 v, uint32_t m16, uint32_t sel, uint32_t acc) {
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.x & nib_to_bytes(m16 & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.y & nib_to_bytes((m16 >> 4) & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.z & nib_to_bytes((m16 >> 8) & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.w & nib_to_bytes((m16 >> 12) & 15u), sel), acc);
+    return acc;
+}
+
+// Bits [lo, hi) of a 16-bit chunk mask; lo, hi in [0, 16].
+__device__ __forceinline__ uint32_t bits16(uint32_t lo, uint32_t hi) {
+    return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+
+// Mask of the bytes of chunk k (chunk 0 starts at a0 = start & ~15, r = start - a0)
+// that lie in [r + x0, r + x1), x0 <= x1 relative to the frame start.
+__device__ __forceinline__ uint32_t chunk_range_mask(uint32_t k, uint64_t x0r, uint64_t x1r) {
+    const uint64_t c = (uint64_t)k << 4;
+    const uint32_t lo = x0r <= c ? 0u : (x0r - c >= 16 ? 16u : (uint32_t)(x0r - c));
+    const uint32_t hi = x1r <= c ? 0u : (x1r - c >= 16 ? 16u : (uint32_t)(x1r - c));
+    return hi > lo ? bits16(lo, hi) : 0u;
+}
+
+// Clears the two bits of a 2-byte field at chunk-relative position d (may be
+// outside [-1, 15], then nothing is cleared).
+__device__ __forceinline__ uint32_t clear_field(uint32_t m, int64_t d) {
+    const uint32_t sh = (d >= -1 && d <= 15) ? (uint32_t)(d + 1) : 20u;
+    return m & ~((3u << sh) >> 1);
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+    if constexpr (G >= 2)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    if constexpr (G >= 4)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    if constexpr (G >= 8)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
+    if constexpr (G >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
+    if constexpr (G >= 32) v += (uint32_t)__shfl_xor((int)v, 16);
+    if constexpr (G >= 64) v += (uint32_t)__shfl_xor((int)v, 32);
+    return v;
+}
+
+// stack/pico_frame.c:301-307: fold with end-around carry, complement, short_be.
+__device__ __forceinline__ uint32_t finalize(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    const uint32_t c = (~s) & 0xFFFFu;
+    return ((c >> 8) | (c << 8)) & 0xFFFFu;
+}
+
+// The 16-bit checksum word as it sits in memory: hdr->crc = short_be(ret).
+__device__ __forceinline__ void store_crc(uint8_t* p, uint32_t ret) {
+    p[0] = (uint8_t)(ret >> 8);
+    p[1] = (uint8_t)(ret & 0xFFu);
+}
+
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* a0, uint32_t k) {
+    return *reinterpret_cast<const uint4*>(a0 + ((uint64_t)k << 4));
+}
+
+// Hands the per-group result of iteration i to lane (i + g): lane j of the wave
+// ends up holding the result of the wave's frame j.
+template <int G>
+__device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t lane, uint32_t i) {
+    constexpr uint32_t NG = 64 / G;
+    if constexpr (NG == 1) {
+        return lane == i ? val : res;
+    } else {
+        const uint32_t src = ((lane - i) & (NG - 1)) * G;
+        const uint32_t got = (uint32_t)__shfl((int)val, (int)src);
+        return (lane >= i && lane < i + NG) ? got : res;
+    }
+}
+
+}  // namespace
+
+// Device view of struct pico_csum_desc (include/pico_csum.h), 16 bytes.
+struct pico_csum_desc_dev {
+    uint64_t off;
+    uint32_t len;
+    uint32_t seed;
+};
+
+namespace {
+
+struct RawArgs {
+    uint8_t* base;
+    const pico_csum_desc_dev* desc;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t n;
+    uint32_t seed;
+    int32_t crc_off;
+    uint32_t flags;
+    uint32_t fpw;
+    uint16_t* out;
+};
+
+// RAW batch: per-frame pico_checksum / pico_dualbuffer_checksum.
+// UNIFORM: frame i = base + i*stride, len, seed (no descriptors).
+template <int G, int CPL, bool UNIFORM>
+__global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
+    constexpr uint32_t NG = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane / G, l = lane % G;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+
+    uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_seed = 0;
+    if constexpr (!UNIFORM) {
+        if (lane < cnt) {
+            const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+            d_lo = d.x; d_hi = d.y; d_len = d.z; d_seed = d.w;
+        }
+    }
+
+    uint32_t res = 0;
+    for (uint32_t i = 0; i < cnt; i += NG) {
+        const uint32_t j = i + g;
+        uint64_t off;
+        uint32_t len, seed;
+        if constexpr (UNIFORM) {
+            off = (f0 + j) * p.stride;
+            len = p.len;
+            seed = p.seed;
+        } else {
+            const uint32_t lo = (uint32_t)__shfl((int)d_lo, (int)j);
+            const uint32_t hi = (uint32_t)__shfl((int)d_hi, (int)j);
+            off = ((uint64_t)hi << 32) | lo;
+            len = (uint32_t)__shfl((int)d_len, (int)j);
+            seed = (uint32_t)__shfl((int)d_seed, (int)j);
+        }
+        if (j >= cnt) len = 0;
+
+        uint8_t* fp = p.base + off;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
+        const uint32_t r = (uint32_t)(a & 15u);
+        const uint64_t span = (uint64_t)r + len;
+        const uint32_t nchunks = len ? (uint32_t)((span + 15u) >> 4) : 0u;
+        const uint32_t sel = (a & 1u) ? SEL_ODD : SEL_EVEN;
+        const bool has_crc = p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len;
+        const int64_t xr = has_crc ? (int64_t)r + p.crc_off : (int64_t)1 << 40;
+
+        uint32_t acc = 0;
+        for (uint32_t kb = 0; kb < nchunks; kb += G * CPL) {
+            uint4 v[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + l + G * c;
+                v[c] = k < nchunks ? load_chunk(a0, k) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + l + G * c;
+                if (k < nchunks) {
+                    uint32_t m = chunk_range_mask(k, r, span);
+                    m = clear_field(m, xr - ((int64_t)k << 4));
+                    acc = add_chunk(v[c], m, sel, acc);
+                }
+            }
+        }
+        const uint32_t ret = finalize(group_sum<G>(acc) + seed);
+        if ((p.flags & 1u) && has_crc && l == 0 && j < cnt)
+            store_crc(fp + p.crc_off, ret);
+        res = collect<G>(res, ret, lane, i);
+    }
+    if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
+}
+
+struct Ipv4Args {
+    uint8_t* base;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint32_t flags;
+    uint32_t fpw;
+    uint16_t* out_net;
+    uint16_t* out_l4;
+    uint8_t* verdict;
+};
+
+constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u;
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+}
+
+// Fused IPv4 header + TCP/UDP/ICMP checksums, RX verify or TX compute.
+// Semantics: include/pico_csum.h pico_ipv4_checksum_batch_dev; reference
+// modules/pico_ipv4.c:231-257,381-420, stack/pico_socket.c:1916-1968,
+// modules/pico_tcp.c:422-446, pico_udp.c:36-60,123, pico_icmp4.c:30-41.
+template <int G, int CPL>
+__global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
+    constexpr uint32_t NG = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane / G, l = lane % G;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const bool tx = (p.flags & 2u) != 0;
+
+    uint32_t d_lo = 0, d_hi = 0, d_len = 0;
+    if (lane < cnt) {
+        const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+        d_lo = d.x; d_hi = d.y; d_len = d.z;
+    }
+
+    uint32_t res_net = 0, res_l4 = 0, res_v = 0;
+    for (uint32_t i = 0; i < cnt; i += NG) {
+        const uint32_t j = i + g;
+        const uint32_t lo = (uint32_t)__shfl((int)d_lo, (int)j);
+        const uint32_t hi = (uint32_t)__shfl((int)d_hi, (int)j);
+        uint32_t avail = (uint32_t)__shfl((int)d_len, (int)j);
+        if (j >= cnt) avail = 0;
+        uint8_t* fp = p.base + (((uint64_t)hi << 32) | lo);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
+        const uint32_t r = (uint32_t)(a & 15u);
+        const uint32_t sel = (a & 1u) ? SEL_ODD : SEL_EVEN;
+
+        // ---- header parse: chunks 0..2 cover header bytes [0, 20); every lane
+        // of the group loads the same lines (one request per line).
+        uint32_t verdict = V_MALFORMED;
+        bool parsed = false;
+        uint32_t hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0;
+        uint32_t span = 0, load_len = 0;
+        int64_t xoff = (int64_t)1 << 40;
+        bool l4_needed = false;
+        if (avail >= 20) {
+            const uint4 c0 = load_chunk(a0, 0);
+            const uint4 c1 = (r + 20 > 16) ? load_chunk(a0, 1) : make_uint4(0, 0, 0, 0);
+            const uint4 c2 = (r + 20 > 32) ? load_chunk(a0, 2) : make_uint4(0, 0, 0, 0);
+            const uint32_t D[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+            const uint32_t q = r >> 2, s = r & 3u;
+            uint32_t E[6];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+            uint32_t H[5];
+#pragma unroll
+            for (int m = 0; m < 5; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], s);
+            const uint32_t ihl = H[0] & 0x0Fu;
+            hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+            const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+            proto = (H[2] >> 8) & 0xFFu;
+            ipcrc = H[2] >> 16;
+            tl = (tot - hl) & 0xFFFFu;                       // uint16 wrap, pico_ipv4.c:395
+            const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;  // pico_ipv4.c:386
+            const bool bad = hl > avail || (!tx && tl > max_allowed) || hl + tl > avail;
+            if (!bad) {
+                parsed = true;
+                verdict = 0;
+                span = hl + tl;
+                load_len = span;
+                pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
+                         (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
+                if (!tx) {
+                    if (proto == 6u) {
+                        l4_needed = true;
+                    } else if (proto == 17u) {
+                        if (hl + 8u > avail) {
+                            verdict |= V_MALFORMED;
+                        } else {
+                            l4_needed = true;   // decided after the crc field is read
+                            xoff = hl + 6u;
+                            load_len = max(span, hl + 8u);
+                        }
+                    }
+                } else {
+                    if (proto == 6u) {
+                        if (tl < 20u) verdict |= V_MALFORMED;
+                        else { l4_needed = true; xoff = hl + 16u; }
+                    } else if (proto == 1u) {
+                        if (tl < 8u) verdict |= V_MALFORMED;
+                        else { l4_needed = true; xoff = hl + 2u; }
+                    }
+                }
+            }
+        }
+
+        // ---- one pass over the datagram: all bytes, header bytes, crc field
+        const uint32_t nchunks = load_len ? (r + load_len + 15u) >> 4 : 0u;
+        const uint64_t xr = (uint64_t)((int64_t)r + xoff);
+        uint32_t acc_all = 0, acc_hdr = 0, acc_x = 0;
+        for (uint32_t kb = 0; kb < nchunks; kb += G * CPL) {
+            uint4 v[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + l + G * c;
+                v[c] = k < nchunks ? load_chunk(a0, k) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + l + G * c;
+                if (k < nchunks) {
+                    acc_all = add_chunk(v[c], chunk_range_mask(k, r, (uint64_t)r + span), sel, acc_all);
+                    if (k < ((r + hl + 15u) >> 4))
+                        acc_hdr = add_chunk(v[c], chunk_range_mask(k, r, (uint64_t)r + hl), sel, acc_hdr);
+                    acc_x = add_chunk(v[c], chunk_range_mask(k, xr, xr + 2u), sel, acc_x);
+                }
+            }
+        }
+        acc_all = group_sum<G>(acc_all);
+        acc_hdr = group_sum<G>(acc_hdr);
+        acc_x = group_sum<G>(acc_x);
+
+        uint32_t net = 0, l4 = 0;
+        if (parsed) {
+            net = finalize(acc_hdr - (tx ? ipcrc : 0u));
+            if (!tx && net != 0) verdict |= V_NET_BAD;
+            const uint32_t tsum = acc_all - acc_hdr;
+            if (l4_needed) {
+                if (!tx) {
+                    if (proto == 6u || acc_x != 0u) {       // UDP: only a non-zero stored crc (pico_socket.c:1941)
+                        l4 = finalize(pseudo + tsum);
+                        if (l4 != 0) verdict |= V_L4_BAD;
+                    }
+                } else if (proto == 6u) {
+                    l4 = finalize(pseudo + tsum - acc_x);
+                } else {
+                    l4 = finalize(tsum - acc_x);          // ICMPv4: no pseudo header
+                }
+            }
+            if (verdict == 0) verdict = V_ACCEPT;
+        }
+
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l == 0 && j < cnt) {
+            store_crc(fp + 10, net);
+            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + xoff, l4);
+            else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+        }
+        res_net = collect<G>(res_net, net, lane, i);
+        res_l4 = collect<G>(res_l4, l4, lane, i);
+        res_v = collect<G>(res_v, verdict, lane, i);
+    }
+    if (lane < cnt) {
+        if (p.out_net) p.out_net[f0 + lane] = (uint16_t)res_net;
+        if (p.out_l4) p.out_l4[f0 + lane] = (uint16_t)res_l4;
+        if (p.verdict) p.verdict[f0 + lane] = (uint8_t)res_v;
+    }
+}
+
+// ---------------------------------------------------------------- dispatch
+
+#define PICO_FOR_SHAPES(X) \
+    X(64, 1) X(64, 2) X(64, 4) X(64, 8) \
+    X(32, 1) X(32, 2) X(32, 4) X(32, 8) \
+    X(16, 1) X(16, 2) X(16, 4) X(16, 8) \
+    X(8, 1)  X(8, 2)  X(8, 4)  X(8, 8)  \
+    X(4, 1)  X(4, 2)  X(4, 4)  X(4, 8)
+
+inline bool shape_ok(uint32_t G, uint32_t CPL, uint32_t fpw) {
+    if (!(G == 4 || G == 8 || G == 16 || G == 32 || G == 64)) return false;
+    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8)) return false;
+    return fpw >= 1 && fpw <= 64 && fpw % (64 / G) == 0;
+}
+
+inline dim3 grid_for(uint32_t n, uint32_t fpw) {
+    const uint64_t waves = ((uint64_t)n + fpw - 1) / fpw;
+    return dim3((unsigned)((waves + 3) / 4));
+}
+
+}  // namespace
+
+extern "C" {
+
+// Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
+// validate the launch shape, enqueue, and return the hipError_t as int.
+
+int pico_csum_launch_raw(void* base, const void* desc, uint64_t stride, uint32_t len, uint32_t n,
+                         uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t* out,
+                         uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void* stream) {
+    if (!shape_ok(G, CPL, fpw)) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    RawArgs a{static_cast<uint8_t*>(base), static_cast<const pico_csum_desc_dev*>(desc), stride, len, n,
+              seed, crc_off, flags, fpw, out};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define X(g, c)                                                                                 \
+    if (G == g && CPL == c) {                                                                   \
+        if (uniform) hipLaunchKernelGGL((csum_raw_kernel<g, c, true>), grid, block, 0, s, a);   \
+        else hipLaunchKernelGGL((csum_raw_kernel<g, c, false>), grid, block, 0, s, a);          \
+        return (int)hipGetLastError();                                                          \
+    }
+    PICO_FOR_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
+
+int pico_csum_launch_ipv4(void* base, const void* desc, uint32_t n, uint32_t flags, uint16_t* out_net,
+                          uint16_t* out_l4, uint8_t* verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
+                          void* stream) {
+    if (!shape_ok(G, CPL, fpw)) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    Ipv4Args a{static_cast<uint8_t*>(base), static_cast<const pico_csum_desc_dev*>(desc), n, flags, fpw,
+               out_net, out_l4, verdict};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define X(g, c)                                                                      \
+    if (G == g && CPL == c) {                                                        \
+        hipLaunchKernelGGL((csum_ipv4_kernel<g, c>), grid, block, 0, s, a);          \
+        return (int)hipGetLastError();                                               \
+    }
+    PICO_FOR_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
+
+}  // extern "C"

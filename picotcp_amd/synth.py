@@ -1,0 +1,111 @@
+"""Seeded synthetic frame batches.
+
+Byte source: splitmix64 (Steele, Lea, Flood 2014): state_i = seed + (i+1)*0x9E3779B97F4A7C15,
+z = mix(state_i), little-endian bytes of z concatenated.  Same definition in the
+golden-fixture generator (tests/golden/make_golden.py), so fixtures store only
+seeds and expected outputs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(seed: int, count: int, start: int = 0) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        i = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + i * GAMMA
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        return z ^ (z >> np.uint64(31))
+
+
+def random_bytes(seed: int, nbytes: int) -> np.ndarray:
+    words = splitmix64(seed, (nbytes + 7) // 8)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def uniform_batch(n: int, length: int, stride: int | None = None, seed: int = 1) -> np.ndarray:
+    """C1/C3/C4: n frames of `length` random bytes at `stride` (default packed)."""
+    stride = length if stride is None else stride
+    total = (n - 1) * stride + length if n else 0
+    return random_bytes(seed, total)
+
+
+SIMPLE_IMIX = ((64, 7), (576, 4), (1500, 1))
+
+
+def imix_lengths(n: int, seed: int, mix=SIMPLE_IMIX) -> np.ndarray:
+    """C2: frame sizes in the simple-IMIX ratio 7:4:1, seeded shuffle."""
+    sizes = np.concatenate([np.full(w, s, dtype=np.uint32) for s, w in mix])
+    reps = -(-n // sizes.size)
+    lens = np.tile(sizes, reps)[:n]
+    perm = np.argsort(splitmix64(seed ^ 0x5EED, n), kind="stable")
+    return lens[perm]
+
+
+def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = True, ihl: int = 5):
+    """IPv4 datagrams of the given total lengths, packed back to back, each with a
+    valid header (vhl = 0x40|ihl, len, ttl 64, proto, random id/addresses/ports/payload)
+    and a transport header (TCP 20 B, UDP 8 B, ICMP 8 B).  Every crc field is zero:
+    make them valid with the TX kernel (PICO_CSUM_F_TX | F_WRITE) or a host checker.
+    eth=True puts a 14-byte Ethernet header in front of each datagram (pico_ethernet.c:183),
+    so the IPv4 headers are 2-byte aligned as in the reference RX path.
+    Returns (buffer uint8, net offsets uint64, available bytes uint32)."""
+    lengths = np.asarray(lengths, dtype=np.uint32)
+    n = lengths.size
+    pre = 14 if eth else 0
+    frame_len = lengths.astype(np.uint64) + pre
+    starts = np.zeros(n, dtype=np.uint64)
+    if n:
+        starts[1:] = np.cumsum(frame_len)[:-1]
+    total = int(frame_len.sum())
+    buf = random_bytes(seed, total)
+    net = starts + np.uint64(pre)
+    hl = 4 * ihl
+    rnd = splitmix64(seed ^ 0xABCDEF, n).view(np.uint8).reshape(n, 8)
+    idx = net.astype(np.int64)
+
+    def put(off, vals):
+        buf[idx + off] = vals
+
+    if eth:
+        e = starts.astype(np.int64)
+        buf[e + 12] = 0x08
+        buf[e + 13] = 0x00
+    put(0, np.uint8(0x40 | ihl))
+    put(1, 0)
+    put(2, (lengths >> 8).astype(np.uint8))
+    put(3, (lengths & 0xFF).astype(np.uint8))
+    put(4, rnd[:, 0]); put(5, rnd[:, 1])
+    put(6, 0x40); put(7, 0)
+    put(8, 64)
+    put(9, np.uint8(proto))
+    put(10, 0); put(11, 0)
+    # src 10.x.y.z / dst 192.168.y.z from the random word
+    put(12, 10); put(13, rnd[:, 2]); put(14, rnd[:, 3]); put(15, rnd[:, 4])
+    put(16, 192); put(17, 168); put(18, rnd[:, 5]); put(19, rnd[:, 6])
+    for o in range(20, hl):               # options: NOP padding
+        put(o, 1)
+    t = idx + hl
+    if proto == 6:
+        buf[t + 12] = 0x50                  # data offset 5
+        buf[t + 13] = 0x18                  # PSH|ACK
+        buf[t + 16] = 0
+        buf[t + 17] = 0
+    elif proto == 17:
+        ul = (lengths - hl).astype(np.uint32)
+        buf[t + 4] = (ul >> 8).astype(np.uint8)
+        buf[t + 5] = (ul & 0xFF).astype(np.uint8)
+        buf[t + 6] = 0
+        buf[t + 7] = 0
+    elif proto == 1:
+        buf[t + 0] = 8                      # echo request
+        buf[t + 1] = 0
+        buf[t + 2] = 0
+        buf[t + 3] = 0
+    avail = lengths.copy()
+    return buf, net, avail

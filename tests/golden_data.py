@@ -1,0 +1,56 @@
+"""Loaders for the committed golden fixtures (tests/golden/, made by make_golden.py)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from picotcp_amd import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+
+
+def kat() -> dict:
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        return json.load(f)
+
+
+def raw_cases() -> dict:
+    z = np.load(os.path.join(GOLDEN, "raw_cases.npz"))
+    cases: dict = {}
+    for key in z.files:
+        name, field = key.split("__")
+        cases.setdefault(name, {})[field] = z[key]
+    return cases
+
+
+def raw_case_inputs(case: dict, seed_fn):
+    """(buffer, desc) for a raw case; seed_fn(first12_bytes) -> accumulator seed."""
+    buf = synth.random_bytes(int(case["buf_seed"]), int(case["buf_len"]))
+    n = case["off"].size
+    first = synth.random_bytes(int(case["buf_seed"]) ^ 0x77, 12 * n).reshape(n, 12)
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    desc["off"] = case["off"]
+    desc["len"] = case["len"]
+    for i in np.nonzero(case["first_len"])[0]:
+        desc["seed"][i] = seed_fn(first[i, :case["first_len"][i]])
+    return buf, desc
+
+
+def ipv4_cases() -> dict:
+    z = np.load(os.path.join(GOLDEN, "ipv4_cases.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def unit_socket_frames() -> dict:
+    z = np.load(os.path.join(GOLDEN, "unit_socket_frames.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def ipv4_desc(net: np.ndarray, avail: np.ndarray) -> np.ndarray:
+    d = np.zeros(net.size, dtype=DESC_DTYPE)
+    d["off"] = net
+    d["len"] = avail
+    return d

@@ -1,0 +1,244 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the
+reference's golden fixtures, bit-exact.  Run on an MI355X with `-m gpu`."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from picotcp_amd import batch, synth
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
+
+
+def u16(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint16)
+
+
+def to_dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(autouse=True)
+def _reset_override():
+    yield
+    batch.set_launch_override(0, 0, 0)
+
+
+# ------------------------------------------------------------------ uniform
+
+@pytest.mark.parametrize("name,stride", [("c1_1500_packed", 1500), ("c1_1500_stride1536", 1536)])
+def test_uniform_golden(name, stride):
+    case = G.raw_cases()[name]
+    buf, _ = G.raw_case_inputs(case, lambda b: O.adder(0, b))
+    n = case["off"].size
+    got = u16(batch.checksum_uniform(to_dev(buf), stride, 1500, n))
+    np.testing.assert_array_equal(got, case["expected"])
+
+
+@pytest.mark.parametrize("g,c", SHAPES)
+def test_uniform_every_shape(g, c):
+    """Every compiled (group, chunks-per-lane) shape, several frames-per-wave, odd lengths,
+    odd strides, a seed -- against the oracle."""
+    rng = np.random.default_rng(g * 10 + c)
+    for ln, stride in ((1500, 1500), (1501, 1503), (63, 64), (0, 8), (9000, 9001), (3, 5)):
+        n = int(rng.integers(1, 700))
+        buf = synth.uniform_batch(n, ln, stride, seed=ln + stride)
+        if buf.size == 0:
+            buf = np.zeros(16, np.uint8)
+        seed = int(rng.integers(0, 1 << 32))
+        want = O.batch_uniform(buf, stride, ln, n, seed)
+        d = to_dev(buf)
+        for fpw in sorted({64 // g, 64, (64 // g) * 3 if (64 // g) * 3 <= 64 else 64}):
+            batch.set_launch_override(g, c, fpw)
+            got = u16(batch.checksum_uniform(d, stride, ln, n, seed=seed))
+            np.testing.assert_array_equal(got, want, err_msg=f"g={g} c={c} fpw={fpw} len={ln} stride={stride}")
+
+
+def test_uniform_c1_full_size():
+    """C1 at its full size: 256K x 1500 B, bit-exact against the oracle on every frame."""
+    n, ln = 262144, 1500
+    buf = synth.uniform_batch(n, ln, seed=2026)
+    want = O.batch_uniform(buf, ln, ln, n)
+    got = u16(batch.checksum_uniform(to_dev(buf), ln, ln, n))
+    np.testing.assert_array_equal(got, want)
+
+
+def test_uniform_c3_jumbo_full_size():
+    """C3: 256K x 9000 B jumbo frames (2.2 GiB), bit-exact on every frame."""
+    n, ln = 262144, 9000
+    buf = synth.uniform_batch(n, ln, seed=2027)
+    want = O.batch_uniform(buf, ln, ln, n)
+    got = u16(batch.checksum_uniform(to_dev(buf), ln, ln, n))
+    np.testing.assert_array_equal(got, want)
+    del buf
+
+
+# ------------------------------------------------------------------ descriptors
+
+@pytest.mark.parametrize("name", ["mixed_align", "c2_imix_raw", "c3_9000", "c3_65536", "wrap_lengths",
+                                  "c1_1500_packed"])
+def test_desc_golden(name):
+    case = G.raw_cases()[name]
+    buf, desc = G.raw_case_inputs(case, lambda b: O.adder(0, b))
+    got = u16(batch.checksum_batch(to_dev(buf), batch.desc_to_device(desc, DEV), desc.size))
+    np.testing.assert_array_equal(got, case["expected"])
+
+
+@pytest.mark.parametrize("g,c", SHAPES)
+def test_desc_every_shape(g, c):
+    case = G.raw_cases()["mixed_align"]
+    buf, desc = G.raw_case_inputs(case, lambda b: O.adder(0, b))
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
+    for fpw in sorted({64 // g, 64}):
+        batch.set_launch_override(g, c, fpw)
+        got = u16(batch.checksum_batch(d_buf, d_desc, desc.size))
+        np.testing.assert_array_equal(got, case["expected"], err_msg=f"g={g} c={c} fpw={fpw}")
+
+
+def test_desc_empty_and_edge_lengths():
+    buf = synth.random_bytes(99, 4096)
+    offs, lens = [], []
+    for off in range(0, 33):
+        for ln in (0, 1, 2, 3, 4, 15, 16, 17, 31, 32, 33):
+            offs.append(off)
+            lens.append(ln)
+    desc = batch.make_desc(offs, lens)
+    want = O.batch_raw(buf, desc)
+    got = u16(batch.checksum_batch(to_dev(buf), batch.desc_to_device(desc, DEV), desc.size))
+    np.testing.assert_array_equal(got, want)
+    assert (want[np.array(lens) == 0] == 0xFFFF).all()
+
+
+def test_desc_crc_field_and_write_roundtrip():
+    """crc_off: the field reads as zero; F_WRITE stores short_be(ret) there; the
+    region then verifies to 0 -- the TX insert / RX verify round trip."""
+    rng = np.random.default_rng(12)
+    buf = synth.random_bytes(7, 1 << 20)
+    n = 3000
+    lens = rng.integers(12, 1500, n)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 5, n).astype(np.uint64))[:-1]
+    offs += 1
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    desc = batch.make_desc(offs, lens, seeds)
+    want = O.batch_raw(buf, desc, crc_off=10)
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
+    got = u16(batch.checksum_batch(d_buf, d_desc, n, crc_off=10))
+    np.testing.assert_array_equal(got, want)
+    got = u16(batch.checksum_batch(d_buf, d_desc, n, crc_off=10, flags=batch.F_WRITE))
+    np.testing.assert_array_equal(got, want)
+    after = d_buf.cpu().numpy()
+    f = offs.astype(np.int64) + 10
+    np.testing.assert_array_equal(after[f], (want >> 8).astype(np.uint8))
+    np.testing.assert_array_equal(after[f + 1], (want & 0xFF).astype(np.uint8))
+    verify = u16(batch.checksum_batch(d_buf, d_desc, n))
+    assert (verify == 0).all()
+    # bytes outside the crc fields untouched
+    mask = np.ones(after.size, bool)
+    mask[f] = False
+    mask[f + 1] = False
+    np.testing.assert_array_equal(after[mask], buf[mask])
+
+
+# ------------------------------------------------------------------ IPv4 fused
+
+def test_ipv4_golden_rx_tx():
+    c = G.ipv4_cases()
+    desc = batch.desc_to_device(G.ipv4_desc(c["net"], c["avail"]), DEV)
+    n = c["net"].size
+    net, l4, v = batch.ipv4_checksum_batch(to_dev(c["buf"]), desc, n)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(v.cpu().numpy(), c["rx_verdict"])
+    np.testing.assert_array_equal(u16(net), c["rx_net"])
+    np.testing.assert_array_equal(u16(l4), c["rx_l4"])
+    net, l4, v = batch.ipv4_checksum_batch(to_dev(c["tx_buf"]), desc, n, flags=batch.F_TX)
+    np.testing.assert_array_equal(u16(net), c["tx_net"])
+    np.testing.assert_array_equal(u16(l4), c["tx_l4"])
+    np.testing.assert_array_equal(v.cpu().numpy(), c["tx_verdict"])
+
+
+@pytest.mark.parametrize("g,c", SHAPES)
+def test_ipv4_every_shape(g, c):
+    cs = G.ipv4_cases()
+    desc = batch.desc_to_device(G.ipv4_desc(cs["net"], cs["avail"]), DEV)
+    n = cs["net"].size
+    d_buf = to_dev(cs["buf"])
+    for fpw in sorted({64 // g, 64}):
+        batch.set_launch_override(g, c, fpw)
+        net, l4, v = batch.ipv4_checksum_batch(d_buf, desc, n)
+        np.testing.assert_array_equal(u16(net), cs["rx_net"], err_msg=f"g={g} c={c} fpw={fpw}")
+        np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"g={g} c={c} fpw={fpw}")
+        np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"g={g} c={c} fpw={fpw}")
+
+
+def test_ipv4_unit_socket_frames():
+    c = G.unit_socket_frames()
+    desc = batch.desc_to_device(G.ipv4_desc(c["net"], c["avail"]), DEV)
+    net, l4, v = batch.ipv4_checksum_batch(to_dev(c["buf"]), desc, c["net"].size)
+    np.testing.assert_array_equal(v.cpu().numpy(), c["rx_verdict"])
+    np.testing.assert_array_equal(u16(net), c["rx_net"])
+    np.testing.assert_array_equal(u16(l4), c["rx_l4"])
+
+
+@pytest.mark.parametrize("proto,eth,ihl", [(6, True, 5), (6, False, 7), (17, True, 5), (1, True, 5), (6, True, 15)])
+def test_ipv4_tx_write_then_rx_accepts(proto, eth, ihl):
+    """C2-style IMIX batch: TX compute + in-place write, then RX verify accepts every
+    datagram; the written fields equal the oracle's TX outputs."""
+    lens = synth.imix_lengths(20000, 5 + proto)
+    lens = np.maximum(lens, 4 * ihl + 20).astype(np.uint32)
+    buf, net_off, avail = synth.ipv4_batch(lens, seed=proto * 7 + ihl, proto=proto, eth=eth, ihl=ihl)
+    desc_h = G.ipv4_desc(net_off, avail)
+    want_net, want_l4, want_v = O.batch_ipv4(buf, desc_h, tx=True)
+    assert (want_v == 1).all()
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc_h, DEV)
+    net, l4, v = batch.ipv4_checksum_batch(d_buf, d_desc, lens.size, flags=batch.F_TX | batch.F_WRITE)
+    np.testing.assert_array_equal(u16(net), want_net)
+    np.testing.assert_array_equal(u16(l4), want_l4)
+    net, l4, v = batch.ipv4_checksum_batch(d_buf, d_desc, lens.size)
+    assert (v.cpu().numpy() == 1).all()
+    assert (u16(net) == 0).all()
+    assert (u16(l4) == 0).all()
+    # oracle agrees on the written buffer
+    wb = d_buf.cpu().numpy()
+    on, ol, ov = O.batch_ipv4(wb, desc_h, tx=False)
+    assert (ov == 1).all()
+
+
+def test_c2_full_size_rx():
+    """C2 at full size: 256K IMIX IPv4/TCP datagrams, RX verify vs oracle, with 1/64 corrupted."""
+    lens = synth.imix_lengths(262144, 2026)
+    buf, net_off, avail = synth.ipv4_batch(lens, seed=11, proto=6, eth=True)
+    desc_h = G.ipv4_desc(net_off, avail)
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc_h, DEV)
+    batch.ipv4_checksum_batch(d_buf, d_desc, lens.size, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize()
+    h = d_buf.cpu().numpy()
+    bad = net_off[::64].astype(np.int64) + 30
+    h[bad] ^= 0x10
+    want = O.batch_ipv4(h, desc_h, tx=False)
+    got = batch.ipv4_checksum_batch(to_dev(h), d_desc, lens.size)
+    np.testing.assert_array_equal(u16(got[0]), want[0])
+    np.testing.assert_array_equal(u16(got[1]), want[1])
+    np.testing.assert_array_equal(got[2].cpu().numpy(), want[2])
+    assert (want[2][::64] != 1).all() and (np.delete(want[2], np.arange(0, lens.size, 64)) == 1).all()
+
+
+# ------------------------------------------------------------------ host-resident
+
+def test_host_batch_roundtrip():
+    n, ln = 50000, 1500
+    buf = synth.uniform_batch(n, ln, seed=31)
+    want = O.batch_uniform(buf, ln, ln, n)
+    hb = batch.HostBatch(0, staging_bytes=8 << 20)
+    try:
+        got = hb.checksum_uniform(buf, ln, ln, n)
+    finally:
+        hb.close()
+    np.testing.assert_array_equal(got, want)

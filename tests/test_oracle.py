@@ -1,0 +1,135 @@
+"""CPU tests: the oracle (and the library's scalar drop-in) against the reference's
+golden vectors, and the oracle against the compiled reference on random inputs."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from picotcp_amd import _lib
+from tests import golden_data as G
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _lib.load()
+
+
+def _scalar(lib, data: bytes) -> int:
+    a = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(1, np.uint8)
+    return lib.pico_checksum(ctypes.c_void_p(a.ctypes.data), len(data))
+
+
+def _scalar_dual(lib, d1: bytes, d2: bytes) -> int:
+    a1 = np.frombuffer(d1, dtype=np.uint8).copy()
+    a2 = np.frombuffer(d2, dtype=np.uint8).copy()
+    return lib.pico_dualbuffer_checksum(ctypes.c_void_p(a1.ctypes.data), a1.size,
+                                        ctypes.c_void_p(a2.ctypes.data), a2.size)
+
+
+def test_kat_checksum(lib):
+    for k in G.kat()["checksum"]:
+        data = bytes.fromhex(k["hex"])
+        assert O.checksum(data) == k["expected"], k["name"]
+        assert _scalar(lib, data) == k["expected"], k["name"]
+
+
+def test_kat_fill_wrap(lib):
+    # uint32 accumulator wrap at >= 131076 bytes of 0xFF (pico_frame.c:279-299)
+    for k in G.kat()["fill"]:
+        data = bytes([k["fill"]]) * k["len"]
+        assert O.checksum(data) == k["expected"], k
+        assert _scalar(lib, data) == k["expected"], k
+
+
+def test_kat_dualbuffer(lib):
+    for k in G.kat()["dualbuffer"]:
+        d1, d2 = bytes.fromhex(k["hex1"]), bytes.fromhex(k["hex2"])
+        assert O.dualbuffer_checksum(d1, d2) == k["expected"], k["name"]
+        assert _scalar_dual(lib, d1, d2) == k["expected"], k["name"]
+
+
+@pytest.mark.parametrize("name", ["mixed_align", "c1_1500_packed", "c1_1500_stride1536", "c3_9000",
+                                  "c3_65536", "c2_imix_raw", "wrap_lengths"])
+def test_raw_cases(name):
+    case = G.raw_cases()[name]
+    buf, desc = G.raw_case_inputs(case, lambda b: O.adder(0, b))
+    got = O.batch_raw(buf, desc)
+    np.testing.assert_array_equal(got, case["expected"])
+
+
+def test_seed_helpers_match_oracle(lib):
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        b = rng.integers(0, 256, int(rng.integers(0, 41)), dtype=np.uint8)
+        s0 = int(rng.integers(0, 1 << 32))
+        assert lib.pico_checksum_partial(s0, ctypes.c_void_p(b.ctypes.data), b.size) == O.adder(s0, b)
+        src, dst = rng.integers(0, 256, 4, dtype=np.uint8), rng.integers(0, 256, 4, dtype=np.uint8)
+        proto, tl = int(rng.integers(0, 256)), int(rng.integers(0, 65536))
+        want = O.ipv4_pseudo_sum(src.tobytes(), dst.tobytes(), proto, tl)
+        got = lib.pico_ipv4_pseudo_partial(int(src.view("<u4")[0]), int(dst.view("<u4")[0]), proto, tl)
+        assert got == want
+
+
+def test_ipv4_cases_rx_tx():
+    c = G.ipv4_cases()
+    desc = G.ipv4_desc(c["net"], c["avail"])
+    n, l4, v = O.batch_ipv4(c["buf"], desc, tx=False)
+    np.testing.assert_array_equal(v, c["rx_verdict"])
+    np.testing.assert_array_equal(n, c["rx_net"])
+    np.testing.assert_array_equal(l4, c["rx_l4"])
+    n, l4, v = O.batch_ipv4(c["tx_buf"], desc, tx=True)
+    np.testing.assert_array_equal(v, c["tx_verdict"])
+    np.testing.assert_array_equal(n, c["tx_net"])
+    np.testing.assert_array_equal(l4, c["tx_l4"])
+
+
+def test_unit_socket_frames():
+    c = G.unit_socket_frames()
+    n, l4, v = O.batch_ipv4(c["buf"], G.ipv4_desc(c["net"], c["avail"]), tx=False)
+    np.testing.assert_array_equal(v, c["rx_verdict"])
+    np.testing.assert_array_equal(n, c["rx_net"])
+    np.testing.assert_array_equal(l4, c["rx_l4"])
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+def test_oracle_vs_compiled_reference_random(lib):
+    """Restatement (and the scalar drop-in) == reference pico_frame.c on random
+    regions at every start alignment, lengths 0..4100 and the wrap boundary."""
+    rng = np.random.default_rng(77)
+    big = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    lens = list(range(0, 40)) + list(rng.integers(0, 4100, 1500)) + [131074, 131075, 131076, 131077, 262145]
+    for ln in lens:
+        ln = int(ln)
+        off = int(rng.integers(0, big.size - ln + 1))
+        region = big[off:off + ln]
+        want = O.ref_checksum(region)
+        assert O.checksum(region) == want, (off, ln)
+        p = ctypes.c_void_p(big.ctypes.data + off)
+        assert lib.pico_checksum(p, ln) == want, (off, ln)
+    ones = np.full(131076, 0xFF, dtype=np.uint8)
+    assert O.ref_checksum(ones) == O.checksum(ones) == 0x0100    # the documented wrap
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+def test_oracle_dualbuffer_vs_reference_odd_first_len():
+    """pico_dualbuffer_checksum with an odd len1 (the reference warns, :320) keeps
+    adder semantics: the odd byte of buffer 1 is a low byte."""
+    rng = np.random.default_rng(5)
+    for _ in range(300):
+        b1 = rng.integers(0, 256, int(rng.integers(0, 15)), dtype=np.uint8)
+        b2 = rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)
+        assert O.dualbuffer_checksum(b1, b2) == O.ref_dualbuffer_checksum(b1, b2)
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+def test_multithreaded_baseline_matches():
+    from picotcp_amd import synth
+    n, ln = 2000, 1500
+    buf = synth.uniform_batch(n, ln, seed=9)
+    _, ref = O.uniform_mt(buf, ln, ln, n, 4, kind="reference")
+    _, port = O.uniform_mt(buf, ln, ln, n, 3, kind="port")
+    np.testing.assert_array_equal(ref, port)
+    np.testing.assert_array_equal(ref, O.batch_uniform(buf, ln, ln, n))
