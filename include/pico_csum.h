@@ -98,20 +98,27 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
 
 /* ---------------------------------------------------------------- layer 2 */
 
-/* Batch of pico_checksum / pico_dualbuffer_checksum calls:
+/* Every device batch takes the size of the buffer behind d_base (base_len):
+ * no byte outside [d_base, d_base + base_len) is ever read or written.
+ *
+ * Batch of pico_checksum / pico_dualbuffer_checksum calls:
  *   d_out[i] = finalize(adder(desc[i].seed, d_base + desc[i].off, desc[i].len))
  * crc_off >= 0 (even): the 2 bytes at off+crc_off read as zero when they lie
  * inside the region ("hdr->crc = 0" before computing: pico_ipv4.c:237,
  * pico_icmp4.c:38, pico_tcp.c:980); with PICO_CSUM_F_WRITE the result is
  * stored there (pico_ipv4.c:238, pico_icmp4.c:39, pico_tcp.c:981).
- * crc_off < 0: no crc field.  Regions may not overlap when F_WRITE is set. */
-int pico_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
-                            int32_t crc_off, uint32_t flags, uint16_t *d_out, void *stream);
+ * crc_off < 0: no crc field.  Regions may not overlap when F_WRITE is set.
+ * A region that does not lie inside base_len is not read: d_out[i] = 0 and,
+ * when d_bad != NULL, *d_bad (a device uint32 the caller zeroes) counts it. */
+int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                            uint32_t n, int32_t crc_off, uint32_t flags, uint16_t *d_out,
+                            uint32_t *d_bad, void *stream);
 
 /* Uniform batch (no descriptors): frame i = d_base + i*stride, len bytes,
- * seed added to every frame.  The layout of a packed frame ring. */
-int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len, uint32_t n,
-                                    uint32_t seed, uint16_t *d_out, void *stream);
+ * seed added to every frame.  The layout of a packed frame ring.
+ * (n-1)*stride + len must not exceed base_len (else -EINVAL). */
+int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint64_t stride, uint32_t len,
+                                    uint32_t n, uint32_t seed, uint16_t *d_out, void *stream);
 
 /* Fused IPv4 header + transport batch, one IPv4 datagram per descriptor
  * (desc.off -> IPv4 header, desc.len = bytes available).
@@ -124,10 +131,11 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_
  * TX (F_TX): crc fields read as zero; d_out_* are the values to store
  *   (IPv4 header; TCP with pseudo header; ICMPv4 without; UDP 0 as
  *   pico_udp.c:123).  F_WRITE stores them into accepted frames in place.
+ * A datagram whose [off, off+len) is not inside base_len is MALFORMED, unread.
  * Any output pointer may be NULL. */
-int pico_ipv4_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
-                                 uint32_t flags, uint16_t *d_out_net, uint16_t *d_out_transport,
-                                 uint8_t *d_verdict, void *stream);
+int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                                 uint32_t n, uint32_t flags, uint16_t *d_out_net,
+                                 uint16_t *d_out_transport, uint8_t *d_verdict, void *stream);
 
 /* ---------------------------------------------------------------- layer 3 */
 

@@ -70,9 +70,9 @@ def load() -> ctypes.CDLL:
     sig("pico_dualbuffer_checksum", u16, vp, u32, vp, u32)
     sig("pico_checksum_partial", u32, u32, vp, u32)
     sig("pico_ipv4_pseudo_partial", u32, u32, u32, ctypes.c_uint8, ctypes.c_uint16)
-    sig("pico_checksum_batch_dev", ctypes.c_int, vp, vp, u32, i32, u32, vp, vp)
-    sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u32, u32, u32, vp, vp)
-    sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, vp, u32, u32, vp, vp, vp, vp)
+    sig("pico_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, i32, u32, vp, vp, vp)
+    sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u64, u32, u32, u32, vp, vp)
+    sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
     sig("pico_csum_ctx_destroy", None, vp)
     sig("pico_checksum_batch_uniform_host", ctypes.c_int, vp, vp, u64, u32, u32, u32, vp)

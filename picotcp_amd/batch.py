@@ -73,15 +73,16 @@ def checksum_uniform(base: torch.Tensor, stride: int, length: int, n: int, seed:
         out = torch.empty(n, dtype=torch.int16, device=base.device)
     lib = _lib.load()
     _lib.check("pico_checksum_batch_uniform_dev",
-               lib.pico_checksum_batch_uniform_dev(_ptr(base), stride, length, n, seed & 0xFFFFFFFF,
+               lib.pico_checksum_batch_uniform_dev(_ptr(base), base.numel(), stride, length, n, seed & 0xFFFFFFFF,
                                                    _ptr(out), _stream_handle(stream)))
     return out
 
 
 def checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, crc_off: int = -1, flags: int = 0,
-                   out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                   out: torch.Tensor | None = None, bad: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """out[i] = finalize(adder(desc[i].seed, base + desc[i].off, desc[i].len)); crc field
-    at crc_off read as zero (and written with F_WRITE)."""
+    at crc_off read as zero (and written with F_WRITE).  Regions outside `base` are not
+    read (out 0); `bad` (int32[1] on the device) counts them when given."""
     _require_device(base, "base")
     _require_device(desc, "desc")
     if desc.numel() < 16 * n:
@@ -90,8 +91,8 @@ def checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, crc_off: int 
         out = torch.empty(n, dtype=torch.int16, device=base.device)
     lib = _lib.load()
     _lib.check("pico_checksum_batch_dev",
-               lib.pico_checksum_batch_dev(_ptr(base), _ptr(desc), n, crc_off, flags, _ptr(out),
-                                           _stream_handle(stream)))
+               lib.pico_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, crc_off, flags, _ptr(out),
+                                           _ptr(bad), _stream_handle(stream)))
     return out
 
 
@@ -108,7 +109,7 @@ def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     lib = _lib.load()
     _lib.check("pico_ipv4_checksum_batch_dev",
-               lib.pico_ipv4_checksum_batch_dev(_ptr(base), _ptr(desc), n, flags, _ptr(out_net),
+               lib.pico_ipv4_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_net),
                                                 _ptr(out_l4), _ptr(verdict), _stream_handle(stream)))
     return out_net, out_l4, verdict
 

@@ -22,10 +22,11 @@
 #include "pico_csum.h"
 
 /* kernels TU (C++/HIP), extern "C" */
-int pico_csum_launch_raw(void *base, const void *desc, uint64_t stride, uint32_t len, uint32_t n,
-                         uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
-                         uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void *stream);
-int pico_csum_launch_ipv4(void *base, const void *desc, uint32_t n, uint32_t flags, uint16_t *out_net,
+int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64_t stride, uint32_t len,
+                         uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
+                         uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void *stream);
+int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
+                          uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
                           void *stream);
 
@@ -185,8 +186,9 @@ static int launch_status(int herr, const char *what)
  * sync): tuned for the simple-IMIX mean (354 B) .. MTU range. */
 #define DESC_TYPICAL_LEN 512u
 
-int pico_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
-                            int32_t crc_off, uint32_t flags, uint16_t *d_out, void *stream)
+int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                            uint32_t n, int32_t crc_off, uint32_t flags, uint16_t *d_out,
+                            uint32_t *d_bad, void *stream)
 {
     struct shape s;
     int rc;
@@ -205,12 +207,12 @@ int pico_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, u
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN);
-    return launch_status(pico_csum_launch_raw(d_base, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
-                                              s.G, s.CPL, s.fpw, 0, stream), "pico_checksum_batch_dev");
+    return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
+                                              d_bad, s.G, s.CPL, s.fpw, 0, stream), "pico_checksum_batch_dev");
 }
 
-int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_t len, uint32_t n,
-                                    uint32_t seed, uint16_t *d_out, void *stream)
+int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint64_t stride, uint32_t len,
+                                    uint32_t n, uint32_t seed, uint16_t *d_out, void *stream)
 {
     struct shape s;
     int rc;
@@ -218,16 +220,20 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t stride, uint32_
         return 0;
     if (!d_base || !d_out)
         return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if ((uint64_t)(n - 1) > (UINT64_MAX - len) / (stride ? stride : 1) ||
+        (uint64_t)(n - 1) * stride + len > base_len)
+        return fail(PICO_CSUM_EINVAL, "frames exceed base_len");
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, len);
-    return launch_status(pico_csum_launch_raw((void *)d_base, NULL, stride, len, n, seed, -1, 0, d_out,
-                                              s.G, s.CPL, s.fpw, 1, stream), "pico_checksum_batch_uniform_dev");
+    return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
+                                              d_out, NULL, s.G, s.CPL, s.fpw, 1, stream),
+                         "pico_checksum_batch_uniform_dev");
 }
 
-int pico_ipv4_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_desc, uint32_t n,
-                                 uint32_t flags, uint16_t *d_out_net, uint16_t *d_out_transport,
-                                 uint8_t *d_verdict, void *stream)
+int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                                 uint32_t n, uint32_t flags, uint16_t *d_out_net,
+                                 uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
 {
     struct shape s;
     int rc;
@@ -244,7 +250,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, const struct pico_csum_desc *d_de
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN);
-    return launch_status(pico_csum_launch_ipv4(d_base, d_desc, n, flags, d_out_net, d_out_transport,
+    return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),
                          "pico_ipv4_checksum_batch_dev");
 }
@@ -352,8 +358,8 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
         e = hipMemcpyAsync(c->d_buf[b], src, bytes, hipMemcpyHostToDevice, c->st[b]);
         if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "H2D: %s", hipGetErrorString(e)); break; }
         s = pick_shape(cnt, len);
-        rc = launch_status(pico_csum_launch_raw(c->d_buf[b], NULL, stride, len, cnt, seed, -1, 0,
-                                                c->d_out[b], s.G, s.CPL, s.fpw, 1, c->st[b]),
+        rc = launch_status(pico_csum_launch_raw(c->d_buf[b], c->staging, NULL, stride, len, cnt, seed, -1, 0,
+                                                c->d_out[b], NULL, s.G, s.CPL, s.fpw, 1, c->st[b]),
                            "pico_checksum_batch_uniform_host");
         if (rc) break;
         e = hipMemcpyAsync(out + first, c->d_out[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]);

@@ -128,6 +128,7 @@ namespace {
 
 struct RawArgs {
     uint8_t* base;
+    uint64_t base_len;
     const pico_csum_desc_dev* desc;
     uint64_t stride;
     uint32_t len;
@@ -137,6 +138,7 @@ struct RawArgs {
     uint32_t flags;
     uint32_t fpw;
     uint16_t* out;
+    uint32_t* bad;
 };
 
 // RAW batch: per-frame pico_checksum / pico_dualbuffer_checksum.
@@ -176,6 +178,9 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
             seed = (uint32_t)__shfl((int)d_seed, (int)j);
         }
         if (j >= cnt) len = 0;
+        // a region outside the batch buffer is never read (include/pico_csum.h)
+        const bool oob = !UNIFORM && j < cnt && (off > p.base_len || len > p.base_len - off);
+        if (oob) len = 0;
 
         uint8_t* fp = p.base + off;
         const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
@@ -205,9 +210,10 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
                 }
             }
         }
-        const uint32_t ret = finalize(group_sum<G>(acc) + seed);
+        const uint32_t ret = oob ? 0u : finalize(group_sum<G>(acc) + seed);
         if ((p.flags & 1u) && has_crc && l == 0 && j < cnt)
             store_crc(fp + p.crc_off, ret);
+        if (oob && l == 0 && p.bad) atomicAdd(p.bad, 1u);
         res = collect<G>(res, ret, lane, i);
     }
     if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
@@ -215,6 +221,7 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
 
 struct Ipv4Args {
     uint8_t* base;
+    uint64_t base_len;
     const pico_csum_desc_dev* desc;
     uint32_t n;
     uint32_t flags;
@@ -257,8 +264,9 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
         const uint32_t lo = (uint32_t)__shfl((int)d_lo, (int)j);
         const uint32_t hi = (uint32_t)__shfl((int)d_hi, (int)j);
         uint32_t avail = (uint32_t)__shfl((int)d_len, (int)j);
-        if (j >= cnt) avail = 0;
-        uint8_t* fp = p.base + (((uint64_t)hi << 32) | lo);
+        const uint64_t off = ((uint64_t)hi << 32) | lo;
+        if (j >= cnt || off > p.base_len || avail > p.base_len - off) avail = 0;   // unread -> MALFORMED
+        uint8_t* fp = p.base + off;
         const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
         const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
         const uint32_t r = (uint32_t)(a & 15u);
@@ -412,13 +420,13 @@ extern "C" {
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
 
-int pico_csum_launch_raw(void* base, const void* desc, uint64_t stride, uint32_t len, uint32_t n,
-                         uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t* out,
-                         uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void* stream) {
+int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64_t stride, uint32_t len,
+                         uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t* out,
+                         uint32_t* bad, uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void* stream) {
     if (!shape_ok(G, CPL, fpw)) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
-    RawArgs a{static_cast<uint8_t*>(base), static_cast<const pico_csum_desc_dev*>(desc), stride, len, n,
-              seed, crc_off, flags, fpw, out};
+    RawArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), stride, len, n,
+              seed, crc_off, flags, fpw, out, bad};
     const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define X(g, c)                                                                                 \
@@ -432,12 +440,12 @@ int pico_csum_launch_raw(void* base, const void* desc, uint64_t stride, uint32_t
     return (int)hipErrorInvalidValue;
 }
 
-int pico_csum_launch_ipv4(void* base, const void* desc, uint32_t n, uint32_t flags, uint16_t* out_net,
-                          uint16_t* out_l4, uint8_t* verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
-                          void* stream) {
+int pico_csum_launch_ipv4(void* base, uint64_t base_len, const void* desc, uint32_t n, uint32_t flags,
+                          uint16_t* out_net, uint16_t* out_l4, uint8_t* verdict, uint32_t G, uint32_t CPL,
+                          uint32_t fpw, void* stream) {
     if (!shape_ok(G, CPL, fpw)) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
-    Ipv4Args a{static_cast<uint8_t*>(base), static_cast<const pico_csum_desc_dev*>(desc), n, flags, fpw,
+    Ipv4Args a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, flags, fpw,
                out_net, out_l4, verdict};
     const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);

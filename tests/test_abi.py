@@ -68,18 +68,24 @@ def test_argument_validation():
     lib = _lib.load()
     vp = ctypes.c_void_p
     # odd crc_off
-    assert lib.pico_checksum_batch_dev(vp(0x1000), vp(0x2000), 4, 3, 0, vp(0x3000), None) == -_lib.EINVAL
-    # misaligned descriptors
-    assert lib.pico_checksum_batch_dev(vp(0x1000), vp(0x2008), 4, -1, 0, vp(0x3000), None) == -_lib.EINVAL
-    # F_WRITE without a crc field
-    assert lib.pico_checksum_batch_dev(vp(0x1000), vp(0x2000), 4, -1, _lib.F_WRITE, vp(0x3000), None) == -_lib.EINVAL
-    # F_WRITE on an RX ipv4 batch
-    assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), vp(0x2000), 4, _lib.F_WRITE, None, None, None, None) \
+    assert lib.pico_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, 3, 0, vp(0x3000), None, None) \
         == -_lib.EINVAL
+    # misaligned descriptors
+    assert lib.pico_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2008), 4, -1, 0, vp(0x3000), None, None) \
+        == -_lib.EINVAL
+    # F_WRITE without a crc field
+    assert lib.pico_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, -1, _lib.F_WRITE, vp(0x3000), None,
+                                       None) == -_lib.EINVAL
+    # F_WRITE on an RX ipv4 batch
+    assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_WRITE, None, None, None,
+                                            None) == -_lib.EINVAL
     # NULL buffers
-    assert lib.pico_checksum_batch_uniform_dev(None, 1500, 1500, 4, 0, vp(0x3000), None) == -_lib.EINVAL
+    assert lib.pico_checksum_batch_uniform_dev(None, 6000, 1500, 1500, 4, 0, vp(0x3000), None) == -_lib.EINVAL
+    # frames past base_len
+    assert lib.pico_checksum_batch_uniform_dev(vp(0x1000), 5999, 1500, 1500, 4, 0, vp(0x3000), None) \
+        == -_lib.EINVAL
     # n == 0 is a no-op
-    assert lib.pico_checksum_batch_uniform_dev(None, 1500, 1500, 0, 0, None, None) == 0
+    assert lib.pico_checksum_batch_uniform_dev(None, 0, 1500, 1500, 0, 0, None, None) == 0
     msg = lib.pico_csum_last_error().decode()
     assert isinstance(msg, str)
 
@@ -98,7 +104,7 @@ def test_batch_path_fails_loudly_without_gpu():
     """No CPU fallback: without a HIP device the batched API returns -ENODEV."""
     lib = _lib.load()
     vp = ctypes.c_void_p
-    rc = lib.pico_checksum_batch_uniform_dev(vp(0x1000), 1500, 1500, 4, 0, vp(0x3000), None)
+    rc = lib.pico_checksum_batch_uniform_dev(vp(0x1000), 6000, 1500, 1500, 4, 0, vp(0x3000), None)
     assert rc == -_lib.ENODEV
     assert "HIP device" in lib.pico_csum_last_error().decode()
     from picotcp_amd import batch

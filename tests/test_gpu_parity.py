@@ -120,12 +120,12 @@ def test_desc_crc_field_and_write_roundtrip():
     """crc_off: the field reads as zero; F_WRITE stores short_be(ret) there; the
     region then verifies to 0 -- the TX insert / RX verify round trip."""
     rng = np.random.default_rng(12)
-    buf = synth.random_bytes(7, 1 << 20)
     n = 3000
     lens = rng.integers(12, 1500, n)
     offs = np.zeros(n, dtype=np.uint64)
     offs[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 5, n).astype(np.uint64))[:-1]
     offs += 1
+    buf = synth.random_bytes(7, int(offs[-1]) + int(lens[-1]) + 7)
     seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     desc = batch.make_desc(offs, lens, seeds)
     want = O.batch_raw(buf, desc, crc_off=10)
@@ -145,6 +145,22 @@ def test_desc_crc_field_and_write_roundtrip():
     mask[f] = False
     mask[f + 1] = False
     np.testing.assert_array_equal(after[mask], buf[mask])
+
+
+def test_desc_out_of_bounds_regions_are_not_read():
+    """Descriptors past the buffer: not read, result 0, counted in d_bad; the rest exact."""
+    buf = synth.random_bytes(8, 10000)
+    offs = [0, 9000, 9990, 10000, 10001, 1 << 40, 5000, 100]
+    lens = [1500, 1000, 10, 0, 1, 16, 6000, 200]
+    desc = batch.make_desc(offs, lens)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = u16(batch.checksum_batch(to_dev(buf), batch.desc_to_device(desc, DEV), len(offs), bad=bad))
+    ok = [i for i in range(len(offs)) if offs[i] + lens[i] <= buf.size]
+    want = O.batch_raw(buf, desc[ok])
+    np.testing.assert_array_equal(got[ok], want)
+    oob = [i for i in range(len(offs)) if i not in ok]
+    assert (got[oob] == 0).all()
+    assert int(bad.item()) == len(oob)
 
 
 # ------------------------------------------------------------------ IPv4 fused
@@ -176,6 +192,15 @@ def test_ipv4_every_shape(g, c):
         np.testing.assert_array_equal(u16(net), cs["rx_net"], err_msg=f"g={g} c={c} fpw={fpw}")
         np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"g={g} c={c} fpw={fpw}")
         np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"g={g} c={c} fpw={fpw}")
+
+
+def test_ipv4_out_of_bounds_is_malformed():
+    c = G.unit_socket_frames()
+    net = np.array([0, 64 * 5, 64 * 5 + 1, 1 << 33], dtype=np.uint64)
+    avail = np.array([64, 64, 64, 64], dtype=np.uint32)
+    desc = batch.desc_to_device(G.ipv4_desc(net, avail), DEV)
+    _, _, v = batch.ipv4_checksum_batch(to_dev(c["buf"]), desc, 4)
+    np.testing.assert_array_equal(v.cpu().numpy(), [c["rx_verdict"][0], c["rx_verdict"][5], 8, 8])
 
 
 def test_ipv4_unit_socket_frames():
