@@ -24,7 +24,8 @@
 /* kernels TU (C++/HIP), extern "C" */
 int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64_t stride, uint32_t len,
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
-                         uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void *stream);
+                         uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
+                         int uniform, void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -109,49 +110,64 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
 
 /* ------------------------------------------------------------------ layer 2 */
 
-static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_fpw;
+static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt;
 
-int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t fpw)
+int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt)
 {
-    if (group == 0 && cpl == 0 && fpw == 0) {
-        g_ovr_group = g_ovr_cpl = g_ovr_fpw = 0;
+    if (group == 0 && cpl == 0 && unroll == 0 && fpw == 0 && nt == 0) {
+        g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = 0;
         return 0;
     }
     if (!(group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
         return fail(PICO_CSUM_EINVAL, "group must be 4, 8, 16, 32 or 64");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
+    if (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8)
+        return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
     if (fpw == 0 || fpw > 64 || fpw % (64 / group) != 0)
         return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
-    g_ovr_group = group; g_ovr_cpl = cpl; g_ovr_fpw = fpw;
+    if (nt > 2)
+        return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off) or 2 (on)");
+    g_ovr_group = group; g_ovr_cpl = cpl; g_ovr_unroll = unroll; g_ovr_fpw = fpw; g_ovr_nt = nt;
     return 0;
 }
 
-struct shape { uint32_t G, CPL, fpw; };
+struct shape { uint32_t G, CPL, U, nt, fpw; };
 
-/* Frames per wave: keep >= ~8192 waves (32 per CU on 256 CUs) in the grid
- * when the batch allows, at most 64 (one coalesced result store per wave). */
+/* Launch shape from the typical frame length (measured on MI355X, see
+ * DESIGN.md "Launch shapes"): a lane group spans the frame in about 6-8
+ * 16-byte chunks per lane, all issued in one pass (CPL = 8), so a wave keeps
+ * 8 KiB of loads in flight and the per-frame head/tail corrections and group
+ * reductions are shared by 64/G frames.  Frames per wave: about 16K waves in
+ * the grid (2 residency rounds on 256 CUs) balances the tail; at most 64 (one
+ * coalesced result store per wave).  Non-temporal loads pay on streams of
+ * frames >= 1 KiB (C1 +3 %, C3 +10 %) and cost a little on small IMIX frames. */
 static uint32_t pick_fpw(uint32_t n, uint32_t G)
 {
-    uint32_t ng = 64u / G, f = n / 8192u;
+    uint32_t ng = 64u / G, f = n / 16384u;
     if (f > 64u) f = 64u;
     f -= f % ng;
     if (f < ng) f = ng;
     return f;
 }
 
-static struct shape pick_shape(uint32_t n, uint32_t typical_len)
+static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
 {
     struct shape s;
-    uint32_t chunks = typical_len / 16u + 1u, cpl;
-    if (g_ovr_group) {
-        s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.fpw = g_ovr_fpw;
-        return s;
-    }
-    s.G = chunks >= 48 ? 64 : chunks >= 24 ? 32 : chunks >= 12 ? 16 : chunks >= 6 ? 8 : 4;
-    cpl = (chunks + s.G - 1) / s.G;
-    s.CPL = cpl <= 1 ? 1 : cpl <= 2 ? 2 : cpl <= 4 ? 4 : 8;
+    uint32_t chunks = typical_len / 16u + 1u, per;
+    s.G = 4;
+    while (s.G < 64 && s.G * 8u < chunks)
+        s.G *= 2;
+    per = (chunks + s.G - 1) / s.G;
+    s.CPL = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
+    s.U = 1;
+    s.nt = typical_len >= 1024u;
     s.fpw = pick_fpw(n, s.G);
+    (void)uniform;
+    if (g_ovr_group) {
+        s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
+        s.nt = g_ovr_nt == 2;
+    }
     return s;
 }
 
@@ -183,8 +199,8 @@ static int launch_status(int herr, const char *what)
 }
 
 /* Typical frame length for descriptor batches (unknown on the host without a
- * sync): tuned for the simple-IMIX mean (354 B) .. MTU range. */
-#define DESC_TYPICAL_LEN 512u
+ * sync): the simple-IMIX mean (354 B). */
+#define DESC_TYPICAL_LEN 354u
 
 int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
                             uint32_t n, int32_t crc_off, uint32_t flags, uint16_t *d_out,
@@ -206,9 +222,10 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
         return fail(PICO_CSUM_EINVAL, "F_WRITE needs crc_off >= 0");
     if ((rc = need_device()) != 0)
         return rc;
-    s = pick_shape(n, DESC_TYPICAL_LEN);
+    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
     return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
-                                              d_bad, s.G, s.CPL, s.fpw, 0, stream), "pico_checksum_batch_dev");
+                                              d_bad, s.G, s.CPL, s.U, s.nt, s.fpw, 0, stream),
+                         "pico_checksum_batch_dev");
 }
 
 int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint64_t stride, uint32_t len,
@@ -225,9 +242,9 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return fail(PICO_CSUM_EINVAL, "frames exceed base_len");
     if ((rc = need_device()) != 0)
         return rc;
-    s = pick_shape(n, len);
+    s = pick_shape(n, len, 1);
     return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
-                                              d_out, NULL, s.G, s.CPL, s.fpw, 1, stream),
+                                              d_out, NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, stream),
                          "pico_checksum_batch_uniform_dev");
 }
 
@@ -249,7 +266,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0)
         return rc;
-    s = pick_shape(n, DESC_TYPICAL_LEN);
+    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
     return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),
                          "pico_ipv4_checksum_batch_dev");
@@ -357,9 +374,9 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
         /* staging buffer b is free once its previous chunk's D2H is done (same stream: ordered) */
         e = hipMemcpyAsync(c->d_buf[b], src, bytes, hipMemcpyHostToDevice, c->st[b]);
         if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "H2D: %s", hipGetErrorString(e)); break; }
-        s = pick_shape(cnt, len);
+        s = pick_shape(cnt, len, 1);
         rc = launch_status(pico_csum_launch_raw(c->d_buf[b], c->staging, NULL, stride, len, cnt, seed, -1, 0,
-                                                c->d_out[b], NULL, s.G, s.CPL, s.fpw, 1, c->st[b]),
+                                                c->d_out[b], NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, c->st[b]),
                            "pico_checksum_batch_uniform_host");
         if (rc) break;
         e = hipMemcpyAsync(out + first, c->d_out[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]);

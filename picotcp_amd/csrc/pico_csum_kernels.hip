@@ -25,6 +25,7 @@
 //   * No MFMA: this is an HBM-bound byte reduction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace {
 
@@ -51,6 +52,23 @@ __device__ __forceinline__ uint32_t add_chunk(const uint4 v, uint32_t m16, uint3
     return acc;
 }
 
+// Adds all 16 bytes of chunk v (frame-relative pairing via sel when PERM).
+template <bool PERM>
+__device__ __forceinline__ uint32_t add_full(const uint4 v, uint32_t sel, uint32_t acc) {
+    if constexpr (PERM) {
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.x, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.y, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.z, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.w, sel), acc);
+    } else {
+        acc = dot2_add(v.x, acc);
+        acc = dot2_add(v.y, acc);
+        acc = dot2_add(v.z, acc);
+        acc = dot2_add(v.w, acc);
+    }
+    return acc;
+}
+
 // Bits [lo, hi) of a 16-bit chunk mask; lo, hi in [0, 16].
 __device__ __forceinline__ uint32_t bits16(uint32_t lo, uint32_t hi) {
     return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
@@ -72,14 +90,18 @@ __device__ __forceinline__ uint32_t clear_field(uint32_t m, int64_t d) {
     return m & ~((3u << sh) >> 1);
 }
 
+// Sum over a lane group of G lanes (G | 64, groups aligned).  The total lands in
+// the group's LAST lane (lane g*G + G-1); for G <= 16 every lane of the group has it.
+// DPP only: quad_perm xor1/xor2, row_half_mirror, row_mirror, then row_bcast:15
+// (rows 1,3 += lane 15 of the row below) and row_bcast:31 (rows 2,3 += lane 31).
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
-    if constexpr (G >= 2)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    if constexpr (G >= 4)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    if constexpr (G >= 8)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
-    if constexpr (G >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
-    if constexpr (G >= 32) v += (uint32_t)__shfl_xor((int)v, 16);
-    if constexpr (G >= 64) v += (uint32_t)__shfl_xor((int)v, 32);
+    if constexpr (G >= 2)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    if constexpr (G >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
     return v;
 }
 
@@ -101,18 +123,35 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* a0, uint32_t k) {
     return *reinterpret_cast<const uint4*>(a0 + ((uint64_t)k << 4));
 }
 
-// Hands the per-group result of iteration i to lane (i + g): lane j of the wave
-// ends up holding the result of the wave's frame j.
+// Hands the group results of one iteration to lanes base..base+NG-1: lane base+g
+// receives the value group g holds in its last lane.  Lane j of the wave thus ends
+// up with the result of the wave's frame j (one coalesced store per wave later).
 template <int G>
-__device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t lane, uint32_t i) {
+__device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t lane, uint32_t base) {
     constexpr uint32_t NG = 64 / G;
-    if constexpr (NG == 1) {
-        return lane == i ? val : res;
+    if constexpr (NG <= 4) {
+#pragma unroll
+        for (uint32_t g = 0; g < NG; ++g) {
+            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)(g * G + G - 1));
+            res = (lane == base + g) ? s : res;
+        }
+        return res;
     } else {
-        const uint32_t src = ((lane - i) & (NG - 1)) * G;
+        const uint32_t src = ((lane - base) & (NG - 1)) * G + (G - 1);
         const uint32_t got = (uint32_t)__shfl((int)val, (int)src);
-        return (lane >= i && lane < i + NG) ? got : res;
+        return (lane >= base && lane < base + NG) ? got : res;
     }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 load_chunk_t(const uint8_t* a0, uint32_t k) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(a0 + ((uint64_t)k << 4));
+    u32x4 x;
+    if constexpr (NT) x = __builtin_nontemporal_load(q);
+    else x = *q;
+    return make_uint4(x.x, x.y, x.z, x.w);
 }
 
 }  // namespace
@@ -143,7 +182,10 @@ struct RawArgs {
 
 // RAW batch: per-frame pico_checksum / pico_dualbuffer_checksum.
 // UNIFORM: frame i = base + i*stride, len, seed (no descriptors).
-template <int G, int CPL, bool UNIFORM>
+// Each lane group keeps U frames in flight: one pass issues U*CPL dwordx4 loads
+// per lane before any of them is consumed, so a wave has U*CPL KiB (G=64) of
+// reads outstanding while earlier frames are being reduced.
+template <int G, int CPL, int U, bool UNIFORM, bool NT>
 __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
     constexpr uint32_t NG = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
@@ -162,59 +204,100 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
     }
 
     uint32_t res = 0;
-    for (uint32_t i = 0; i < cnt; i += NG) {
-        const uint32_t j = i + g;
-        uint64_t off;
-        uint32_t len, seed;
-        if constexpr (UNIFORM) {
-            off = (f0 + j) * p.stride;
-            len = p.len;
-            seed = p.seed;
-        } else {
-            const uint32_t lo = (uint32_t)__shfl((int)d_lo, (int)j);
-            const uint32_t hi = (uint32_t)__shfl((int)d_hi, (int)j);
-            off = ((uint64_t)hi << 32) | lo;
-            len = (uint32_t)__shfl((int)d_len, (int)j);
-            seed = (uint32_t)__shfl((int)d_seed, (int)j);
-        }
-        if (j >= cnt) len = 0;
-        // a region outside the batch buffer is never read (include/pico_csum.h)
-        const bool oob = !UNIFORM && j < cnt && (off > p.base_len || len > p.base_len - off);
-        if (oob) len = 0;
-
-        uint8_t* fp = p.base + off;
-        const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
-        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
-        const uint32_t r = (uint32_t)(a & 15u);
-        const uint64_t span = (uint64_t)r + len;
-        const uint32_t nchunks = len ? (uint32_t)((span + 15u) >> 4) : 0u;
-        const uint32_t sel = (a & 1u) ? SEL_ODD : SEL_EVEN;
-        const bool has_crc = p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len;
-        const int64_t xr = has_crc ? (int64_t)r + p.crc_off : (int64_t)1 << 40;
-
-        uint32_t acc = 0;
-        for (uint32_t kb = 0; kb < nchunks; kb += G * CPL) {
-            uint4 v[CPL];
+    for (uint32_t i = 0; i < cnt; i += NG * U) {
+        uint8_t* fp[U];
+        const uint8_t* a0[U];
+        uint32_t r[U], nch[U], sel[U], seed[U], acc[U];
+        uint64_t span[U];
+        int64_t xr[U];
+        bool oob[U], has_crc[U];
+        uint32_t maxch = 0;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t k = kb + l + G * c;
-                v[c] = k < nchunks ? load_chunk(a0, k) : make_uint4(0, 0, 0, 0);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = i + u * NG + g;
+            uint64_t off;
+            uint32_t len;
+            if constexpr (UNIFORM) {
+                off = (f0 + j) * p.stride;
+                len = p.len;
+                seed[u] = p.seed;
+            } else {
+                const uint32_t lo = (uint32_t)__shfl((int)d_lo, (int)j);
+                const uint32_t hi = (uint32_t)__shfl((int)d_hi, (int)j);
+                off = ((uint64_t)hi << 32) | lo;
+                len = (uint32_t)__shfl((int)d_len, (int)j);
+                seed[u] = (uint32_t)__shfl((int)d_seed, (int)j);
             }
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t k = kb + l + G * c;
-                if (k < nchunks) {
-                    uint32_t m = chunk_range_mask(k, r, span);
-                    m = clear_field(m, xr - ((int64_t)k << 4));
-                    acc = add_chunk(v[c], m, sel, acc);
-                }
-            }
+            if (j >= cnt) len = 0;
+            // a region outside the batch buffer is never read (include/pico_csum.h)
+            oob[u] = !UNIFORM && j < cnt && (off > p.base_len || len > p.base_len - off);
+            if (oob[u]) len = 0;
+            fp[u] = p.base + off;
+            const uintptr_t a = reinterpret_cast<uintptr_t>(fp[u]);
+            r[u] = (uint32_t)(a & 15u);
+            a0[u] = fp[u] - r[u];          // stays a global pointer: global_load, not flat_load
+            span[u] = (uint64_t)r[u] + len;
+            nch[u] = len ? (uint32_t)((span[u] + 15u) >> 4) : 0u;
+            sel[u] = (a & 1u) ? SEL_ODD : SEL_EVEN;
+            has_crc[u] = p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len;
+            xr[u] = has_crc[u] ? (int64_t)r[u] + p.crc_off : (int64_t)1 << 40;
+            acc[u] = 0;
+            maxch = max(maxch, nch[u]);
         }
-        const uint32_t ret = oob ? 0u : finalize(group_sum<G>(acc) + seed);
-        if ((p.flags & 1u) && has_crc && l == 0 && j < cnt)
-            store_crc(fp + p.crc_off, ret);
-        if (oob && l == 0 && p.bad) atomicAdd(p.bad, 1u);
-        res = collect<G>(res, ret, lane, i);
+
+        // Chunks [1, nch-2] lie wholly inside the frame: they are added unmasked.
+        // The head chunk (k = 0), the tail chunk (k = nch-1) and the chunk(s)
+        // holding the crc field are added unmasked too, then the bytes that do not
+        // count are subtracted again (exact: every sum is mod 2^32).
+        uint32_t xk0[U], xk1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            xk0[u] = has_crc[u] ? (uint32_t)(xr[u] >> 4) : 0u;
+            xk1[u] = has_crc[u] ? (uint32_t)((xr[u] + 1) >> 4) : 0u;
+        }
+        bool any_odd = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) any_odd |= (sel[u] != SEL_EVEN);
+        any_odd = __builtin_amdgcn_ballot_w64(any_odd) != 0;
+
+        auto pass = [&](auto perm_tag) {
+            constexpr bool PERM = decltype(perm_tag)::value;
+            for (uint32_t kb = 0; kb < maxch; kb += G * CPL) {
+                uint4 v[U][CPL];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) {
+                        const uint32_t k = kb + l + G * c;
+                        v[u][c] = k < nch[u] ? load_chunk_t<NT>(a0[u], k) : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) {
+                        const uint32_t k = kb + l + G * c;
+                        acc[u] = add_full<PERM>(v[u][c], sel[u], acc[u]);
+                        const bool edge = k < nch[u] && (k == 0 || k + 1 == nch[u] || k == xk0[u] || k == xk1[u]);
+                        if (edge) {
+                            uint32_t m = chunk_range_mask(k, r[u], span[u]);
+                            m = clear_field(m, xr[u] - ((int64_t)k << 4));
+                            acc[u] -= add_chunk(v[u][c], ~m & 0xFFFFu, sel[u], 0u);
+                        }
+                    }
+            }
+        };
+        if (any_odd) pass(std::integral_constant<bool, true>{});
+        else pass(std::integral_constant<bool, false>{});
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = i + u * NG + g;
+            const uint32_t ret = oob[u] ? 0u : finalize(group_sum<G>(acc[u]) + seed[u]);
+            if (l == G - 1 && j < cnt) {
+                if ((p.flags & 1u) && has_crc[u]) store_crc(fp[u] + p.crc_off, ret);
+                if (oob[u] && p.bad) atomicAdd(p.bad, 1u);
+            }
+            res = collect<G>(res, ret, lane, i + u * NG);
+        }
     }
     if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
 }
@@ -268,8 +351,8 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
         if (j >= cnt || off > p.base_len || avail > p.base_len - off) avail = 0;   // unread -> MALFORMED
         uint8_t* fp = p.base + off;
         const uintptr_t a = reinterpret_cast<uintptr_t>(fp);
-        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
         const uint32_t r = (uint32_t)(a & 15u);
+        const uint8_t* a0 = fp - r;
         const uint32_t sel = (a & 1u) ? SEL_ODD : SEL_EVEN;
 
         // ---- header parse: chunks 0..2 cover header bytes [0, 20); every lane
@@ -377,7 +460,7 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
             if (verdict == 0) verdict = V_ACCEPT;
         }
 
-        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l == 0 && j < cnt) {
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l == G - 1 && j < cnt) {
             store_crc(fp + 10, net);
             if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + xoff, l4);
             else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
@@ -395,12 +478,19 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
 
 // ---------------------------------------------------------------- dispatch
 
+// (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
+// group) and NT (non-temporal loads), with CPL*U <= 8 (<= 32 data VGPRs).
 #define PICO_FOR_SHAPES(X) \
     X(64, 1) X(64, 2) X(64, 4) X(64, 8) \
     X(32, 1) X(32, 2) X(32, 4) X(32, 8) \
     X(16, 1) X(16, 2) X(16, 4) X(16, 8) \
     X(8, 1)  X(8, 2)  X(8, 4)  X(8, 8)  \
     X(4, 1)  X(4, 2)  X(4, 4)  X(4, 8)
+
+#define PICO_FOR_CU(Y, g) \
+    Y(g, 1, 1) Y(g, 2, 1) Y(g, 4, 1) Y(g, 8, 1) Y(g, 1, 2) Y(g, 2, 2) Y(g, 4, 2) Y(g, 1, 4) Y(g, 2, 4)
+
+#define PICO_FOR_RAW(Y) PICO_FOR_CU(Y, 64) PICO_FOR_CU(Y, 32) PICO_FOR_CU(Y, 16) PICO_FOR_CU(Y, 8) PICO_FOR_CU(Y, 4)
 
 inline bool shape_ok(uint32_t G, uint32_t CPL, uint32_t fpw) {
     if (!(G == 4 || G == 8 || G == 16 || G == 32 || G == 64)) return false;
@@ -422,21 +512,27 @@ extern "C" {
 
 int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64_t stride, uint32_t len,
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t* out,
-                         uint32_t* bad, uint32_t G, uint32_t CPL, uint32_t fpw, int uniform, void* stream) {
-    if (!shape_ok(G, CPL, fpw)) return (int)hipErrorInvalidValue;
+                         uint32_t* bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
+                         int uniform, void* stream) {
+    if (!shape_ok(G, CPL, fpw) || !(U == 1 || U == 2 || U == 4) || CPL * U > 8) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     RawArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), stride, len, n,
               seed, crc_off, flags, fpw, out, bad};
     const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);
-#define X(g, c)                                                                                 \
-    if (G == g && CPL == c) {                                                                   \
-        if (uniform) hipLaunchKernelGGL((csum_raw_kernel<g, c, true>), grid, block, 0, s, a);   \
-        else hipLaunchKernelGGL((csum_raw_kernel<g, c, false>), grid, block, 0, s, a);          \
-        return (int)hipGetLastError();                                                          \
+#define Y(g, c, u)                                                                                          \
+    if (G == g && CPL == c && U == u) {                                                                     \
+        if (uniform) {                                                                                      \
+            if (nt) hipLaunchKernelGGL((csum_raw_kernel<g, c, u, true, true>), grid, block, 0, s, a);       \
+            else hipLaunchKernelGGL((csum_raw_kernel<g, c, u, true, false>), grid, block, 0, s, a);         \
+        } else {                                                                                            \
+            if (nt) hipLaunchKernelGGL((csum_raw_kernel<g, c, u, false, true>), grid, block, 0, s, a);      \
+            else hipLaunchKernelGGL((csum_raw_kernel<g, c, u, false, false>), grid, block, 0, s, a);        \
+        }                                                                                                   \
+        return (int)hipGetLastError();                                                                      \
     }
-    PICO_FOR_SHAPES(X)
-#undef X
+    PICO_FOR_RAW(Y)
+#undef Y
     return (int)hipErrorInvalidValue;
 }
 

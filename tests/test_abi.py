@@ -92,11 +92,13 @@ def test_argument_validation():
 
 def test_launch_override_validation():
     lib = _lib.load()
-    assert lib.pico_csum_set_launch_override(12, 2, 16) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(16, 3, 16) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(16, 2, 6) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(16, 2, 16) == 0
-    assert lib.pico_csum_set_launch_override(0, 0, 0) == 0
+    assert lib.pico_csum_set_launch_override(12, 2, 1, 16, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 3, 1, 16, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 2, 1, 6, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 4, 4, 16, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 3) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 2, 4, 16, 2) == 0
+    assert lib.pico_csum_set_launch_override(0, 0, 0, 0, 0) == 0
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device error path")

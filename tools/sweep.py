@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep in ONE process, variants interleaved over rounds
+(cdna_hip_programming.md 5.4 rule 24).  Prints one JSON line per (config, shape)
+with the median kernel time and the achieved algorithmic GB/s.
+
+  python tools/sweep.py --config c1 --rounds 5 --shapes 64,2,2,32,1 64,2,1,32,1 ...
+  shape = G,CPL,U,FPW,NT   (NT: 1 plain loads, 2 non-temporal)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from picotcp_amd import batch, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--shapes", nargs="*", default=[])
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    if a.config in ("c1", "c3", "c3_64k", "c1_1536"):
+        n, ln, stride = {"c1": (262144, 1500, 1500), "c3": (262144, 9000, 9000), "c3_64k": (16384, 65536, 65536),
+                         "c1_1536": (262144, 1500, 1536)}[a.config]
+        per = (n - 1) * stride + ln
+        rot = max(3, -(-(3 << 30) // per) // 2)
+        bufs = [torch.randint(0, 256, (per,), dtype=torch.uint8, device=dev) for _ in range(rot)]
+        outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
+
+        def launch(i):
+            batch.checksum_uniform(bufs[i % rot], stride, ln, n, out=outs[i % rot])
+        algo = n * ln + 2 * n
+    elif a.config in ("c2raw", "c2"):
+        n = 262144
+        lens = synth.imix_lengths(n, 3)
+        rot = 3
+        sets = []
+        for r in range(rot):
+            buf, net, avail = synth.ipv4_batch(lens, seed=10 + r, proto=6, eth=True)
+            d_buf = torch.from_numpy(buf).to(dev)
+            d_desc = batch.desc_to_device(batch.make_desc(net, avail), dev)
+            batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+            sets.append((d_buf, d_desc))
+        outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
+        if a.config == "c2raw":
+            def launch(i):
+                b, d = sets[i % rot]
+                batch.checksum_batch(b, d, n, out=outs[i % rot])
+        else:
+            def launch(i):
+                b, d = sets[i % rot]
+                batch.ipv4_checksum_batch(b, d, n)
+        algo = int(lens.sum()) + 16 * n + (2 if a.config == "c2raw" else 5) * n
+    else:
+        raise SystemExit("unknown config")
+
+    shapes = [tuple(int(x) for x in s.split(",")) for s in a.shapes] or [(0, 0, 0, 0, 0)]
+    times = {s: [] for s in shapes}
+    stream = torch.cuda.current_stream()
+    for rnd in range(a.rounds):
+        for s in shapes:
+            g, c, u, f, nt = s
+            batch.set_launch_override(g, c, f, u, nt)
+            for i in range(3):
+                launch(i)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+            for i in range(a.iters):
+                evs[i][0].record(stream)
+                launch(i)
+                evs[i][1].record(stream)
+            torch.cuda.synchronize()
+            times[s].append(float(np.median([x.elapsed_time(y) for x, y in evs])))
+    batch.set_launch_override(0)
+    for s in shapes:
+        t = float(np.median(times[s]))
+        print(json.dumps({"config": a.config, "shape": "auto" if s[0] == 0 else ",".join(map(str, s)),
+                          "us": round(t * 1e3, 2), "us_min_round": round(min(times[s]) * 1e3, 2),
+                          "GBs": round(algo / (t / 1e3) / 1e9, 1), "frac": round(algo / (t / 1e3) / 8e12, 4)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
