@@ -14,8 +14,8 @@ are independent shards; no collective touches the data path -- RCCL only carries
 barrier and the max-over-ranks timing).
 
 Rank 0 prints ONE JSON line.  `roofline` is the checksum kernel's achieved algorithmic HBM
-bandwidth (HIP events around every launch on the launch stream) against the 8.0 TB/s
-HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch from profiles/ (gfx950
+bandwidth (HIP events bracketing the K timed launches on the launch stream; elapsed / K =
+average launch duration) against the 8.0 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch from profiles/ (gfx950
 FETCH_SIZE x2 correction, rocprofv3 separate passes) when recorded for this config;
 `cpu_baseline` times the reference's own pico_checksum (compiled from stack/pico_frame.c,
 oracle/_ref) on the host cores over a bounded sample of the same frames.
@@ -67,7 +67,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU-baseline wall per leg")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
-    p.add_argument("--shape", default="", help="G,CPL,FPW launch override (sweeps)")
+    p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
     return p.parse_args()
 
 
@@ -193,21 +193,23 @@ def main():
         step(i)
     torch.cuda.synchronize(dev)
 
-    # per-launch HIP events on the launch stream (kernel duration) ...
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # HIP events on the launch stream bracket the timed region: their elapsed
+    # time / K is the average launch duration (kernel + the ~1-2 us dependent
+    # kernel boundary), the figure the roofline fraction uses.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(a.steps):
-        ev[i][0].record(stream)
         step(i)
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
 
     # ... and whole-job time = max over ranks
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)

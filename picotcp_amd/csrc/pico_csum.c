@@ -26,6 +26,10 @@ int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
                          uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
                          int uniform, void *stream);
+int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int ipv4,
+                          int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
+                          uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
+                          void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -118,13 +122,13 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = 0;
         return 0;
     }
-    if (!(group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
-        return fail(PICO_CSUM_EINVAL, "group must be 4, 8, 16, 32 or 64");
+    if (!(group == 1 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
+        return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 4, 8, 16, 32 or 64");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
     if (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8)
         return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
-    if (fpw == 0 || fpw > 64 || fpw % (64 / group) != 0)
+    if (fpw == 0 || fpw > 64 || (group > 1 && fpw % (64 / group) != 0))
         return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
     if (nt > 2)
         return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off) or 2 (on)");
@@ -223,6 +227,10 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (s.G == 1)
+        return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
+                                                   NULL, NULL, NULL, s.CPL, s.nt, s.fpw, stream),
+                             "pico_checksum_batch_dev");
     return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
                                               d_bad, s.G, s.CPL, s.U, s.nt, s.fpw, 0, stream),
                          "pico_checksum_batch_dev");
@@ -243,6 +251,8 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, len, 1);
+    if (s.G == 1)
+        return fail(PICO_CSUM_EINVAL, "the flat kernel (group 1) serves descriptor batches only");
     return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
                                               d_out, NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, stream),
                          "pico_checksum_batch_uniform_dev");
@@ -267,6 +277,11 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (s.G == 1)
+        return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
+                                                   d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
+                                                   stream),
+                             "pico_ipv4_checksum_batch_dev");
     return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),
                          "pico_ipv4_checksum_batch_dev");

@@ -476,6 +476,289 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
     }
 }
 
+// ---------------------------------------------------------------- flat work-list kernel
+//
+// Descriptor batches of mixed lengths (C2 simple-IMIX, 64..1500 B).  A lane group
+// per frame leaves most lanes idle when a wave's frames differ in size, so here
+// a wave takes up to 64 frames and streams them as ONE list of 16-byte chunks:
+//   1. lane j owns frame j: reads its descriptor (and, IPv4, parses its header),
+//      computes the chunks it spans, and a DPP prefix scan turns the counts into
+//      start indices S[j] (per-wave LDS);
+//   2. every lane walks consecutive virtual chunks t = t0 + 64c + lane, so each
+//      load instruction covers 1 KiB that is contiguous whenever the frames are
+//      packed, whatever their sizes; the frame of t is a 6-step binary search in
+//      S; bytes outside the frame (head/tail) or inside an isolated field are
+//      corrected exactly as in the lane-group kernel;
+//   3. per-lane chunk sums are folded per frame by a DPP segmented scan (key =
+//      frame index) and the last lane of each run adds into the frame's LDS
+//      accumulator (ds_add_u32, conflict-free: one adder per frame per slot);
+//   4. lane j finalizes frame j: one coalesced store per output per wave.
+
+// Inclusive prefix sum over the 64 lanes (DPP row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+// Inclusive segmented prefix sum: lanes with equal (non-decreasing) key form runs.
+__device__ __forceinline__ uint32_t seg_scan_add(uint32_t v, uint32_t key) {
+#define PICO_SEG_STEP(ctrl, rmask)                                                              \
+    {                                                                                           \
+        const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, rmask, 0xF, false);  \
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)key, ctrl, rmask, 0xF, false); \
+        v += (pk == key) ? pv : 0u;                                                             \
+    }
+    PICO_SEG_STEP(0x111, 0xF)
+    PICO_SEG_STEP(0x112, 0xF)
+    PICO_SEG_STEP(0x114, 0xF)
+    PICO_SEG_STEP(0x118, 0xF)
+    PICO_SEG_STEP(0x142, 0xA)
+    PICO_SEG_STEP(0x143, 0xC)
+#undef PICO_SEG_STEP
+    return v;
+}
+
+struct FlatArgs {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint32_t fpw;
+    int32_t crc_off;      // RAW
+    uint32_t flags;
+    uint16_t* out;        // RAW
+    uint32_t* bad;        // RAW
+    uint16_t* out_net;    // IPV4
+    uint16_t* out_l4;
+    uint8_t* verdict;
+};
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+struct FlatWaveLds {
+    uint32_t S[64];        // exclusive prefix of chunk counts
+    uint32_t acc_all[64];  // bytes [0, span) of the frame
+    uint32_t acc_x[64];    // the isolated 2-byte field (RAW crc / UDP crc / TX crc)
+    uint32_t acc_opt[64];  // IPv4 option bytes [20, hl)
+    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4}
+    uint2 xo[64];          // {field position r + xoff (NONE), option end r + hl (0)}
+};
+
+template <bool IPV4, int CPL, bool NT>
+__global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
+    __shared__ FlatWaveLds lds_all[4];
+    const uint32_t lane = threadIdx.x & 63u;
+    FlatWaveLds& L = lds_all[threadIdx.x >> 6];
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const bool tx = IPV4 && (p.flags & 2u) != 0;
+
+    // ---- 1. lane j = frame j
+    uint64_t off = 0;
+    uint32_t len = 0, seed = 0;
+    if (lane < cnt) {
+        const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+        off = ((uint64_t)d.y << 32) | d.x;
+        len = d.z;
+        seed = d.w;
+    }
+    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
+    if (oob) len = 0;
+    uint8_t* fp = p.base + off;
+    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+    const uint64_t a0off = off - r;
+    const uint32_t odd = r & 1u;
+
+    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
+    // IPv4 per-frame state
+    uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
+    bool parsed = false, l4_needed = false;
+    if constexpr (!IPV4) {
+        span = ext = len;
+        if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
+    } else {
+        const uint32_t avail = len;
+        if (avail >= 20) {
+            const uint8_t* a0 = p.base + a0off;
+            const uint4 c0 = load_chunk(a0, 0);
+            const uint4 c1 = (r + 20 > 16) ? load_chunk(a0, 1) : make_uint4(0, 0, 0, 0);
+            const uint4 c2 = (r + 20 > 32) ? load_chunk(a0, 2) : make_uint4(0, 0, 0, 0);
+            const uint32_t D[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+            const uint32_t q = r >> 2, sh = r & 3u;
+            uint32_t E[6];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+            uint32_t H[5];
+#pragma unroll
+            for (int m = 0; m < 5; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+            const uint32_t ihl = H[0] & 0x0Fu;
+            hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+            const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+            proto = (H[2] >> 8) & 0xFFu;
+            ipcrc = H[2] >> 16;
+            tl = (tot - hl) & 0xFFFFu;                              // uint16 wrap, pico_ipv4.c:395
+            const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;   // pico_ipv4.c:386
+            if (!(hl > avail || (!tx && tl > max_allowed) || hl + tl > avail)) {
+                parsed = true;
+                verdict = 0;
+                span = ext = hl + tl;
+#pragma unroll
+                for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
+                pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
+                         (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
+                if (hl > 20u) optend = r + hl;
+                if (!tx) {
+                    if (proto == 6u) {
+                        l4_needed = true;
+                    } else if (proto == 17u) {
+                        if (hl + 8u > avail) verdict |= V_MALFORMED;
+                        else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
+                    }
+                } else {
+                    if (proto == 6u) {
+                        if (tl < 20u) verdict |= V_MALFORMED;
+                        else { l4_needed = true; xpos = r + hl + 16u; }
+                    } else if (proto == 1u) {
+                        if (tl < 8u) verdict |= V_MALFORMED;
+                        else { l4_needed = true; xpos = r + hl + 2u; }
+                    }
+                }
+            }
+        }
+    }
+    const uint32_t nch = ext ? (r + ext + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_scan_add(nch);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t S = incl - nch;
+    const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
+    const bool any_x = __builtin_amdgcn_ballot_w64(nch != 0 && xpos != NONE) != 0;
+    const bool any_opt = IPV4 && __builtin_amdgcn_ballot_w64(nch != 0 && optend != 0) != 0;
+    L.S[lane] = lane < cnt ? S : T;
+    L.acc_all[lane] = 0;
+    L.acc_x[lane] = 0;
+    L.acc_opt[lane] = 0;
+    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4));
+    L.xo[lane] = make_uint2(xpos, optend);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- 2. stream the wave's chunk list
+    auto stream = [&](auto perm_tag) {
+        constexpr bool PERM = decltype(perm_tag)::value;
+        for (uint32_t t0 = 0; t0 < T; t0 += 64u * CPL) {
+            uint4 v[CPL];
+            uint32_t jj[CPL], kk[CPL];
+            uint4 fi[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t t = t0 + 64u * c + lane;
+                uint32_t j = 0, sj = 0;
+#pragma unroll
+                for (uint32_t step = 32; step; step >>= 1) {
+                    const uint32_t s2 = L.S[j + step];
+                    if (s2 <= t) { j += step; sj = s2; }
+                }
+                jj[c] = j;
+                kk[c] = t - sj;
+                fi[c] = L.info[j];
+                const uint8_t* a0 = p.base + ((((uint64_t)fi[c].y) << 32) | fi[c].x);
+                v[c] = t < T ? load_chunk_t<NT>(a0, kk[c]) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t t = t0 + 64u * c + lane;
+                const bool valid = t < T;
+                const uint32_t k = kk[c], j = jj[c];
+                const uint32_t rr = fi[c].w & 15u;
+                const uint32_t sl = (fi[c].w & 16u) ? SEL_ODD : SEL_EVEN;
+                const uint32_t send = fi[c].z;
+                uint32_t x = add_full<PERM>(v[c], sl, 0u);
+                const uint32_t ch = k << 4;
+                if (valid && (ch < rr || ch + 16u > send)) {
+                    const uint32_t m = chunk_range_mask(k, rr, send);
+                    x -= add_chunk(v[c], ~m & 0xFFFFu, sl, 0u);
+                }
+                if (any_x || any_opt) {
+                    const uint2 xo = L.xo[j];
+                    if (any_x && valid && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4))) {
+                        const uint32_t xv = add_chunk(v[c], chunk_range_mask(k, xo.x, (uint64_t)xo.x + 2u), sl, 0u);
+                        if (xv) atomicAdd(&L.acc_x[j], xv);
+                    }
+                    if (IPV4 && any_opt && valid && xo.y != 0u && ch < xo.y) {
+                        const uint32_t ov = add_chunk(v[c], chunk_range_mask(k, rr + 20u, xo.y), sl, 0u);
+                        if (ov) atomicAdd(&L.acc_opt[j], ov);
+                    }
+                }
+                if (!valid) x = 0;
+                const uint32_t key = valid ? j : 0xFFFFFFFEu;
+                const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+                const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
+                if (k0 == k63) {                       // the whole slot is one frame
+                    const uint32_t tot = group_sum<64>(x);
+                    if (lane == 63 && valid) atomicAdd(&L.acc_all[j], tot);
+                } else {
+                    const uint32_t run = seg_scan_add(x, key);
+                    const uint32_t nk = (uint32_t)__shfl_down((int)key, 1);
+                    if (valid && (lane == 63 || nk != key)) atomicAdd(&L.acc_all[j], run);
+                }
+            }
+        }
+    };
+    if (any_odd) stream(std::integral_constant<bool, true>{});
+    else stream(std::integral_constant<bool, false>{});
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS atomics are done
+
+    // ---- 3. lane j finalizes frame j
+    if (lane >= cnt) return;
+    const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
+    if constexpr (!IPV4) {
+        uint32_t ret = 0;
+        if (oob) {
+            if (p.bad) atomicAdd(p.bad, 1u);
+        } else {
+            ret = finalize(seed + acc_all - acc_x);
+            if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
+        }
+        p.out[f0 + lane] = (uint16_t)ret;
+    } else {
+        uint32_t net = 0, l4 = 0;
+        if (parsed) {
+            const uint32_t acc_hdr = hdr20 + acc_opt;
+            net = finalize(acc_hdr - (tx ? ipcrc : 0u));
+            if (!tx && net != 0) verdict |= V_NET_BAD;
+            const uint32_t tsum = acc_all - acc_hdr;
+            if (l4_needed) {
+                if (!tx) {
+                    if (proto == 6u || acc_x != 0u) {
+                        l4 = finalize(pseudo + tsum);
+                        if (l4 != 0) verdict |= V_L4_BAD;
+                    }
+                } else if (proto == 6u) {
+                    l4 = finalize(pseudo + tsum - acc_x);
+                } else {
+                    l4 = finalize(tsum - acc_x);
+                }
+            }
+            if (verdict == 0) verdict = V_ACCEPT;
+        }
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
+            store_crc(fp + 10, net);
+            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
+            else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+        }
+        if (p.out_net) p.out_net[f0 + lane] = (uint16_t)net;
+        if (p.out_l4) p.out_l4[f0 + lane] = (uint16_t)l4;
+        if (p.verdict) p.verdict[f0 + lane] = (uint8_t)verdict;
+    }
+}
+
 // ---------------------------------------------------------------- dispatch
 
 // (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
@@ -533,6 +816,33 @@ int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64
     }
     PICO_FOR_RAW(Y)
 #undef Y
+    return (int)hipErrorInvalidValue;
+}
+
+// Flat work-list kernel for descriptor batches: ipv4 = 0 RAW, 1 fused IPv4.
+int pico_csum_launch_flat(void* base, uint64_t base_len, const void* desc, uint32_t n, int ipv4,
+                          int32_t crc_off, uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net,
+                          uint16_t* out_l4, uint8_t* verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
+                          void* stream) {
+    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8) || fpw < 1 || fpw > 64) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
+               crc_off, flags, out, bad, out_net, out_l4, verdict};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define Z(c)                                                                                        \
+    if (CPL == c) {                                                                                 \
+        if (ipv4) {                                                                                 \
+            if (nt) hipLaunchKernelGGL((csum_flat_kernel<true, c, true>), grid, block, 0, s, a);    \
+            else hipLaunchKernelGGL((csum_flat_kernel<true, c, false>), grid, block, 0, s, a);      \
+        } else {                                                                                    \
+            if (nt) hipLaunchKernelGGL((csum_flat_kernel<false, c, true>), grid, block, 0, s, a);   \
+            else hipLaunchKernelGGL((csum_flat_kernel<false, c, false>), grid, block, 0, s, a);     \
+        }                                                                                           \
+        return (int)hipGetLastError();                                                              \
+    }
+    Z(1) Z(2) Z(4) Z(8)
+#undef Z
     return (int)hipErrorInvalidValue;
 }
 

@@ -14,6 +14,12 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
+# descriptor batches also run on the flat work-list kernel (group 1)
+DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)]
+
+
+def fpws(g):
+    return (1, 13, 64) if g == 1 else sorted({64 // g, 64})
 
 
 def u16(t: torch.Tensor) -> np.ndarray:
@@ -91,12 +97,12 @@ def test_desc_golden(name):
     np.testing.assert_array_equal(got, case["expected"])
 
 
-@pytest.mark.parametrize("g,c", SHAPES)
+@pytest.mark.parametrize("g,c", DESC_SHAPES)
 def test_desc_every_shape(g, c):
     case = G.raw_cases()["mixed_align"]
     buf, desc = G.raw_case_inputs(case, lambda b: O.adder(0, b))
     d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
-    for fpw in sorted({64 // g, 64}):
+    for fpw in fpws(g):
         batch.set_launch_override(g, c, fpw)
         got = u16(batch.checksum_batch(d_buf, d_desc, desc.size))
         np.testing.assert_array_equal(got, case["expected"], err_msg=f"g={g} c={c} fpw={fpw}")
@@ -147,6 +153,34 @@ def test_desc_crc_field_and_write_roundtrip():
     np.testing.assert_array_equal(after[mask], buf[mask])
 
 
+@pytest.mark.parametrize("flat", [False, True])
+def test_desc_crc_write_both_kernels(flat):
+    rng = np.random.default_rng(21)
+    n = 2000
+    lens = rng.integers(0, 3000, n)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 3, n).astype(np.uint64))[:-1]
+    offs += 3
+    buf = synth.random_bytes(17, int(offs[-1]) + int(lens[-1]) + 5)
+    desc = batch.make_desc(offs, lens, rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32))
+    want = O.batch_raw(buf, desc, crc_off=16)
+    if flat:
+        batch.set_launch_override(1, 4, 64, 1, 1)
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
+    got = u16(batch.checksum_batch(d_buf, d_desc, n, crc_off=16, flags=batch.F_WRITE))
+    np.testing.assert_array_equal(got, want)
+    verify = u16(batch.checksum_batch(d_buf, d_desc, n))
+    has = lens >= 18
+    assert (verify[has] == 0).all()
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_desc_out_of_bounds_both_kernels(flat):
+    if flat:
+        batch.set_launch_override(1, 2, 64, 1, 1)
+    test_desc_out_of_bounds_regions_are_not_read()
+
+
 def test_desc_out_of_bounds_regions_are_not_read():
     """Descriptors past the buffer: not read, result 0, counted in d_bad; the rest exact."""
     buf = synth.random_bytes(8, 10000)
@@ -180,18 +214,22 @@ def test_ipv4_golden_rx_tx():
     np.testing.assert_array_equal(v.cpu().numpy(), c["tx_verdict"])
 
 
-@pytest.mark.parametrize("g,c", SHAPES)
+@pytest.mark.parametrize("g,c", DESC_SHAPES)
 def test_ipv4_every_shape(g, c):
     cs = G.ipv4_cases()
     desc = batch.desc_to_device(G.ipv4_desc(cs["net"], cs["avail"]), DEV)
     n = cs["net"].size
     d_buf = to_dev(cs["buf"])
-    for fpw in sorted({64 // g, 64}):
+    for fpw in fpws(g):
         batch.set_launch_override(g, c, fpw)
         net, l4, v = batch.ipv4_checksum_batch(d_buf, desc, n)
         np.testing.assert_array_equal(u16(net), cs["rx_net"], err_msg=f"g={g} c={c} fpw={fpw}")
         np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"g={g} c={c} fpw={fpw}")
         np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"g={g} c={c} fpw={fpw}")
+        net, l4, v = batch.ipv4_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
+        np.testing.assert_array_equal(u16(net), cs["tx_net"], err_msg=f"TX g={g} c={c} fpw={fpw}")
+        np.testing.assert_array_equal(u16(l4), cs["tx_l4"], err_msg=f"TX g={g} c={c} fpw={fpw}")
+        np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"], err_msg=f"TX g={g} c={c} fpw={fpw}")
 
 
 def test_ipv4_out_of_bounds_is_malformed():

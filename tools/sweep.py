@@ -29,9 +29,11 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=[])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    if a.config in ("c1", "c3", "c3_64k", "c1_1536"):
-        n, ln, stride = {"c1": (262144, 1500, 1500), "c3": (262144, 9000, 9000), "c3_64k": (16384, 65536, 65536),
-                         "c1_1536": (262144, 1500, 1536)}[a.config]
+    UNI = {"c1": (262144, 1500, 1500), "c3": (262144, 9000, 9000), "c3_64k": (16384, 65536, 65536),
+           "c1_1536": (262144, 1500, 1536), "u354": (262144, 354, 354), "u64": (262144, 64, 64),
+           "u576": (262144, 576, 576)}
+    if a.config in UNI:
+        n, ln, stride = UNI[a.config]
         per = (n - 1) * stride + ln
         rot = max(3, -(-(3 << 30) // per) // 2)
         bufs = [torch.randint(0, 256, (per,), dtype=torch.uint8, device=dev) for _ in range(rot)]
