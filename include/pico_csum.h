@@ -161,8 +161,12 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
  * group = lanes per frame (4..64, power of 2); cpl = 16-byte chunks per lane
  * per pass (1,2,4,8); unroll = frames in flight per group (1,2,4; RAW batches
  * only, cpl*unroll <= 8); fpw = frames per wave (multiple of 64/group, <= 64);
- * nt = 0 auto / 1 plain / 2 non-temporal loads (RAW batches).  Process-wide. */
-int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt);
+ * nt = 0 auto / 1 plain / 2 non-temporal loads (RAW batches); pipeline = 0 auto /
+ * 1 off / 2 on (uniform batches whose frames fit one pass: double-buffered frame
+ * sets).  group = 1 selects the flat work-list kernel (descriptor batches).
+ * Process-wide. */
+int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
+                                  uint32_t pipeline);
 
 #ifdef __cplusplus
 }

@@ -80,7 +80,7 @@ def load() -> ctypes.CDLL:
     sig("pico_csum_host_unregister", ctypes.c_int, vp)
     sig("pico_csum_abi_version", ctypes.c_int)
     sig("pico_csum_last_error", ctypes.c_char_p)
-    sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32, u32, u32)
+    sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32, u32, u32, u32)
     del u8p
     _lib = lib
     return lib

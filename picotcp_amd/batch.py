@@ -114,12 +114,13 @@ def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     return out_net, out_l4, verdict
 
 
-def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int = 1, nt: int = 0) -> None:
+def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int = 1, nt: int = 0,
+                        pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic."""
     if group == 0:
-        unroll = fpw = cpl = nt = 0
+        unroll = fpw = cpl = nt = pipeline = 0
     _lib.check("pico_csum_set_launch_override",
-               _lib.load().pico_csum_set_launch_override(group, cpl, unroll, fpw, nt))
+               _lib.load().pico_csum_set_launch_override(group, cpl, unroll, fpw, nt, pipeline))
 
 
 class HostBatch:

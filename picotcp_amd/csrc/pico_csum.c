@@ -26,6 +26,9 @@ int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
                          uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
                          int uniform, void *stream);
+int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
+                                uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
+                                void *stream);
 int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int ipv4,
                           int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
@@ -114,14 +117,17 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
 
 /* ------------------------------------------------------------------ layer 2 */
 
-static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt;
+static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 
-int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt)
+int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
+                                  uint32_t pipeline)
 {
-    if (group == 0 && cpl == 0 && unroll == 0 && fpw == 0 && nt == 0) {
-        g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = 0;
+    if (group == 0 && cpl == 0 && unroll == 0 && fpw == 0 && nt == 0 && pipeline == 0) {
+        g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = g_ovr_pipe = 0;
         return 0;
     }
+    if (pipeline > 2)
+        return fail(PICO_CSUM_EINVAL, "pipeline must be 0 (auto), 1 (off) or 2 (on)");
     if (!(group == 1 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
         return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 4, 8, 16, 32 or 64");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
@@ -133,10 +139,11 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
     if (nt > 2)
         return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off) or 2 (on)");
     g_ovr_group = group; g_ovr_cpl = cpl; g_ovr_unroll = unroll; g_ovr_fpw = fpw; g_ovr_nt = nt;
+    g_ovr_pipe = pipeline;
     return 0;
 }
 
-struct shape { uint32_t G, CPL, U, nt, fpw; };
+struct shape { uint32_t G, CPL, U, nt, fpw, pipe; };
 
 /* Launch shape from the typical frame length (measured on MI355X, see
  * DESIGN.md "Launch shapes"): a lane group spans the frame in about 6-8
@@ -167,10 +174,27 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
     s.U = 1;
     s.nt = typical_len >= 1024u;
     s.fpw = pick_fpw(n, s.G);
-    (void)uniform;
+    /* uniform frames that fit one pass: the software-pipelined kernel, with two
+     * frame sets per wave (more, shorter waves balance best: C1 8 frames/wave) */
+    s.pipe = uniform && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)typical_len + 15u;
+    if (s.pipe) {
+        uint32_t ng = 64u / s.G, f = n / 32768u;
+        f -= f % ng;
+        s.fpw = f < 2 * ng ? 2 * ng : f > 64 ? 64 : f;
+    }
+    if (!uniform) {
+        /* descriptor batches: flat work-list kernel (mixed lengths stream as one
+         * chunk list); 4 slots per pass, ~8K waves */
+        uint32_t f = n / 8192u;
+        s.G = 1;
+        s.CPL = 4;
+        s.fpw = f < 1 ? 1 : f > 64 ? 64 : f;
+    }
     if (g_ovr_group) {
         s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
         s.nt = g_ovr_nt == 2;
+        if (g_ovr_pipe)
+            s.pipe = g_ovr_pipe == 2;
     }
     return s;
 }
@@ -253,6 +277,10 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
     s = pick_shape(n, len, 1);
     if (s.G == 1)
         return fail(PICO_CSUM_EINVAL, "the flat kernel (group 1) serves descriptor batches only");
+    if (s.pipe && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u)
+        return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,
+                                                         s.nt, s.fpw, stream),
+                             "pico_checksum_batch_uniform_dev");
     return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
                                               d_out, NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, stream),
                          "pico_checksum_batch_uniform_dev");

@@ -302,6 +302,72 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
     if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
 }
 
+// Uniform batch, software-pipelined: when a frame fits in one pass (G*CPL chunks),
+// a lane group holds two frame sets in registers -- the loads of set i+1 are
+// issued before set i is consumed, so a wave never waits on the HBM round trip
+// of the frame it is about to reduce.  Frame pairing, masks and results are
+// exactly those of csum_raw_kernel (same helpers).
+template <int G, int CPL, bool NT>
+__global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
+    constexpr uint32_t NG = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane / G, l = lane % G;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+
+    struct Frame {
+        const uint8_t* a0;
+        uint32_t r, nch, sel;
+        uint64_t span;
+    };
+    auto frame = [&](uint32_t i) {
+        Frame f;
+        const uint32_t j = i + g;
+        const uint32_t len = j < cnt ? p.len : 0u;
+        const uint8_t* fp = p.base + (f0 + j) * p.stride;
+        f.r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+        f.a0 = fp - f.r;
+        f.span = (uint64_t)f.r + len;
+        f.nch = len ? (uint32_t)((f.span + 15u) >> 4) : 0u;
+        f.sel = (f.r & 1u) ? SEL_ODD : SEL_EVEN;
+        return f;
+    };
+    auto issue = [&](const Frame& f, uint4 (&v)[CPL]) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = l + G * c;
+            v[c] = k < f.nch ? load_chunk_t<NT>(f.a0, k) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto consume = [&](const Frame& f, const uint4 (&v)[CPL]) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = l + G * c;
+            acc = add_full<true>(v[c], f.sel, acc);
+            if (k < f.nch && (k == 0 || k + 1 == f.nch))
+                acc -= add_chunk(v[c], ~chunk_range_mask(k, f.r, f.span) & 0xFFFFu, f.sel, 0u);
+        }
+        return finalize(group_sum<G>(acc) + p.seed);
+    };
+
+    uint32_t res = 0;
+    uint4 va[CPL], vb[CPL];
+    Frame fa = frame(0), fb;
+    issue(fa, va);
+    for (uint32_t i = 0; i < cnt; i += 2 * NG) {
+        fb = frame(i + NG);
+        issue(fb, vb);                                   // set i+NG in flight
+        res = collect<G>(res, consume(fa, va), lane, i);
+        fa = frame(i + 2 * NG);
+        issue(fa, va);                                   // set i+2NG in flight
+        if (i + NG < cnt) res = collect<G>(res, consume(fb, vb), lane, i + NG);
+    }
+    if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
+}
+
 struct Ipv4Args {
     uint8_t* base;
     uint64_t base_len;
@@ -481,18 +547,21 @@ __global__ __launch_bounds__(256) void csum_ipv4_kernel(Ipv4Args p) {
 // Descriptor batches of mixed lengths (C2 simple-IMIX, 64..1500 B).  A lane group
 // per frame leaves most lanes idle when a wave's frames differ in size, so here
 // a wave takes up to 64 frames and streams them as ONE list of 16-byte chunks:
-//   1. lane j owns frame j: reads its descriptor (and, IPv4, parses its header),
-//      computes the chunks it spans, and a DPP prefix scan turns the counts into
-//      start indices S[j] (per-wave LDS);
-//   2. every lane walks consecutive virtual chunks t = t0 + 64c + lane, so each
-//      load instruction covers 1 KiB that is contiguous whenever the frames are
-//      packed, whatever their sizes; the frame of t is a 6-step binary search in
-//      S; bytes outside the frame (head/tail) or inside an isolated field are
-//      corrected exactly as in the lane-group kernel;
-//   3. per-lane chunk sums are folded per frame by a DPP segmented scan (key =
-//      frame index) and the last lane of each run adds into the frame's LDS
-//      accumulator (ds_add_u32, conflict-free: one adder per frame per slot);
+//   1. lane j owns frame j: reads its descriptor (and, IPv4, parses its header)
+//      and counts the chunks it spans, padded to a multiple of 8; a DPP prefix
+//      scan of the padded counts gives each frame's start S[j] (per-wave LDS);
+//   2. every lane walks consecutive virtual chunks t = t0 + 64c + lane: each load
+//      instruction covers 1 KiB that is contiguous wherever the frames are packed,
+//      whatever their sizes.  The frame of t is a 6-step binary search in S.  Each
+//      chunk is added through a branch-free 128-bit byte mask (two 64-bit shifts)
+//      that drops the bytes outside the frame;
+//   3. because frames start on 8-lane boundaries, every aligned 8-lane group holds
+//      chunks of one frame: 3 DPP adds fold it (a 4th joins the two halves of a row
+//      when they share the frame; a whole-wave frame folds in 6) and one lane per
+//      run adds into the frame's LDS accumulator (ds_add_u32);
 //   4. lane j finalizes frame j: one coalesced store per output per wave.
+// Frames of more than 64K chunks (> 1 MiB) are streamed afterwards by the whole
+// wave, one at a time, so the 32-bit chunk counts cannot overflow.
 
 // Inclusive prefix sum over the 64 lanes (DPP row_shr 1/2/4/8, row_bcast 15/31).
 __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
@@ -505,22 +574,28 @@ __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
     return v;
 }
 
-// Inclusive segmented prefix sum: lanes with equal (non-decreasing) key form runs.
-__device__ __forceinline__ uint32_t seg_scan_add(uint32_t v, uint32_t key) {
-#define PICO_SEG_STEP(ctrl, rmask)                                                              \
-    {                                                                                           \
-        const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, rmask, 0xF, false);  \
-        const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)key, ctrl, rmask, 0xF, false); \
-        v += (pk == key) ? pv : 0u;                                                             \
+// Sum of the bytes of chunk v (chunk start at relative position ch) that lie in
+// [x0, x1) (relative to the same origin), frame-relative pairing via sel.
+// Branch-free: the 16-byte validity mask is built as two 64-bit masks.
+template <bool PERM>
+__device__ __forceinline__ uint32_t masked_chunk_sum(const uint4 v, uint32_t ch, uint32_t x0, uint32_t x1,
+                                                     uint32_t sel) {
+    const uint32_t lo = x0 <= ch ? 0u : min(x0 - ch, 16u);
+    const uint32_t hi = x1 <= ch ? 0u : min(x1 - ch, 16u);
+    const uint64_t ALL = ~0ull;
+    uint64_t m0 = lo >= 8u ? 0ull : (ALL << (8u * lo));
+    m0 &= hi >= 8u ? ALL : ~(ALL << (8u * hi));
+    uint64_t m1 = lo >= 16u ? 0ull : (lo <= 8u ? ALL : (ALL << (8u * (lo - 8u))));
+    m1 &= hi >= 16u ? ALL : (hi <= 8u ? 0ull : ~(ALL << (8u * (hi - 8u))));
+    uint32_t a = v.x & (uint32_t)m0, b = v.y & (uint32_t)(m0 >> 32);
+    uint32_t c = v.z & (uint32_t)m1, d = v.w & (uint32_t)(m1 >> 32);
+    if constexpr (PERM) {
+        a = __builtin_amdgcn_perm(0u, a, sel);
+        b = __builtin_amdgcn_perm(0u, b, sel);
+        c = __builtin_amdgcn_perm(0u, c, sel);
+        d = __builtin_amdgcn_perm(0u, d, sel);
     }
-    PICO_SEG_STEP(0x111, 0xF)
-    PICO_SEG_STEP(0x112, 0xF)
-    PICO_SEG_STEP(0x114, 0xF)
-    PICO_SEG_STEP(0x118, 0xF)
-    PICO_SEG_STEP(0x142, 0xA)
-    PICO_SEG_STEP(0x143, 0xC)
-#undef PICO_SEG_STEP
-    return v;
+    return dot2_add(d, dot2_add(c, dot2_add(b, dot2_add(a, 0u))));
 }
 
 struct FlatArgs {
@@ -539,13 +614,14 @@ struct FlatArgs {
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t BIG_CHUNKS = 1u << 16;   // frames above this stream on their own
 
 struct FlatWaveLds {
-    uint32_t S[64];        // exclusive prefix of chunk counts
+    uint32_t S[64];        // exclusive prefix of the padded chunk counts
     uint32_t acc_all[64];  // bytes [0, span) of the frame
     uint32_t acc_x[64];    // the isolated 2-byte field (RAW crc / UDP crc / TX crc)
     uint32_t acc_opt[64];  // IPv4 option bytes [20, hl)
-    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4}
+    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4 | nch << 5}
     uint2 xo[64];          // {field position r + xoff (NONE), option end r + hl (0)}
 };
 
@@ -633,18 +709,22 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
             }
         }
     }
-    const uint32_t nch = ext ? (r + ext + 15u) >> 4 : 0u;
-    const uint32_t incl = wave_scan_add(nch);
+    const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
+    const bool big = nch64 > BIG_CHUNKS;
+    const uint32_t nch = big ? 0u : (uint32_t)nch64;
+    const uint32_t pch = (nch + 7u) & ~7u;
+    const uint32_t incl = wave_scan_add(pch);
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t S = incl - nch;
-    const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
-    const bool any_x = __builtin_amdgcn_ballot_w64(nch != 0 && xpos != NONE) != 0;
+    const uint32_t S = incl - pch;
+    const bool any_odd = __builtin_amdgcn_ballot_w64(nch64 != 0 && odd) != 0;
+    const bool any_x = __builtin_amdgcn_ballot_w64(nch64 != 0 && xpos != NONE) != 0;
     const bool any_opt = IPV4 && __builtin_amdgcn_ballot_w64(nch != 0 && optend != 0) != 0;
+    uint64_t bigmask = __builtin_amdgcn_ballot_w64(big);
     L.S[lane] = lane < cnt ? S : T;
     L.acc_all[lane] = 0;
     L.acc_x[lane] = 0;
     L.acc_opt[lane] = 0;
-    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4));
+    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (nch << 5));
     L.xo[lane] = make_uint2(xpos, optend);
     __builtin_amdgcn_wave_barrier();
 
@@ -655,6 +735,7 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
             uint4 v[CPL];
             uint32_t jj[CPL], kk[CPL];
             uint4 fi[CPL];
+            bool ok[CPL];
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const uint32_t t = t0 + 64u * c + lane;
@@ -667,53 +748,92 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
                 jj[c] = j;
                 kk[c] = t - sj;
                 fi[c] = L.info[j];
+                ok[c] = t < T && kk[c] < (fi[c].w >> 5);
                 const uint8_t* a0 = p.base + ((((uint64_t)fi[c].y) << 32) | fi[c].x);
-                v[c] = t < T ? load_chunk_t<NT>(a0, kk[c]) : make_uint4(0, 0, 0, 0);
+                v[c] = ok[c] ? load_chunk_t<NT>(a0, kk[c]) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const uint32_t t = t0 + 64u * c + lane;
-                const bool valid = t < T;
                 const uint32_t k = kk[c], j = jj[c];
                 const uint32_t rr = fi[c].w & 15u;
                 const uint32_t sl = (fi[c].w & 16u) ? SEL_ODD : SEL_EVEN;
-                const uint32_t send = fi[c].z;
-                uint32_t x = add_full<PERM>(v[c], sl, 0u);
                 const uint32_t ch = k << 4;
-                if (valid && (ch < rr || ch + 16u > send)) {
-                    const uint32_t m = chunk_range_mask(k, rr, send);
-                    x -= add_chunk(v[c], ~m & 0xFFFFu, sl, 0u);
-                }
+                uint32_t x = ok[c] ? masked_chunk_sum<PERM>(v[c], ch, rr, fi[c].z, sl) : 0u;
                 if (any_x || any_opt) {
                     const uint2 xo = L.xo[j];
-                    if (any_x && valid && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4))) {
-                        const uint32_t xv = add_chunk(v[c], chunk_range_mask(k, xo.x, (uint64_t)xo.x + 2u), sl, 0u);
+                    if (any_x && ok[c] && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4))) {
+                        const uint32_t xv = masked_chunk_sum<PERM>(v[c], ch, xo.x, xo.x + 2u, sl);
                         if (xv) atomicAdd(&L.acc_x[j], xv);
                     }
-                    if (IPV4 && any_opt && valid && xo.y != 0u && ch < xo.y) {
-                        const uint32_t ov = add_chunk(v[c], chunk_range_mask(k, rr + 20u, xo.y), sl, 0u);
+                    if (IPV4 && any_opt && ok[c] && xo.y != 0u && ch < xo.y) {
+                        const uint32_t ov = masked_chunk_sum<PERM>(v[c], ch, rr + 20u, xo.y, sl);
                         if (ov) atomicAdd(&L.acc_opt[j], ov);
                     }
                 }
-                if (!valid) x = 0;
-                const uint32_t key = valid ? j : 0xFFFFFFFEu;
-                const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
-                const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
-                if (k0 == k63) {                       // the whole slot is one frame
+                // fold: the whole slot one frame -> 6 DPP steps; else per row / half row
+                const uint32_t blk_ok = (t0 + 64u * c + lane) < T;   // lane's 8-block lies in the list
+                const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+                const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+                const bool whole = k0 == k63 && __builtin_amdgcn_readlane((int)blk_ok, 63);
+                if (whole) {
                     const uint32_t tot = group_sum<64>(x);
-                    if (lane == 63 && valid) atomicAdd(&L.acc_all[j], tot);
+                    if (lane == 63) atomicAdd(&L.acc_all[j], tot);
                 } else {
-                    const uint32_t run = seg_scan_add(x, key);
-                    const uint32_t nk = (uint32_t)__shfl_down((int)key, 1);
-                    if (valid && (lane == 63 || nk != key)) atomicAdd(&L.acc_all[j], run);
+                    x = group_sum<8>(x);                          // every lane of the 8-group
+                    const uint32_t xm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+                    const uint32_t jm = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)j, 0x140, 0xF, 0xF, false);
+                    const bool same = jm == j;
+                    const uint32_t q = lane & 15u;
+                    const bool adder = blk_ok && (q == 15u || (q == 7u && !same) ||
+                                                  (q == 7u && same && !((t0 + 64u * c + (lane | 15u)) < T)));
+                    const uint32_t val = (q == 15u && same) ? x + xm : x;
+                    if (adder) atomicAdd(&L.acc_all[j], val);
                 }
             }
         }
     };
-    if (any_odd) stream(std::integral_constant<bool, true>{});
-    else stream(std::integral_constant<bool, false>{});
+    if (T) {
+        if (any_odd) stream(std::integral_constant<bool, true>{});
+        else stream(std::integral_constant<bool, false>{});
+    }
+
+    // ---- 2b. frames over BIG_CHUNKS, one at a time by the whole wave
+    while (bigmask) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(bigmask);
+        bigmask &= bigmask - 1;
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0off, (int)j);
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a0off >> 32), (int)j);
+        const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)j);
+        const uint32_t bspan = (uint32_t)__builtin_amdgcn_readlane((int)span, (int)j);
+        const uint32_t bx = (uint32_t)__builtin_amdgcn_readlane((int)xpos, (int)j);
+        const uint64_t bend = (uint64_t)br + bspan;
+        const uint32_t bn = (uint32_t)((bend + 15u) >> 4);
+        const uint32_t bsel = (br & 1u) ? SEL_ODD : SEL_EVEN;
+        const uint8_t* a0 = p.base + (((uint64_t)bhi << 32) | blo);
+        uint32_t acc = 0, accx = 0;
+        for (uint32_t kb = 0; kb < bn; kb += 64u * CPL) {
+            uint4 v[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + 64u * c + lane;
+                v[c] = k < bn ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = kb + 64u * c + lane;
+                const bool edge = k < bn && (k == 0 || k + 1 == bn);
+                acc = add_full<true>(v[c], bsel, acc);
+                if (edge) acc -= add_chunk(v[c], ~chunk_range_mask(k, br, bend) & 0xFFFFu, bsel, 0u);
+                if (bx != NONE && (k == (bx >> 4) || k == ((bx + 1u) >> 4)))
+                    accx += add_chunk(v[c], chunk_range_mask(k, bx, (uint64_t)bx + 2u), bsel, 0u);
+            }
+        }
+        acc = group_sum<64>(acc);
+        accx = group_sum<64>(accx);
+        if (lane == 63) { L.acc_all[j] = acc; L.acc_x[j] = accx; }
+    }
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS atomics are done
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS updates are done
 
     // ---- 3. lane j finalizes frame j
     if (lane >= cnt) return;
@@ -792,6 +912,27 @@ extern "C" {
 
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
+
+// Software-pipelined uniform kernel (one pass per frame: G*CPL*16 >= len + 15).
+int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
+                                uint32_t seed, uint16_t* out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
+                                void* stream) {
+    if (!shape_ok(G, CPL, fpw) || (uint64_t)G * CPL * 16u < (uint64_t)len + 15u) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    RawArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), base_len, nullptr, stride, len, n, seed, -1, 0u, fpw,
+              out, nullptr};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define X(g, c)                                                                                     \
+    if (G == g && CPL == c) {                                                                       \
+        if (nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, true>), grid, block, 0, s, a);     \
+        else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, false>), grid, block, 0, s, a);       \
+        return (int)hipGetLastError();                                                              \
+    }
+    PICO_FOR_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
 
 int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64_t stride, uint32_t len,
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t* out,

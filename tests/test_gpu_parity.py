@@ -62,9 +62,11 @@ def test_uniform_every_shape(g, c):
         want = O.batch_uniform(buf, stride, ln, n, seed)
         d = to_dev(buf)
         for fpw in sorted({64 // g, 64, (64 // g) * 3 if (64 // g) * 3 <= 64 else 64}):
-            batch.set_launch_override(g, c, fpw)
-            got = u16(batch.checksum_uniform(d, stride, ln, n, seed=seed))
-            np.testing.assert_array_equal(got, want, err_msg=f"g={g} c={c} fpw={fpw} len={ln} stride={stride}")
+            for pipe in (1, 2):
+                batch.set_launch_override(g, c, fpw, 1, 2 if pipe == 2 else 1, pipe)
+                got = u16(batch.checksum_uniform(d, stride, ln, n, seed=seed))
+                np.testing.assert_array_equal(got, want, err_msg=f"g={g} c={c} fpw={fpw} pipe={pipe} len={ln} "
+                                                                 f"stride={stride}")
 
 
 def test_uniform_c1_full_size():
@@ -106,6 +108,23 @@ def test_desc_every_shape(g, c):
         batch.set_launch_override(g, c, fpw)
         got = u16(batch.checksum_batch(d_buf, d_desc, desc.size))
         np.testing.assert_array_equal(got, case["expected"], err_msg=f"g={g} c={c} fpw={fpw}")
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_desc_big_regions(flat):
+    """Regions over 64K chunks (> 1 MiB) take the flat kernel's whole-wave path; mixed with
+    small ones, odd offsets, seeds and a crc field."""
+    rng = np.random.default_rng(44)
+    buf = synth.random_bytes(45, 12 << 20)
+    offs = [1, 3 << 20, 5, (7 << 20) + 3, 100, 2000, 11 << 20]
+    lens = [2 << 20, (3 << 20) + 1, 64, (1 << 20) + 17, 1500, 0, 123457]
+    desc = batch.make_desc(offs, lens, rng.integers(0, 1 << 32, len(offs), dtype=np.uint64).astype(np.uint32))
+    if flat:
+        batch.set_launch_override(1, 4, 8, 1, 1)
+    for crc in (-1, 10):
+        want = O.batch_raw(buf, desc, crc_off=crc)
+        got = u16(batch.checksum_batch(to_dev(buf), batch.desc_to_device(desc, DEV), len(offs), crc_off=crc))
+        np.testing.assert_array_equal(got, want)
 
 
 def test_desc_empty_and_edge_lengths():

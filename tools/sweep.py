@@ -4,7 +4,7 @@
 with the median kernel time and the achieved algorithmic GB/s.
 
   python tools/sweep.py --config c1 --rounds 5 --shapes 64,2,2,32,1 64,2,1,32,1 ...
-  shape = G,CPL,U,FPW,NT   (NT: 1 plain loads, 2 non-temporal)
+  shape = G,CPL,U,FPW,NT[,PIPE]   (NT / PIPE: 1 off, 2 on; G = 1: flat work-list kernel)
 """
 from __future__ import annotations
 
@@ -71,8 +71,8 @@ def main():
     stream = torch.cuda.current_stream()
     for rnd in range(a.rounds):
         for s in shapes:
-            g, c, u, f, nt = s
-            batch.set_launch_override(g, c, f, u, nt)
+            g, c, u, f, nt = s[:5]
+            batch.set_launch_override(g, c, f, u, nt, s[5] if len(s) > 5 else 0)
             for i in range(3):
                 launch(i)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
