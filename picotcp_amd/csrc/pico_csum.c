@@ -26,13 +26,15 @@ int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64
                          uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
                          uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
                          int uniform, void *stream);
+int pico_csum_launch_desc_adaptive(void *base, uint64_t base_len, const void *desc, uint32_t n, int32_t crc_off,
+                                   uint32_t flags, uint16_t *out, uint32_t *bad, uint32_t nt, void *stream);
 int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
                                 void *stream);
 int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int ipv4,
                           int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
-                          void *stream);
+                          uint32_t max_blocks, void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -132,12 +134,14 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 4, 8, 16, 32 or 64");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
-    if (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8)
+    if (group == 1 && unroll > 8)
+        return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
+    if (group > 1 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
         return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
     if (fpw == 0 || fpw > 64 || (group > 1 && fpw % (64 / group) != 0))
         return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
-    if (nt > 2)
-        return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off) or 2 (on)");
+    if (nt > 3)
+        return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off), 2 (on) or 3 (on except frame edges)");
     g_ovr_group = group; g_ovr_cpl = cpl; g_ovr_unroll = unroll; g_ovr_fpw = fpw; g_ovr_nt = nt;
     g_ovr_pipe = pipeline;
     return 0;
@@ -185,14 +189,15 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
     if (!uniform) {
         /* descriptor batches: flat work-list kernel (mixed lengths stream as one
          * chunk list); 4 slots per pass, ~8K waves */
-        uint32_t f = n / 8192u;
+        uint32_t f = n / 16384u;
         s.G = 1;
-        s.CPL = 4;
+        s.CPL = 2;
+        s.U = 0;          /* flat kernel: 0 = one batch per wave (measured faster than persistent) */
         s.fpw = f < 1 ? 1 : f > 64 ? 64 : f;
     }
     if (g_ovr_group) {
         s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
-        s.nt = g_ovr_nt == 2;
+        s.nt = g_ovr_nt >= 2 ? g_ovr_nt - 1 : 0;
         if (g_ovr_pipe)
             s.pipe = g_ovr_pipe == 2;
     }
@@ -200,16 +205,19 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
 }
 
 static int g_dev_state; /* 0 unknown, 1 ok, -1 none */
+static uint32_t g_cus = 256; /* compute units of device 0 (MI355X: 256) */
 
 static int need_device(void)
 {
-    int count = 0;
+    int count = 0, cus = 0;
     if (g_dev_state == 1)
         return 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         g_dev_state = -1;
         return fail(PICO_CSUM_ENODEV, "no HIP device: the batched checksum path runs only on the GPU");
     }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && cus > 0)
+        g_cus = (uint32_t)cus;
     g_dev_state = 1;
     return 0;
 }
@@ -251,9 +259,14 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (!g_ovr_group)   /* default: lane groups sized per wave from its frames' lengths */
+        return launch_status(pico_csum_launch_desc_adaptive(d_base, base_len, d_desc, n, crc_off, flags, d_out,
+                                                            d_bad, 0, stream),
+                             "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
-                                                   NULL, NULL, NULL, s.CPL, s.nt, s.fpw, stream),
+                                                   NULL, NULL, NULL, s.CPL, s.nt, s.fpw,
+                                                   s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
                              "pico_checksum_batch_dev");
     return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
                                               d_bad, s.G, s.CPL, s.U, s.nt, s.fpw, 0, stream),
@@ -308,7 +321,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
                                                    d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                                   stream),
+                                                   s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
                              "pico_ipv4_checksum_batch_dev");
     return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),

@@ -185,24 +185,13 @@ struct RawArgs {
 // Each lane group keeps U frames in flight: one pass issues U*CPL dwordx4 loads
 // per lane before any of them is consumed, so a wave has U*CPL KiB (G=64) of
 // reads outstanding while earlier frames are being reduced.
+// One wave's frames [f0, f0 + cnt); lane j holds descriptor j (unless UNIFORM).
 template <int G, int CPL, int U, bool UNIFORM, bool NT>
-__global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
+__device__ __forceinline__ void raw_wave(const RawArgs& p, uint64_t f0, uint32_t cnt, uint32_t d_lo, uint32_t d_hi,
+                                         uint32_t d_len, uint32_t d_seed) {
     constexpr uint32_t NG = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t g = lane / G, l = lane % G;
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t f0 = wave * p.fpw;
-    if (f0 >= p.n) return;
-    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
-
-    uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_seed = 0;
-    if constexpr (!UNIFORM) {
-        if (lane < cnt) {
-            const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
-            d_lo = d.x; d_hi = d.y; d_len = d.z; d_seed = d.w;
-        }
-    }
-
     uint32_t res = 0;
     for (uint32_t i = 0; i < cnt; i += NG * U) {
         uint8_t* fp[U];
@@ -302,12 +291,61 @@ __global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
     if (lane < cnt) p.out[f0 + lane] = (uint16_t)res;
 }
 
+template <int G, int CPL, int U, bool UNIFORM, bool NT>
+__global__ __launch_bounds__(256) void csum_raw_kernel(RawArgs p) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_seed = 0;
+    if constexpr (!UNIFORM) {
+        if (lane < cnt) {
+            const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+            d_lo = d.x; d_hi = d.y; d_len = d.z; d_seed = d.w;
+        }
+    }
+    raw_wave<G, CPL, U, UNIFORM, NT>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+}
+
+// Descriptor batch, launch shape chosen PER WAVE: the wave reads its (up to 16)
+// descriptors, takes the mean chunk count of its frames and runs the lane-group
+// body with the smallest G in 4..64 with G*8 >= mean chunks (CPL 8, 16 frames per
+// wave = a multiple of every 64/G).  Mixed-size batches (IMIX) then get small
+// groups where frames are small and wide groups where they are large, without the
+// host knowing the sizes.  Frames > 1 MiB are summed with G = 64.
+// Non-temporal loads for waves of frames >= 1 KiB (G >= 16), as for uniform batches.
+__global__ __launch_bounds__(256) void csum_desc_adaptive_kernel(RawArgs p) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    uint32_t d_lo = 0, d_hi = 0, d_len = 0, d_seed = 0;
+    if (lane < cnt) {
+        const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+        d_lo = d.x; d_hi = d.y; d_len = d.z; d_seed = d.w;
+    }
+    // mean chunks per frame (lengths capped at 1 MiB so the 32-bit sum cannot wrap)
+    uint32_t ch = lane < cnt ? (min(d_len, 1u << 20) >> 4) + 1u : 0u;
+    ch = group_sum<64>(ch);
+    const uint32_t mean = (uint32_t)__builtin_amdgcn_readlane((int)ch, 63) / max(cnt, 1u);
+    if (mean <= 32u)       raw_wave<4, 8, 1, false, false>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+    else if (mean <= 64u)  raw_wave<8, 8, 1, false, false>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+    else if (mean <= 128u) raw_wave<16, 8, 1, false, true>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+    else if (mean <= 256u) raw_wave<32, 8, 1, false, true>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+    else                   raw_wave<64, 8, 1, false, true>(p, f0, cnt, d_lo, d_hi, d_len, d_seed);
+}
+
 // Uniform batch, software-pipelined: when a frame fits in one pass (G*CPL chunks),
 // a lane group holds two frame sets in registers -- the loads of set i+1 are
 // issued before set i is consumed, so a wave never waits on the HBM round trip
 // of the frame it is about to reduce.  Frame pairing, masks and results are
 // exactly those of csum_raw_kernel (same helpers).
-template <int G, int CPL, bool NT>
+// NTM: 0 plain loads, 1 non-temporal, 2 non-temporal except the slots that hold a
+// frame's head or tail chunk (the 128-byte line two neighbouring frames share
+// stays in L2 for the second reader).
+template <int G, int CPL, int NTM>
 __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
     constexpr uint32_t NG = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
@@ -338,7 +376,13 @@ __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const uint32_t k = l + G * c;
-            v[c] = k < f.nch ? load_chunk_t<NT>(f.a0, k) : make_uint4(0, 0, 0, 0);
+            if constexpr (NTM == 2) {
+                const bool edge_slot = __builtin_amdgcn_ballot_w64(k < f.nch && (k == 0 || k + 1 == f.nch)) != 0;
+                if (edge_slot) v[c] = k < f.nch ? load_chunk_t<false>(f.a0, k) : make_uint4(0, 0, 0, 0);
+                else v[c] = k < f.nch ? load_chunk_t<true>(f.a0, k) : make_uint4(0, 0, 0, 0);
+            } else {
+                v[c] = k < f.nch ? load_chunk_t<NTM == 1>(f.a0, k) : make_uint4(0, 0, 0, 0);
+            }
         }
     };
     auto consume = [&](const Frame& f, const uint4 (&v)[CPL]) {
@@ -625,257 +669,294 @@ struct FlatWaveLds {
     uint2 xo[64];          // {field position r + xoff (NONE), option end r + hl (0)}
 };
 
+// Persistent: each wave loops over batches b = wave, wave + W, ... of fpw frames.
+// The next batch's descriptors (two batches ahead) and IPv4 header chunks (one
+// ahead) are loaded before the current batch streams, so their HBM round trips
+// overlap the stream instead of preceding it.
 template <bool IPV4, int CPL, bool NT>
 __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
     __shared__ FlatWaveLds lds_all[4];
     const uint32_t lane = threadIdx.x & 63u;
     FlatWaveLds& L = lds_all[threadIdx.x >> 6];
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t f0 = wave * p.fpw;
-    if (f0 >= p.n) return;
-    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t nb = ((uint64_t)p.n + p.fpw - 1) / p.fpw;
+    uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= nb) return;
     const bool tx = IPV4 && (p.flags & 2u) != 0;
 
-    // ---- 1. lane j = frame j
-    uint64_t off = 0;
-    uint32_t len = 0, seed = 0;
-    if (lane < cnt) {
-        const uint4 d = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
-        off = ((uint64_t)d.y << 32) | d.x;
-        len = d.z;
-        seed = d.w;
-    }
-    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
-    if (oob) len = 0;
-    uint8_t* fp = p.base + off;
-    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
-    const uint64_t a0off = off - r;
-    const uint32_t odd = r & 1u;
-
-    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
-    // IPv4 per-frame state
-    uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
-    bool parsed = false, l4_needed = false;
-    if constexpr (!IPV4) {
-        span = ext = len;
-        if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
-    } else {
-        const uint32_t avail = len;
-        if (avail >= 20) {
-            const uint8_t* a0 = p.base + a0off;
-            const uint4 c0 = load_chunk(a0, 0);
-            const uint4 c1 = (r + 20 > 16) ? load_chunk(a0, 1) : make_uint4(0, 0, 0, 0);
-            const uint4 c2 = (r + 20 > 32) ? load_chunk(a0, 2) : make_uint4(0, 0, 0, 0);
-            const uint32_t D[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-            const uint32_t q = r >> 2, sh = r & 3u;
-            uint32_t E[6];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
-            uint32_t H[5];
-#pragma unroll
-            for (int m = 0; m < 5; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
-            const uint32_t ihl = H[0] & 0x0Fu;
-            hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-            const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
-            proto = (H[2] >> 8) & 0xFFu;
-            ipcrc = H[2] >> 16;
-            tl = (tot - hl) & 0xFFFFu;                              // uint16 wrap, pico_ipv4.c:395
-            const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;   // pico_ipv4.c:386
-            if (!(hl > avail || (!tx && tl > max_allowed) || hl + tl > avail)) {
-                parsed = true;
-                verdict = 0;
-                span = ext = hl + tl;
-#pragma unroll
-                for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
-                pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
-                         (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
-                if (hl > 20u) optend = r + hl;
-                if (!tx) {
-                    if (proto == 6u) {
-                        l4_needed = true;
-                    } else if (proto == 17u) {
-                        if (hl + 8u > avail) verdict |= V_MALFORMED;
-                        else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
-                    }
-                } else {
-                    if (proto == 6u) {
-                        if (tl < 20u) verdict |= V_MALFORMED;
-                        else { l4_needed = true; xpos = r + hl + 16u; }
-                    } else if (proto == 1u) {
-                        if (tl < 8u) verdict |= V_MALFORMED;
-                        else { l4_needed = true; xpos = r + hl + 2u; }
-                    }
-                }
-            }
+    auto load_desc = [&](uint64_t bb) {
+        uint4 d = make_uint4(0, 0, 0, 0);
+        if (bb < nb) {
+            const uint64_t f = bb * p.fpw + lane;
+            if (lane < p.fpw && f < p.n) d = *reinterpret_cast<const uint4*>(p.desc + f);
         }
-    }
-    const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
-    const bool big = nch64 > BIG_CHUNKS;
-    const uint32_t nch = big ? 0u : (uint32_t)nch64;
-    const uint32_t pch = (nch + 7u) & ~7u;
-    const uint32_t incl = wave_scan_add(pch);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t S = incl - pch;
-    const bool any_odd = __builtin_amdgcn_ballot_w64(nch64 != 0 && odd) != 0;
-    const bool any_x = __builtin_amdgcn_ballot_w64(nch64 != 0 && xpos != NONE) != 0;
-    const bool any_opt = IPV4 && __builtin_amdgcn_ballot_w64(nch != 0 && optend != 0) != 0;
-    uint64_t bigmask = __builtin_amdgcn_ballot_w64(big);
-    L.S[lane] = lane < cnt ? S : T;
-    L.acc_all[lane] = 0;
-    L.acc_x[lane] = 0;
-    L.acc_opt[lane] = 0;
-    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (nch << 5));
-    L.xo[lane] = make_uint2(xpos, optend);
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- 2. stream the wave's chunk list
-    auto stream = [&](auto perm_tag) {
-        constexpr bool PERM = decltype(perm_tag)::value;
-        for (uint32_t t0 = 0; t0 < T; t0 += 64u * CPL) {
-            uint4 v[CPL];
-            uint32_t jj[CPL], kk[CPL];
-            uint4 fi[CPL];
-            bool ok[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t t = t0 + 64u * c + lane;
-                uint32_t j = 0, sj = 0;
-#pragma unroll
-                for (uint32_t step = 32; step; step >>= 1) {
-                    const uint32_t s2 = L.S[j + step];
-                    if (s2 <= t) { j += step; sj = s2; }
-                }
-                jj[c] = j;
-                kk[c] = t - sj;
-                fi[c] = L.info[j];
-                ok[c] = t < T && kk[c] < (fi[c].w >> 5);
-                const uint8_t* a0 = p.base + ((((uint64_t)fi[c].y) << 32) | fi[c].x);
-                v[c] = ok[c] ? load_chunk_t<NT>(a0, kk[c]) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t k = kk[c], j = jj[c];
-                const uint32_t rr = fi[c].w & 15u;
-                const uint32_t sl = (fi[c].w & 16u) ? SEL_ODD : SEL_EVEN;
-                const uint32_t ch = k << 4;
-                uint32_t x = ok[c] ? masked_chunk_sum<PERM>(v[c], ch, rr, fi[c].z, sl) : 0u;
-                if (any_x || any_opt) {
-                    const uint2 xo = L.xo[j];
-                    if (any_x && ok[c] && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4))) {
-                        const uint32_t xv = masked_chunk_sum<PERM>(v[c], ch, xo.x, xo.x + 2u, sl);
-                        if (xv) atomicAdd(&L.acc_x[j], xv);
-                    }
-                    if (IPV4 && any_opt && ok[c] && xo.y != 0u && ch < xo.y) {
-                        const uint32_t ov = masked_chunk_sum<PERM>(v[c], ch, rr + 20u, xo.y, sl);
-                        if (ov) atomicAdd(&L.acc_opt[j], ov);
-                    }
-                }
-                // fold: the whole slot one frame -> 6 DPP steps; else per row / half row
-                const uint32_t blk_ok = (t0 + 64u * c + lane) < T;   // lane's 8-block lies in the list
-                const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-                const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
-                const bool whole = k0 == k63 && __builtin_amdgcn_readlane((int)blk_ok, 63);
-                if (whole) {
-                    const uint32_t tot = group_sum<64>(x);
-                    if (lane == 63) atomicAdd(&L.acc_all[j], tot);
-                } else {
-                    x = group_sum<8>(x);                          // every lane of the 8-group
-                    const uint32_t xm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
-                    const uint32_t jm = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)j, 0x140, 0xF, 0xF, false);
-                    const bool same = jm == j;
-                    const uint32_t q = lane & 15u;
-                    const bool adder = blk_ok && (q == 15u || (q == 7u && !same) ||
-                                                  (q == 7u && same && !((t0 + 64u * c + (lane | 15u)) < T)));
-                    const uint32_t val = (q == 15u && same) ? x + xm : x;
-                    if (adder) atomicAdd(&L.acc_all[j], val);
-                }
-            }
-        }
+        return d;
     };
-    if (T) {
-        if (any_odd) stream(std::integral_constant<bool, true>{});
-        else stream(std::integral_constant<bool, false>{});
-    }
-
-    // ---- 2b. frames over BIG_CHUNKS, one at a time by the whole wave
-    while (bigmask) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(bigmask);
-        bigmask &= bigmask - 1;
-        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0off, (int)j);
-        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a0off >> 32), (int)j);
-        const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)j);
-        const uint32_t bspan = (uint32_t)__builtin_amdgcn_readlane((int)span, (int)j);
-        const uint32_t bx = (uint32_t)__builtin_amdgcn_readlane((int)xpos, (int)j);
-        const uint64_t bend = (uint64_t)br + bspan;
-        const uint32_t bn = (uint32_t)((bend + 15u) >> 4);
-        const uint32_t bsel = (br & 1u) ? SEL_ODD : SEL_EVEN;
-        const uint8_t* a0 = p.base + (((uint64_t)bhi << 32) | blo);
-        uint32_t acc = 0, accx = 0;
-        for (uint32_t kb = 0; kb < bn; kb += 64u * CPL) {
-            uint4 v[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t k = kb + 64u * c + lane;
-                v[c] = k < bn ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const uint32_t k = kb + 64u * c + lane;
-                const bool edge = k < bn && (k == 0 || k + 1 == bn);
-                acc = add_full<true>(v[c], bsel, acc);
-                if (edge) acc -= add_chunk(v[c], ~chunk_range_mask(k, br, bend) & 0xFFFFu, bsel, 0u);
-                if (bx != NONE && (k == (bx >> 4) || k == ((bx + 1u) >> 4)))
-                    accx += add_chunk(v[c], chunk_range_mask(k, bx, (uint64_t)bx + 2u), bsel, 0u);
+    // header window (IPv4): the chunks covering header bytes [0, 20) of the lane's frame
+    struct Hdr { uint4 c0, c1, c2; };
+    auto load_hdr = [&](const uint4 d) {
+        Hdr h{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if constexpr (IPV4) {
+            const uint64_t off = ((uint64_t)d.y << 32) | d.x;
+            const uint32_t len = d.z;
+            if (len >= 20u && off <= p.base_len && len <= p.base_len - off) {
+                uint8_t* fp = p.base + off;
+                const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+                const uint8_t* a0 = fp - r;
+                h.c0 = load_chunk(a0, 0);
+                if (r + 20 > 16) h.c1 = load_chunk(a0, 1);
+                if (r + 20 > 32) h.c2 = load_chunk(a0, 2);
             }
         }
-        acc = group_sum<64>(acc);
-        accx = group_sum<64>(accx);
-        if (lane == 63) { L.acc_all[j] = acc; L.acc_x[j] = accx; }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS updates are done
+        return h;
+    };
 
-    // ---- 3. lane j finalizes frame j
-    if (lane >= cnt) return;
-    const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
-    if constexpr (!IPV4) {
-        uint32_t ret = 0;
-        if (oob) {
-            if (p.bad) atomicAdd(p.bad, 1u);
+    uint4 dcur = load_desc(b);
+    Hdr hcur = load_hdr(dcur);
+    uint4 dnext = load_desc(b + W);
+
+    for (; b < nb; b += W) {
+        const uint64_t f0 = b * p.fpw;
+        const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+
+        // ---- 1. lane j = frame j of this batch
+        uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
+        uint32_t len = lane < cnt ? dcur.z : 0u;
+        const uint32_t seed = dcur.w;
+        const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
+        if (oob || lane >= cnt) { len = 0; off = 0; }
+        uint8_t* fp = p.base + off;
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+        const uint64_t a0off = off - r;
+        const uint32_t odd = r & 1u;
+
+        uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
+        uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
+        bool parsed = false, l4_needed = false;
+        if constexpr (!IPV4) {
+            span = ext = len;
+            if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
         } else {
-            ret = finalize(seed + acc_all - acc_x);
-            if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
-        }
-        p.out[f0 + lane] = (uint16_t)ret;
-    } else {
-        uint32_t net = 0, l4 = 0;
-        if (parsed) {
-            const uint32_t acc_hdr = hdr20 + acc_opt;
-            net = finalize(acc_hdr - (tx ? ipcrc : 0u));
-            if (!tx && net != 0) verdict |= V_NET_BAD;
-            const uint32_t tsum = acc_all - acc_hdr;
-            if (l4_needed) {
-                if (!tx) {
-                    if (proto == 6u || acc_x != 0u) {
-                        l4 = finalize(pseudo + tsum);
-                        if (l4 != 0) verdict |= V_L4_BAD;
+            const uint32_t avail = len;
+            if (avail >= 20) {
+                const uint32_t D[12] = {hcur.c0.x, hcur.c0.y, hcur.c0.z, hcur.c0.w, hcur.c1.x, hcur.c1.y,
+                                        hcur.c1.z, hcur.c1.w, hcur.c2.x, hcur.c2.y, hcur.c2.z, hcur.c2.w};
+                const uint32_t q = r >> 2, sh = r & 3u;
+                uint32_t E[6];
+#pragma unroll
+                for (int m = 0; m < 6; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+                uint32_t H[5];
+#pragma unroll
+                for (int m = 0; m < 5; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+                const uint32_t ihl = H[0] & 0x0Fu;
+                hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+                proto = (H[2] >> 8) & 0xFFu;
+                ipcrc = H[2] >> 16;
+                tl = (tot - hl) & 0xFFFFu;                              // uint16 wrap, pico_ipv4.c:395
+                const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;   // pico_ipv4.c:386
+                if (!(hl > avail || (!tx && tl > max_allowed) || hl + tl > avail)) {
+                    parsed = true;
+                    verdict = 0;
+                    span = ext = hl + tl;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
+                    pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
+                             (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
+                    if (hl > 20u) optend = r + hl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (hl + 8u > avail) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
+                        }
+                    } else {
+                        if (proto == 6u) {
+                            if (tl < 20u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 16u; }
+                        } else if (proto == 1u) {
+                            if (tl < 8u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 2u; }
+                        }
                     }
-                } else if (proto == 6u) {
-                    l4 = finalize(pseudo + tsum - acc_x);
-                } else {
-                    l4 = finalize(tsum - acc_x);
                 }
             }
-            if (verdict == 0) verdict = V_ACCEPT;
         }
-        if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
-            store_crc(fp + 10, net);
-            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
-            else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+        const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
+        const bool big = nch64 > BIG_CHUNKS;
+        const uint32_t nch = big ? 0u : (uint32_t)nch64;
+        const uint32_t pch = (nch + 7u) & ~7u;
+        const uint32_t incl = wave_scan_add(pch);
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t S = incl - pch;
+        const bool any_odd = __builtin_amdgcn_ballot_w64(nch64 != 0 && odd) != 0;
+        const bool any_x = __builtin_amdgcn_ballot_w64(nch64 != 0 && xpos != NONE) != 0;
+        const bool any_opt = IPV4 && __builtin_amdgcn_ballot_w64(nch != 0 && optend != 0) != 0;
+        uint64_t bigmask = __builtin_amdgcn_ballot_w64(big);
+        L.S[lane] = lane < cnt ? S : T;
+        L.acc_all[lane] = 0;
+        L.acc_x[lane] = 0;
+        L.acc_opt[lane] = 0;
+        L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (nch << 5));
+        L.xo[lane] = make_uint2(xpos, optend);
+        __builtin_amdgcn_wave_barrier();
+
+        // ---- prefetch: headers of the next batch, descriptors of the one after
+        if constexpr (IPV4) hcur = load_hdr(dnext);
+        dcur = dnext;
+        dnext = load_desc(b + 2 * W);
+
+        // ---- 2. stream this batch's chunk list
+        auto stream = [&](auto perm_tag) {
+            constexpr bool PERM = decltype(perm_tag)::value;
+            for (uint32_t t0 = 0; t0 < T; t0 += 64u * CPL) {
+                uint4 v[CPL];
+                uint32_t jj[CPL], kk[CPL];
+                uint4 fi[CPL];
+                bool ok[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t t = t0 + 64u * c + lane;
+                    uint32_t j = 0, sj = 0;
+#pragma unroll
+                    for (uint32_t step = 32; step; step >>= 1) {
+                        const uint32_t s2 = L.S[j + step];
+                        if (s2 <= t) { j += step; sj = s2; }
+                    }
+                    jj[c] = j;
+                    kk[c] = t - sj;
+                    fi[c] = L.info[j];
+                    ok[c] = t < T && kk[c] < (fi[c].w >> 5);
+                    const uint8_t* a0 = p.base + ((((uint64_t)fi[c].y) << 32) | fi[c].x);
+                    v[c] = ok[c] ? load_chunk_t<NT>(a0, kk[c]) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t k = kk[c], j = jj[c];
+                    const uint32_t rr = fi[c].w & 15u;
+                    const uint32_t sl = (fi[c].w & 16u) ? SEL_ODD : SEL_EVEN;
+                    const uint32_t ch = k << 4;
+                    uint32_t x = ok[c] ? masked_chunk_sum<PERM>(v[c], ch, rr, fi[c].z, sl) : 0u;
+                    if (any_x || any_opt) {
+                        const uint2 xo = L.xo[j];
+                        if (any_x && ok[c] && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4))) {
+                            const uint32_t xv = masked_chunk_sum<PERM>(v[c], ch, xo.x, xo.x + 2u, sl);
+                            if (xv) atomicAdd(&L.acc_x[j], xv);
+                        }
+                        if (IPV4 && any_opt && ok[c] && xo.y != 0u && ch < xo.y) {
+                            const uint32_t ov = masked_chunk_sum<PERM>(v[c], ch, rr + 20u, xo.y, sl);
+                            if (ov) atomicAdd(&L.acc_opt[j], ov);
+                        }
+                    }
+                    const bool blk_ok = (t0 + 64u * c + lane) < T;      // the lane's 8-block is in the list
+                    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+                    const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+                    const bool whole = k0 == k63 && __builtin_amdgcn_readlane((int)blk_ok, 63);
+                    if (whole) {                                     // the slot is one frame
+                        const uint32_t tot = group_sum<64>(x);
+                        if (lane == 63) atomicAdd(&L.acc_all[j], tot);
+                    } else {                                         // 8-lane runs, halves joined
+                        x = group_sum<8>(x);
+                        const uint32_t xm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+                        const uint32_t jm = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)j, 0x140, 0xF, 0xF, false);
+                        const bool same = jm == j;
+                        const uint32_t q = lane & 15u;
+                        const bool hi_ok = (t0 + 64u * c + (lane | 15u)) < T;
+                        const bool adder = blk_ok && (q == 15u || (q == 7u && (!same || !hi_ok)));
+                        const uint32_t val = (q == 15u && same) ? x + xm : x;
+                        if (adder) atomicAdd(&L.acc_all[j], val);
+                    }
+                }
+            }
+        };
+        if (T) {
+            if (any_odd) stream(std::integral_constant<bool, true>{});
+            else stream(std::integral_constant<bool, false>{});
         }
-        if (p.out_net) p.out_net[f0 + lane] = (uint16_t)net;
-        if (p.out_l4) p.out_l4[f0 + lane] = (uint16_t)l4;
-        if (p.verdict) p.verdict[f0 + lane] = (uint8_t)verdict;
+
+        // ---- 2b. frames over BIG_CHUNKS, one at a time by the whole wave
+        while (bigmask) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(bigmask);
+            bigmask &= bigmask - 1;
+            const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0off, (int)j);
+            const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a0off >> 32), (int)j);
+            const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)j);
+            const uint32_t bspan = (uint32_t)__builtin_amdgcn_readlane((int)span, (int)j);
+            const uint32_t bx = (uint32_t)__builtin_amdgcn_readlane((int)xpos, (int)j);
+            const uint64_t bend = (uint64_t)br + bspan;
+            const uint32_t bn = (uint32_t)((bend + 15u) >> 4);
+            const uint32_t bsel = (br & 1u) ? SEL_ODD : SEL_EVEN;
+            const uint8_t* a0 = p.base + (((uint64_t)bhi << 32) | blo);
+            uint32_t acc = 0, accx = 0;
+            for (uint32_t kb = 0; kb < bn; kb += 64u * CPL) {
+                uint4 v[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t k = kb + 64u * c + lane;
+                    v[c] = k < bn ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t k = kb + 64u * c + lane;
+                    const bool edge = k < bn && (k == 0 || k + 1 == bn);
+                    acc = add_full<true>(v[c], bsel, acc);
+                    if (edge) acc -= add_chunk(v[c], ~chunk_range_mask(k, br, bend) & 0xFFFFu, bsel, 0u);
+                    if (bx != NONE && (k == (bx >> 4) || k == ((bx + 1u) >> 4)))
+                        accx += add_chunk(v[c], chunk_range_mask(k, bx, (uint64_t)bx + 2u), bsel, 0u);
+                }
+            }
+            acc = group_sum<64>(acc);
+            accx = group_sum<64>(accx);
+            if (lane == 63) { L.acc_all[j] = acc; L.acc_x[j] = accx; }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS updates are done
+
+        // ---- 3. lane j finalizes frame j
+        if (lane < cnt) {
+            const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
+            if constexpr (!IPV4) {
+                uint32_t ret = 0;
+                if (oob) {
+                    if (p.bad) atomicAdd(p.bad, 1u);
+                } else {
+                    ret = finalize(seed + acc_all - acc_x);
+                    if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
+                }
+                p.out[f0 + lane] = (uint16_t)ret;
+            } else {
+                uint32_t net = 0, l4 = 0;
+                if (parsed) {
+                    const uint32_t acc_hdr = hdr20 + acc_opt;
+                    net = finalize(acc_hdr - (tx ? ipcrc : 0u));
+                    if (!tx && net != 0) verdict |= V_NET_BAD;
+                    const uint32_t tsum = acc_all - acc_hdr;
+                    if (l4_needed) {
+                        if (!tx) {
+                            if (proto == 6u || acc_x != 0u) {
+                                l4 = finalize(pseudo + tsum);
+                                if (l4 != 0) verdict |= V_L4_BAD;
+                            }
+                        } else if (proto == 6u) {
+                            l4 = finalize(pseudo + tsum - acc_x);
+                        } else {
+                            l4 = finalize(tsum - acc_x);
+                        }
+                    }
+                    if (verdict == 0) verdict = V_ACCEPT;
+                }
+                if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
+                    store_crc(fp + 10, net);
+                    if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
+                    else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+                }
+                if (p.out_net) p.out_net[f0 + lane] = (uint16_t)net;
+                if (p.out_l4) p.out_l4[f0 + lane] = (uint16_t)l4;
+                if (p.verdict) p.verdict[f0 + lane] = (uint8_t)verdict;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -913,6 +994,19 @@ extern "C" {
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
 
+// Per-wave adaptive descriptor kernel (16 frames per wave).
+int pico_csum_launch_desc_adaptive(void* base, uint64_t base_len, const void* desc, uint32_t n, int32_t crc_off,
+                                   uint32_t flags, uint16_t* out, uint32_t* bad, uint32_t nt, void* stream) {
+    if (n == 0) return (int)hipSuccess;
+    RawArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), 0, 0, n, 0,
+              crc_off, flags, 16u, out, bad};
+    const dim3 grid = grid_for(n, 16u), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    (void)nt;
+    hipLaunchKernelGGL(csum_desc_adaptive_kernel, grid, block, 0, s, a);
+    return (int)hipGetLastError();
+}
+
 // Software-pipelined uniform kernel (one pass per frame: G*CPL*16 >= len + 15).
 int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t* out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
@@ -925,8 +1019,9 @@ int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t st
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define X(g, c)                                                                                     \
     if (G == g && CPL == c) {                                                                       \
-        if (nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, true>), grid, block, 0, s, a);     \
-        else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, false>), grid, block, 0, s, a);       \
+        if (nt == 2) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 2>), grid, block, 0, s, a);   \
+        else if (nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 1>), grid, block, 0, s, a);   \
+        else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 0>), grid, block, 0, s, a);          \
         return (int)hipGetLastError();                                                              \
     }
     PICO_FOR_SHAPES(X)
@@ -964,12 +1059,14 @@ int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64
 int pico_csum_launch_flat(void* base, uint64_t base_len, const void* desc, uint32_t n, int ipv4,
                           int32_t crc_off, uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net,
                           uint16_t* out_l4, uint8_t* verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
-                          void* stream) {
-    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8) || fpw < 1 || fpw > 64) return (int)hipErrorInvalidValue;
+                          uint32_t max_blocks, void* stream) {
+    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8) || fpw < 1 || fpw > 64 || max_blocks == 0)
+        return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict};
-    const dim3 grid = grid_for(n, fpw), block(256);
+    dim3 grid = grid_for(n, fpw), block(256);
+    if (grid.x > max_blocks) grid.x = max_blocks;             // persistent: waves loop over batches
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define Z(c)                                                                                        \
     if (CPL == c) {                                                                                 \

@@ -42,6 +42,17 @@ def main():
         def launch(i):
             batch.checksum_uniform(bufs[i % rot], stride, ln, n, out=outs[i % rot])
         algo = n * ln + 2 * n
+    elif a.config in ("u354d", "c1d"):
+        # uniform frames fed as a descriptor batch (ablation: descriptor kernels vs uniform ones)
+        n, ln = {"u354d": (262144, 354), "c1d": (262144, 1500)}[a.config]
+        rot = 3
+        bufs = [torch.randint(0, 256, (n * ln,), dtype=torch.uint8, device=dev) for _ in range(rot)]
+        d_desc = batch.desc_to_device(batch.make_desc(np.arange(n, dtype=np.uint64) * ln, np.full(n, ln)), dev)
+        outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
+
+        def launch(i):
+            batch.checksum_batch(bufs[i % rot], d_desc, n, out=outs[i % rot])
+        algo = n * ln + 18 * n
     elif a.config in ("c2raw", "c2"):
         n = 262144
         lens = synth.imix_lengths(n, 3)
