@@ -660,7 +660,10 @@ struct FlatArgs {
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t BIG_CHUNKS = 1u << 16;   // frames above this stream on their own
 
+constexpr uint32_t FLAT_MAP_BLOCKS = 1024;   // 8-chunk blocks mapped per wave (8K chunks, 128 KiB)
+
 struct FlatWaveLds {
+    uint8_t map[FLAT_MAP_BLOCKS];  // 8-chunk block -> frame index (when the batch fits)
     uint32_t S[64];        // exclusive prefix of the padded chunk counts
     uint32_t acc_all[64];  // bytes [0, span) of the frame
     uint32_t acc_x[64];    // the isolated 2-byte field (RAW crc / UDP crc / TX crc)
@@ -800,6 +803,10 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         L.acc_opt[lane] = 0;
         L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (nch << 5));
         L.xo[lane] = make_uint2(xpos, optend);
+        // block -> frame map: a frame's blocks are written by its own lane
+        const bool use_map = T <= 8u * FLAT_MAP_BLOCKS;
+        if (use_map && lane < cnt)
+            for (uint32_t i = 0; i < (pch >> 3); ++i) L.map[(S >> 3) + i] = (uint8_t)lane;
         __builtin_amdgcn_wave_barrier();
 
         // ---- prefetch: headers of the next batch, descriptors of the one after
@@ -819,10 +826,15 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
                 for (int c = 0; c < CPL; ++c) {
                     const uint32_t t = t0 + 64u * c + lane;
                     uint32_t j = 0, sj = 0;
+                    if (use_map) {
+                        j = t < T ? L.map[t >> 3] : 63u;
+                        sj = L.S[j];
+                    } else {
 #pragma unroll
-                    for (uint32_t step = 32; step; step >>= 1) {
-                        const uint32_t s2 = L.S[j + step];
-                        if (s2 <= t) { j += step; sj = s2; }
+                        for (uint32_t step = 32; step; step >>= 1) {
+                            const uint32_t s2 = L.S[j + step];
+                            if (s2 <= t) { j += step; sj = s2; }
+                        }
                     }
                     jj[c] = j;
                     kk[c] = t - sj;
