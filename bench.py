@@ -48,6 +48,9 @@ CONFIGS = {
     "c2": dict(kind="ipv4", frames=262144,
                workload="C2: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams (14 B Ethernet header in front), "
                         "fused IPv4 header + TCP pseudo-header RX verify"),
+    "c2v6": dict(kind="ipv6", frames=262144,
+                 workload="C2 (IPv6, SURVEY 8f row 3): 256K simple-IMIX {64,576,1500}+20 B IPv6/TCP datagrams "
+                          "(14 B Ethernet header in front), fused IPv6 pseudo-header TCP RX verify"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -86,6 +89,17 @@ def make_c2(n, device, seed):
     d_desc = batch.desc_to_device(desc, device)
     # make every datagram valid with the TX kernel (untimed setup), so RX verify accepts
     batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize(device)
+    return d_buf, d_desc, int(lens.sum())
+
+
+def make_c2v6(n, device, seed):
+    lens = (synth.imix_lengths(n, seed) + 20).astype(np.uint32)
+    buf, net, avail, seeds = synth.ipv6_batch(lens, seed=seed + 1, proto=6, eth=True)
+    desc = batch.make_desc(net, avail, seeds)
+    d_buf = torch.from_numpy(buf).to(device)
+    d_desc = batch.desc_to_device(desc, device)
+    batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
     return d_buf, d_desc, int(lens.sum())
 
@@ -152,10 +166,19 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # Rehearsal knobs for a 1-GPU box (never set by the driver): every rank on GPU 0,
+    # timing collectives over gloo (RCCL cannot put two ranks on one GPU).
+    if os.environ.get("PICO_BENCH_SAME_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("PICO_BENCH_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
     if a.shape:
         batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
     cfg = CONFIGS[a.config]
@@ -176,7 +199,7 @@ def main():
             batch.checksum_uniform(bufs[i % rot], ln, ln, n, out=outs[i % rot])
         frame_bytes = per
         algo_bytes = per + 2 * n                            # frames read + uint16 results written
-    else:
+    elif cfg["kind"] == "ipv4":
         n = cfg["frames"]
         ln = 0
         rot = max(2, a.rotate)
@@ -187,6 +210,17 @@ def main():
             batch.ipv4_checksum_batch(b, d, n)
         frame_bytes = sets[0][2]
         algo_bytes = frame_bytes + 16 * n + 5 * n           # datagrams + descriptors + (2+2+1) B results
+    else:
+        n = cfg["frames"]
+        ln = 0
+        rot = max(2, a.rotate)
+        sets = [make_c2v6(n, dev, 700 + 13 * rank + i) for i in range(rot)]
+
+        def step(i):
+            b, d, _ = sets[i % rot]
+            batch.ipv6_checksum_batch(b, d, n)
+        frame_bytes = sets[0][2]
+        algo_bytes = frame_bytes + 16 * n + 3 * n           # datagrams + descriptors + (2+1) B results
 
     stream = torch.cuda.current_stream(dev)
     for i in range(a.warmup):
@@ -212,14 +246,14 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / a.steps
 
     # ... and whole-job time = max over ranks
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_max_ms = float(t[0]), float(t[1])
     ms_per_step = wall / a.steps * 1e3
     total_bytes = frame_bytes * (world if not cfg.get("strong") else 1)
     if cfg.get("strong"):
-        tb = torch.tensor([float(frame_bytes)], dtype=torch.float64, device=dev)
+        tb = torch.tensor([float(frame_bytes)], dtype=torch.float64, device=red_dev)
         if world > 1:
             dist.all_reduce(tb)
         total_bytes = float(tb[0])

@@ -137,6 +137,25 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_net,
                                  uint16_t *d_out_transport, uint8_t *d_verdict, void *stream);
 
+/* Fused IPv6 transport batch (TCP / UDP / ICMPv6 over IPv6),
+ * one datagram per descriptor: desc.off -> IPv6 header, desc.len = bytes
+ * available, desc.seed = f->net_len | (transport proto << 16) as
+ * pico_ipv6_extension_headers (pico_ipv6.c:707-800) leaves them -- the
+ * extension-header chain is control logic and stays in the stack; seed 0 = no
+ * extension headers (net_len 40, proto = hdr->nxthdr).  transport_len =
+ * (uint16)(payload_len - (net_len - 40)) (pico_ipv6.c:790); pseudo header =
+ * struct pico_ipv6_pseudo_hdr (pico_ipv6.h:46-53) from the IPv6 header.
+ * RX: pico_transport_crc_check (pico_socket.c:1916-1968; pico_tcp_checksum_ipv6
+ *   pico_tcp.c:449-475, pico_udp_checksum_ipv6 pico_udp.c:63-92): TCP always, UDP
+ *   when its crc != 0; ICMPv6 (pico_icmp6_checksum pico_icmp6.c:38-55) is always
+ *   computed, V_L4_BAD only for the ND / MLD types the reference checks
+ *   (pico_ipv6_nd.c:595, pico_mld.c:415).
+ * TX (F_TX): crc field read as zero (pico_tcp.c:980, pico_ipv6.c:1337,1345);
+ *   F_WRITE stores it.  d_out_transport: the checksum (0 = valid on RX). */
+int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                                 uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
+                                 void *stream);
+
 /* ---------------------------------------------------------------- layer 3 */
 
 struct pico_csum_ctx;   /* device, two streams, double-buffered staging */

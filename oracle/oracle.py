@@ -60,6 +60,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_batch_uniform.argtypes = [_vp, _u64, _u32, _u32, _u32, _vp]
         L.oracle_batch_ipv4.restype = None
         L.oracle_batch_ipv4.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _u32]
+        L.oracle_ipv6_pseudo_sum.restype = _u32
+        L.oracle_ipv6_pseudo_sum.argtypes = [_vp, _vp, ctypes.c_uint8, _u32]
+        L.oracle_batch_ipv6.restype = None
+        L.oracle_batch_ipv6.argtypes = [_vp, _vp, _u32, _vp, _vp, _u32]
         L.oracle_uniform_mt.restype = ctypes.c_double
         L.oracle_uniform_mt.argtypes = [_vp, _vp, _u64, _u32, _u32, _vp, _u32]
         _olib = L
@@ -95,6 +99,11 @@ def ipv4_pseudo_sum(src: bytes, dst: bytes, proto: int, tl: int) -> int:
     return lib().oracle_ipv4_pseudo_sum(_p(s), _p(d), proto, tl)
 
 
+def ipv6_pseudo_sum(src: bytes, dst: bytes, nxt: int, tl: int) -> int:
+    s, d = _buf(src), _buf(dst)
+    return lib().oracle_ipv6_pseudo_sum(_p(s), _p(d), nxt, tl)
+
+
 def batch_raw(base: np.ndarray, desc: np.ndarray, crc_off: int = -1) -> np.ndarray:
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
     out = np.zeros(desc.shape[0], dtype=np.uint16)
@@ -114,6 +123,14 @@ def batch_ipv4(base: np.ndarray, desc: np.ndarray, tx: bool = False):
     on, ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8)
     lib().oracle_batch_ipv4(_p(base), _p(desc), n, _p(on), _p(ol), _p(v), ORACLE_IPV4_TX if tx else 0)
     return on, ol, v
+
+
+def batch_ipv6(base: np.ndarray, desc: np.ndarray, tx: bool = False):
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    n = desc.shape[0]
+    ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint8)
+    lib().oracle_batch_ipv6(_p(base), _p(desc), n, _p(ol), _p(v), ORACLE_IPV4_TX if tx else 0)
+    return ol, v
 
 
 # ---------------------------------------------------------------- reference

@@ -216,6 +216,108 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
     }
 }
 
+/* modules/pico_ipv6.h:46-53 struct pico_ipv6_pseudo_hdr {src[16], dst[16], len (32-bit BE),
+ * zero[3], nxthdr}, summed by pico_checksum_adder as pico_tcp_checksum_ipv6
+ * (pico_tcp.c:449-475), pico_udp_checksum_ipv6 (pico_udp.c:63-92) and
+ * pico_icmp6_checksum (pico_icmp6.c:38-55) pass it as buffer 1. */
+uint32_t oracle_ipv6_pseudo_sum(const uint8_t src[16], const uint8_t dst[16], uint8_t nxthdr, uint32_t transport_len)
+{
+    uint8_t ph[40];
+    memcpy(ph, src, 16);
+    memcpy(ph + 16, dst, 16);
+    ph[32] = (uint8_t)(transport_len >> 24);
+    ph[33] = (uint8_t)(transport_len >> 16);
+    ph[34] = (uint8_t)(transport_len >> 8);
+    ph[35] = (uint8_t)transport_len;
+    ph[36] = ph[37] = ph[38] = 0;
+    ph[39] = nxthdr;
+    return oracle_checksum_adder(0, ph, 40);
+}
+
+static int icmp6_checked_type(uint8_t t)
+{
+    /* ND: pico_ipv6_nd.c:595 (types 133-137); MLD: pico_mld.c:415 (130-132, 143) */
+    return (t >= 133 && t <= 137) || (t >= 130 && t <= 132) || t == 143;
+}
+
+/*
+ * Fused IPv6 transport restatement, one datagram per descriptor.  desc.off ->
+ * IPv6 header; desc.len = bytes available; desc.seed = f->net_len | proto << 16
+ * as pico_ipv6_extension_headers (modules/pico_ipv6.c:707-800) leaves them
+ * (seed 0: net_len 40, proto = hdr->nxthdr).
+ *   transport_len = (uint16)(payload_len - (net_len - 40))     pico_ipv6.c:790
+ * RX: pico_transport_crc_check (stack/pico_socket.c:1916-1968): TCP always (any
+ *   length), UDP when the stored crc (t[6..7], inside the buffer) != 0; ICMPv6:
+ *   pico_icmp6_checksum, a verdict only for the ND / MLD types the reference
+ *   checks (type byte t[0] inside the buffer).  Other protocols: none.
+ *   out = the checksum (0 = valid), 0 when none is computed.
+ * TX: crc field read as zero (TCP pico_tcp.c:980, ICMPv6 pico_ipv6.c:1337, UDP
+ *   crc already 0 from pico_udp_push :123 when pico_ipv6.c:1345 computes it);
+ *   TCP needs 20, UDP 8, ICMPv6 4 transport bytes.  Other protocols: none.
+ * MALFORMED: avail < 40, net_len < 40 or past avail, transport past avail, or a
+ *   field the reference reads lying past avail.
+ */
+void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                       uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
+{
+    uint32_t i;
+    int tx = (flags & ORACLE_IPV4_TX) != 0;
+    for (i = 0; i < n; i++) {
+        const uint8_t *h = base + d[i].off;
+        const uint8_t *t;
+        uint32_t avail = d[i].len, net_len, plen, s;
+        uint16_t tl;
+        uint8_t proto, v = 0;
+        uint16_t l4 = 0;
+
+        out_l4[i] = 0;
+        verdict[i] = PICO_CSUM_V_MALFORMED;
+        if (avail < 40)
+            continue;
+        net_len = d[i].seed & 0xFFFFu;
+        proto = (uint8_t)(d[i].seed >> 16);
+        if (d[i].seed == 0) {
+            net_len = 40;
+            proto = h[6];
+        }
+        plen = (uint32_t)((h[4] << 8) | h[5]);
+        if (net_len < 40 || net_len > avail)
+            continue;
+        tl = (uint16_t)(plen - (net_len - 40u));               /* pico_ipv6.c:790 */
+        if (net_len + (uint32_t)tl > avail)
+            continue;
+        t = h + net_len;
+        s = oracle_ipv6_pseudo_sum(h + 8, h + 24, proto, tl);
+        if (!tx) {
+            if (proto == 6) {
+                l4 = oracle_checksum_finalize(oracle_checksum_adder(s, t, tl));
+                if (l4) v |= PICO_CSUM_V_L4_BAD;
+            } else if (proto == 17) {
+                if (net_len + 8u > avail) continue;
+                if (t[6] || t[7]) {
+                    l4 = oracle_checksum_finalize(oracle_checksum_adder(s, t, tl));
+                    if (l4) v |= PICO_CSUM_V_L4_BAD;
+                }
+            } else if (proto == 58) {
+                if (net_len + 1u > avail) continue;
+                l4 = oracle_checksum_finalize(oracle_checksum_adder(s, t, tl));
+                if (l4 && icmp6_checked_type(t[0])) v |= PICO_CSUM_V_L4_BAD;
+            }
+        } else {
+            int xoff = proto == 6 ? 16 : proto == 17 ? 6 : proto == 58 ? 2 : -1;
+            uint32_t need = proto == 6 ? 20u : proto == 17 ? 8u : 4u;
+            if (xoff >= 0) {
+                if (tl < need) continue;
+                s = oracle_checksum_adder(s, t, tl);
+                s -= (uint32_t)(t[xoff] | (t[xoff + 1] << 8));
+                l4 = oracle_checksum_finalize(s);
+            }
+        }
+        out_l4[i] = l4;
+        verdict[i] = (uint8_t)(v == 0 ? PICO_CSUM_V_ACCEPT : v);
+    }
+}
+
 /* ---- multi-threaded CPU baseline driver (bench.py cpu_baseline leg) ---- */
 
 struct mt_job {

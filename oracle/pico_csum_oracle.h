@@ -33,6 +33,9 @@ void oracle_batch_uniform(const uint8_t *base, uint64_t stride, uint32_t len, ui
                           uint32_t seed, uint16_t *out);
 void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
                        uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
+uint32_t oracle_ipv6_pseudo_sum(const uint8_t src[16], const uint8_t dst[16], uint8_t nxthdr, uint32_t transport_len);
+void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
+                       uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
                          uint32_t n, uint16_t *out, uint32_t nthreads);
 #endif

@@ -22,6 +22,7 @@ EXPORTED = (
     "pico_checksum_batch_dev",
     "pico_checksum_batch_uniform_dev",
     "pico_ipv4_checksum_batch_dev",
+    "pico_ipv6_checksum_batch_dev",
     "pico_csum_ctx_create",
     "pico_csum_ctx_destroy",
     "pico_checksum_batch_uniform_host",
@@ -73,6 +74,7 @@ def load() -> ctypes.CDLL:
     sig("pico_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, i32, u32, vp, vp, vp)
     sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u64, u32, u32, u32, vp, vp)
     sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp)
+    sig("pico_ipv6_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
     sig("pico_csum_ctx_destroy", None, vp)
     sig("pico_checksum_batch_uniform_host", ctypes.c_int, vp, vp, u64, u32, u32, u32, vp)

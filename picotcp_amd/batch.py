@@ -114,6 +114,24 @@ def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     return out_net, out_l4, verdict
 
 
+def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None):
+    """Fused IPv6 transport checksums (TCP / UDP / ICMPv6; RX verify, or TX compute with
+    F_TX).  desc.seed = net_len | proto << 16 (0: no extension headers).
+    Returns (out_transport int16[n], verdict uint8[n])."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    dev = base.device
+    out_l4 = torch.empty(n, dtype=torch.int16, device=dev)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    lib = _lib.load()
+    _lib.check("pico_ipv6_checksum_batch_dev",
+               lib.pico_ipv6_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_l4),
+                                                _ptr(verdict), _stream_handle(stream)))
+    return out_l4, verdict
+
+
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int = 1, nt: int = 0,
                         pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic."""

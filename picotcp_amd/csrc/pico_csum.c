@@ -31,7 +31,7 @@ int pico_csum_launch_desc_adaptive(void *base, uint64_t base_len, const void *de
 int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
                                 void *stream);
-int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int ipv4,
+int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode,
                           int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
                           uint32_t max_blocks, void *stream);
@@ -326,6 +326,37 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),
                          "pico_ipv4_checksum_batch_dev");
+}
+
+int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
+                                 uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
+                                 void *stream)
+{
+    struct shape s;
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+    if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
+    if ((rc = need_device()) != 0)
+        return rc;
+    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (s.G != 1) {           /* the IPv6 mode exists in the flat kernel only */
+        s.G = 1;
+        s.CPL = 2;
+        s.U = 0;
+        s.fpw = n / 16384u < 1 ? 1 : n / 16384u > 64 ? 64 : n / 16384u;
+    }
+    return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
+                                               d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
+                                               s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                         "pico_ipv6_checksum_batch_dev");
 }
 
 /* ------------------------------------------------------------------ layer 3 */

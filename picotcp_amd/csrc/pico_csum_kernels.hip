@@ -676,8 +676,10 @@ struct FlatWaveLds {
 // The next batch's descriptors (two batches ahead) and IPv4 header chunks (one
 // ahead) are loaded before the current batch streams, so their HBM round trips
 // overlap the stream instead of preceding it.
-template <bool IPV4, int CPL, bool NT>
+// MODE: 0 RAW, 1 fused IPv4, 2 fused IPv6 transport (TCP / UDP / ICMPv6).
+template <int MODE, int CPL, bool NT>
 __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
+    constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2;
     __shared__ FlatWaveLds lds_all[4];
     const uint32_t lane = threadIdx.x & 63u;
     FlatWaveLds& L = lds_all[threadIdx.x >> 6];
@@ -685,7 +687,8 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
     const uint64_t nb = ((uint64_t)p.n + p.fpw - 1) / p.fpw;
     uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (b >= nb) return;
-    const bool tx = IPV4 && (p.flags & 2u) != 0;
+    const bool tx = MODE != 0 && (p.flags & 2u) != 0;
+    constexpr uint32_t HDR = IPV6 ? 40u : 20u;      // fixed header bytes parsed in phase 1
 
     auto load_desc = [&](uint64_t bb) {
         uint4 d = make_uint4(0, 0, 0, 0);
@@ -695,20 +698,22 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         }
         return d;
     };
-    // header window (IPv4): the chunks covering header bytes [0, 20) of the lane's frame
-    struct Hdr { uint4 c0, c1, c2; };
+    // header window: the chunks covering the fixed header of the lane's datagram
+    struct Hdr { uint4 c0, c1, c2, c3; };
     auto load_hdr = [&](const uint4 d) {
-        Hdr h{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-        if constexpr (IPV4) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        Hdr h{z, z, z, z};
+        if constexpr (MODE != 0) {
             const uint64_t off = ((uint64_t)d.y << 32) | d.x;
             const uint32_t len = d.z;
-            if (len >= 20u && off <= p.base_len && len <= p.base_len - off) {
+            if (len >= HDR && off <= p.base_len && len <= p.base_len - off) {
                 uint8_t* fp = p.base + off;
                 const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
                 const uint8_t* a0 = fp - r;
                 h.c0 = load_chunk(a0, 0);
-                if (r + 20 > 16) h.c1 = load_chunk(a0, 1);
-                if (r + 20 > 32) h.c2 = load_chunk(a0, 2);
+                if (r + HDR > 16) h.c1 = load_chunk(a0, 1);
+                if (r + HDR > 32) h.c2 = load_chunk(a0, 2);
+                if (IPV6 && r + HDR > 48) h.c3 = load_chunk(a0, 3);
             }
         }
         return h;
@@ -729,17 +734,17 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
         if (oob || lane >= cnt) { len = 0; off = 0; }
         uint8_t* fp = p.base + off;
-        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
-        const uint64_t a0off = off - r;
-        const uint32_t odd = r & 1u;
+        uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+        uint64_t a0off = off - r;
+        uint32_t odd = r & 1u;
 
         uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
         uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
         bool parsed = false, l4_needed = false;
-        if constexpr (!IPV4) {
+        if constexpr (MODE == 0) {
             span = ext = len;
             if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
-        } else {
+        } else if constexpr (IPV4) {
             const uint32_t avail = len;
             if (avail >= 20) {
                 const uint32_t D[12] = {hcur.c0.x, hcur.c0.y, hcur.c0.z, hcur.c0.w, hcur.c1.x, hcur.c1.y,
@@ -785,6 +790,64 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
                     }
                 }
             }
+        } else {
+            // IPv6: pico_ipv6.c:707-800 lengths, pico_ipv6.h:46-53 pseudo header.  The
+            // streamed region is the transport [net_len, net_len + tl) alone.
+            const uint32_t avail = len;
+            if (avail >= 40) {
+                const uint32_t D[16] = {hcur.c0.x, hcur.c0.y, hcur.c0.z, hcur.c0.w, hcur.c1.x, hcur.c1.y,
+                                        hcur.c1.z, hcur.c1.w, hcur.c2.x, hcur.c2.y, hcur.c2.z, hcur.c2.w,
+                                        hcur.c3.x, hcur.c3.y, hcur.c3.z, hcur.c3.w};
+                const uint32_t q = r >> 2, sh = r & 3u;
+                uint32_t E[11];
+#pragma unroll
+                for (int m = 0; m < 11; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+                uint32_t H[10];
+#pragma unroll
+                for (int m = 0; m < 10; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+                uint32_t net_len = seed & 0xFFFFu;
+                proto = (seed >> 16) & 0xFFu;
+                if (seed == 0) { net_len = 40u; proto = (H[1] >> 16) & 0xFFu; }
+                tl = (plen - (net_len - 40u)) & 0xFFFFu;                // pico_ipv6.c:790
+                if (net_len >= 40u && net_len <= avail && net_len + tl <= avail) {
+                    uint32_t addr = 0, xrel = NONE;
+#pragma unroll
+                    for (int m = 2; m < 10; ++m) addr = dot2_add(H[m], addr);
+                    pseudo = addr + (((tl & 0xFFu) << 8) | (tl >> 8)) + (proto << 8);
+                    parsed = true;
+                    verdict = 0;
+                    ext = tl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (net_len + 8u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 6u; ext = max(tl, 8u); }
+                        } else if (proto == 58u) {
+                            if (net_len + 1u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 0u; ext = max(tl, 1u); }
+                        }
+                    } else {
+                        const uint32_t need = proto == 6u ? 20u : proto == 17u ? 8u : 4u;
+                        if (proto == 6u || proto == 17u || proto == 58u) {
+                            if (tl < need) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = proto == 6u ? 16u : proto == 17u ? 6u : 2u; }
+                        }
+                    }
+                    if (parsed) {
+                        off += net_len;                             // the region: the transport
+                        fp = p.base + off;
+                        r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+                        a0off = off - r;
+                        odd = r & 1u;
+                        span = tl;
+                        if (xrel != NONE) xpos = r + xrel;
+                    } else {
+                        ext = 0;
+                    }
+                }
+            }
         }
         const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
         const bool big = nch64 > BIG_CHUNKS;
@@ -810,7 +873,7 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         __builtin_amdgcn_wave_barrier();
 
         // ---- prefetch: headers of the next batch, descriptors of the one after
-        if constexpr (IPV4) hcur = load_hdr(dnext);
+        if constexpr (MODE != 0) hcur = load_hdr(dnext);
         dcur = dnext;
         dnext = load_desc(b + 2 * W);
 
@@ -928,7 +991,7 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         // ---- 3. lane j finalizes frame j
         if (lane < cnt) {
             const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
-            if constexpr (!IPV4) {
+            if constexpr (MODE == 0) {
                 uint32_t ret = 0;
                 if (oob) {
                     if (p.bad) atomicAdd(p.bad, 1u);
@@ -937,6 +1000,27 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
                     if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
                 }
                 p.out[f0 + lane] = (uint16_t)ret;
+            } else if constexpr (IPV6) {
+                uint32_t l4 = 0;
+                if (parsed) {
+                    if (l4_needed) {
+                        if (!tx) {
+                            if (proto == 6u || (proto == 17u && acc_x != 0u) || proto == 58u) {
+                                l4 = finalize(pseudo + acc_all);
+                                const uint32_t type = acc_x & 0xFFu;   // ICMPv6 type (x field = [0, 2))
+                                const bool checked = proto != 58u || (type >= 130u && type <= 137u) || type == 143u;
+                                if (l4 != 0 && checked) verdict |= V_L4_BAD;
+                            }
+                        } else {
+                            l4 = finalize(pseudo + acc_all - acc_x);
+                        }
+                    }
+                    if (verdict == 0) verdict = V_ACCEPT;
+                }
+                if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l4_needed)
+                    store_crc(fp + (xpos - r), l4);
+                if (p.out_l4) p.out_l4[f0 + lane] = (uint16_t)l4;
+                if (p.verdict) p.verdict[f0 + lane] = (uint8_t)verdict;
             } else {
                 uint32_t net = 0, l4 = 0;
                 if (parsed) {
@@ -1067,8 +1151,8 @@ int pico_csum_launch_raw(void* base, uint64_t base_len, const void* desc, uint64
     return (int)hipErrorInvalidValue;
 }
 
-// Flat work-list kernel for descriptor batches: ipv4 = 0 RAW, 1 fused IPv4.
-int pico_csum_launch_flat(void* base, uint64_t base_len, const void* desc, uint32_t n, int ipv4,
+// Flat work-list kernel for descriptor batches: mode 0 RAW, 1 fused IPv4, 2 fused IPv6.
+int pico_csum_launch_flat(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode,
                           int32_t crc_off, uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net,
                           uint16_t* out_l4, uint8_t* verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
                           uint32_t max_blocks, void* stream) {
@@ -1082,12 +1166,15 @@ int pico_csum_launch_flat(void* base, uint64_t base_len, const void* desc, uint3
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define Z(c)                                                                                        \
     if (CPL == c) {                                                                                 \
-        if (ipv4) {                                                                                 \
-            if (nt) hipLaunchKernelGGL((csum_flat_kernel<true, c, true>), grid, block, 0, s, a);    \
-            else hipLaunchKernelGGL((csum_flat_kernel<true, c, false>), grid, block, 0, s, a);      \
+        if (mode == 2) {                                                                            \
+            if (nt) hipLaunchKernelGGL((csum_flat_kernel<2, c, true>), grid, block, 0, s, a);       \
+            else hipLaunchKernelGGL((csum_flat_kernel<2, c, false>), grid, block, 0, s, a);         \
+        } else if (mode == 1) {                                                                     \
+            if (nt) hipLaunchKernelGGL((csum_flat_kernel<1, c, true>), grid, block, 0, s, a);       \
+            else hipLaunchKernelGGL((csum_flat_kernel<1, c, false>), grid, block, 0, s, a);         \
         } else {                                                                                    \
-            if (nt) hipLaunchKernelGGL((csum_flat_kernel<false, c, true>), grid, block, 0, s, a);   \
-            else hipLaunchKernelGGL((csum_flat_kernel<false, c, false>), grid, block, 0, s, a);     \
+            if (nt) hipLaunchKernelGGL((csum_flat_kernel<0, c, true>), grid, block, 0, s, a);       \
+            else hipLaunchKernelGGL((csum_flat_kernel<0, c, false>), grid, block, 0, s, a);         \
         }                                                                                           \
         return (int)hipGetLastError();                                                              \
     }

@@ -109,3 +109,59 @@ def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = T
         buf[t + 3] = 0
     avail = lengths.copy()
     return buf, net, avail
+
+
+def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = True, hbh: bool = False,
+               icmp_type: int = 128):
+    """IPv6 datagrams of the given total lengths (40-byte header + optional 8-byte
+    hop-by-hop header + transport), packed back to back, crc fields zero.  proto
+    6 / 17 / 58 (ICMPv6 of `icmp_type`).  Returns (buffer, net offsets, available
+    bytes, descriptor seeds): seed = net_len | proto << 16 when a hop-by-hop header
+    is present (what pico_ipv6_extension_headers leaves in the frame), else 0."""
+    lengths = np.asarray(lengths, dtype=np.uint32)
+    n = lengths.size
+    pre = 14 if eth else 0
+    frame_len = lengths.astype(np.uint64) + pre
+    starts = np.zeros(n, dtype=np.uint64)
+    if n:
+        starts[1:] = np.cumsum(frame_len)[:-1]
+    buf = random_bytes(seed, int(frame_len.sum()))
+    net = starts + np.uint64(pre)
+    idx = net.astype(np.int64)
+    net_len = 48 if hbh else 40
+    plen = (lengths - 40).astype(np.uint32)
+    if eth:
+        e = starts.astype(np.int64)
+        buf[e + 12] = 0x86
+        buf[e + 13] = 0xDD
+    buf[idx + 0] = 0x60
+    buf[idx + 4] = (plen >> 8).astype(np.uint8)
+    buf[idx + 5] = (plen & 0xFF).astype(np.uint8)
+    buf[idx + 6] = 0 if hbh else proto
+    buf[idx + 7] = 255 if proto == 58 else 64
+    if hbh:
+        buf[idx + 40] = proto        # next header
+        buf[idx + 41] = 0            # length: 8 bytes
+        buf[idx + 42] = 1            # PadN
+        buf[idx + 43] = 4
+        for o in range(44, 48):
+            buf[idx + o] = 0
+    t = idx + net_len
+    if proto == 6:
+        buf[t + 12] = 0x50
+        buf[t + 13] = 0x18
+        buf[t + 16] = 0
+        buf[t + 17] = 0
+    elif proto == 17:
+        ul = (lengths - net_len).astype(np.uint32)
+        buf[t + 4] = (ul >> 8).astype(np.uint8)
+        buf[t + 5] = (ul & 0xFF).astype(np.uint8)
+        buf[t + 6] = 0
+        buf[t + 7] = 0
+    elif proto == 58:
+        buf[t + 0] = icmp_type
+        buf[t + 1] = 0
+        buf[t + 2] = 0
+        buf[t + 3] = 0
+    seeds = np.full(n, (net_len | (proto << 16)) if hbh else 0, dtype=np.uint32)
+    return buf, net, lengths.copy(), seeds

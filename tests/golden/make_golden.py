@@ -19,6 +19,7 @@ Outputs (data only -- inputs and expected outputs):
   kat.json         reference KATs (unit tests, RFC 1071) + edge cases
   raw_cases.npz    seeded random regions (splitmix64 byte source, picotcp_amd/synth.py)
   ipv4_cases.npz   IPv4/TCP/UDP/ICMP datagrams (valid + corrupted) with RX/TX expectations
+  ipv6_cases.npz   IPv6/TCP/UDP/ICMPv6 datagrams (hop-by-hop, ND/MLD types, corruptions) with RX/TX expectations
 """
 from __future__ import annotations
 
@@ -359,6 +360,135 @@ def unit_socket_frames() -> dict:
                 rx_verdict=rx[:, 2].astype(np.uint8), notes=np.array(notes))
 
 
+# --- IPv6 caller logic (independent Python restatement) ----------------------
+
+ND_MLD_TYPES = {130, 131, 132, 143, 133, 134, 135, 136, 137}
+
+
+def pseudo6(src: bytes, dst: bytes, nxt: int, tl: int) -> bytes:
+    """struct pico_ipv6_pseudo_hdr (modules/pico_ipv6.h:46-53): len = long_be(tl)."""
+    return src + dst + tl.to_bytes(4, "big") + bytes([0, 0, 0, nxt])
+
+
+def ipv6_expect(buf: np.ndarray, off: int, avail: int, seed: int, tx: bool):
+    """(out_l4, verdict) for one IPv6 datagram; see oracle_batch_ipv6 / the module doc."""
+    refd = O.ref_dualbuffer_checksum
+    MAL, L4, ACC = 8, 4, 1
+    if avail < 40:
+        return 0, MAL
+    h = buf[off:off + avail].tobytes()
+    net_len, proto = (seed & 0xFFFF, (seed >> 16) & 0xFF) if seed else (40, h[6])
+    plen = (h[4] << 8) | h[5]
+    if net_len < 40 or net_len > avail:
+        return 0, MAL
+    tl = (plen - (net_len - 40)) & 0xFFFF                 # pico_ipv6.c:790
+    if net_len + tl > avail:
+        return 0, MAL
+    t = bytearray(h[net_len:net_len + tl])
+    ps = pseudo6(h[8:24], h[24:40], proto, tl)
+    if not tx:
+        if proto == 6:
+            c = refd(ps, bytes(t))
+            return c, (L4 if c else ACC)
+        if proto == 17:
+            if net_len + 8 > avail:
+                return 0, MAL
+            if h[net_len + 6] == 0 and h[net_len + 7] == 0:
+                return 0, ACC
+            c = refd(ps, bytes(t))
+            return c, (L4 if c else ACC)
+        if proto == 58:
+            if net_len + 1 > avail:
+                return 0, MAL
+            c = refd(ps, bytes(t))
+            return c, (L4 if (c and h[net_len] in ND_MLD_TYPES) else ACC)
+        return 0, ACC
+    xoff, need = {6: (16, 20), 17: (6, 8), 58: (2, 4)}.get(proto, (None, 0))
+    if xoff is None:
+        return 0, ACC
+    if tl < need:
+        return 0, MAL
+    t[xoff:xoff + 2] = b"\0\0"
+    return refd(ps, bytes(t)), ACC
+
+
+def ipv6_cases() -> dict:
+    rng = np.random.default_rng(6060)
+    parts = []
+    specs = [
+        dict(lengths=synth.imix_lengths(160, 61) + 20, proto=6, eth=True, hbh=False, seed=201),
+        dict(lengths=rng.integers(48, 1500, 80).astype(np.uint32), proto=17, eth=True, hbh=False, seed=202),
+        dict(lengths=rng.integers(48, 600, 40).astype(np.uint32), proto=58, eth=False, hbh=False, seed=203,
+             icmp_type=128),
+        dict(lengths=rng.integers(64, 200, 30).astype(np.uint32), proto=58, eth=True, hbh=False, seed=204,
+             icmp_type=135),
+        dict(lengths=rng.integers(64, 200, 30).astype(np.uint32), proto=58, eth=True, hbh=True, seed=205,
+             icmp_type=131),
+        dict(lengths=rng.integers(80, 1500, 40).astype(np.uint32), proto=6, eth=True, hbh=True, seed=206),
+        dict(lengths=np.array([65535 + 40 - 1, 9000, 60, 48], dtype=np.uint32), proto=6, eth=True, hbh=False,
+             seed=207),
+    ]
+    seeds_all = []
+    for sp in specs:
+        kw = dict(seed=sp["seed"], proto=sp["proto"], eth=sp["eth"], hbh=sp["hbh"])
+        if "icmp_type" in sp:
+            kw["icmp_type"] = sp["icmp_type"]
+        lens = np.maximum(sp["lengths"], 48 + 20).astype(np.uint32)
+        b, nt, av, sd = synth.ipv6_batch(lens, **kw)
+        parts.append((b, nt, av))
+        seeds_all.append(sd)
+    bufs, nets, avs = [], [], []
+    base = 0
+    for b, nt, av in parts:
+        bufs.append(b)
+        nets.append(nt + np.uint64(base))
+        avs.append(av)
+        base += b.size
+    buf = np.concatenate(bufs)
+    net = np.concatenate(nets)
+    avail = np.concatenate(avs).astype(np.uint32)
+    seeds = np.concatenate(seeds_all).astype(np.uint32)
+    n = net.size
+    tx_buf = buf.copy()
+    # valid checksums the way the reference TX path writes them
+    for i in range(n):
+        o = int(net[i])
+        c, v = ipv6_expect(buf, o, int(avail[i]), int(seeds[i]), True)
+        if v != 1:
+            continue
+        nl, proto = (int(seeds[i]) & 0xFFFF, int(seeds[i]) >> 16) if seeds[i] else (40, int(buf[o + 6]))
+        xoff = {6: 16, 17: 6, 58: 2}.get(proto)
+        if xoff is not None:
+            buf[o + nl + xoff] = c >> 8
+            buf[o + nl + xoff + 1] = c & 0xFF
+    kind = np.zeros(n, dtype=np.uint8)
+    for i in range(n):
+        r = rng.random()
+        o, a = int(net[i]), int(avail[i])
+        nl = (int(seeds[i]) & 0xFFFF) if seeds[i] else 40
+        if r < 0.55:
+            continue
+        if r < 0.68:
+            buf[o + 8 + int(rng.integers(0, 32))] ^= 0x01; kind[i] = 1       # address flip -> pseudo mismatch
+        elif r < 0.80:
+            buf[o + nl + int(rng.integers(0, max(1, a - nl)))] ^= 0x40; kind[i] = 2  # transport flip
+        elif r < 0.85:
+            avail[i] = max(0, a - int(rng.integers(1, 30))); kind[i] = 3     # truncated buffer
+        elif r < 0.90:
+            buf[o + 4] = 0xFF; buf[o + 5] = 0xF0; kind[i] = 4              # payload length past the buffer
+        elif r < 0.94 and (seeds[i] == 0 and buf[o + 6] == 17):
+            buf[o + nl + 6] = 0; buf[o + nl + 7] = 0; kind[i] = 5           # UDP crc 0 -> not verified
+        elif r < 0.97:
+            avail[i] = int(rng.integers(0, 40)); kind[i] = 6                # shorter than the IPv6 header
+        else:
+            seeds[i] = 20 | (6 << 16); kind[i] = 7                          # net_len < 40
+    rx = np.array([ipv6_expect(buf, int(net[i]), int(avail[i]), int(seeds[i]), False) for i in range(n)])
+    tx = np.array([ipv6_expect(tx_buf, int(net[i]), int(avail[i]), int(seeds[i]), True) for i in range(n)])
+    return dict(buf=buf, tx_buf=tx_buf, net=net, avail=avail, seed=seeds, kind=kind,
+                rx_l4=rx[:, 0].astype(np.uint16), rx_verdict=rx[:, 1].astype(np.uint8),
+                tx_l4=tx[:, 0].astype(np.uint16), tx_verdict=tx[:, 1].astype(np.uint8))
+
+
 def main() -> None:
     if not O.ref_available():
         sys.exit("oracle/_ref/libpicoref.so missing: run `make -C oracle ref` first")
@@ -373,6 +503,9 @@ def main() -> None:
     np.savez_compressed(os.path.join(OUT, "raw_cases.npz"), **flat)
     ic = ipv4_cases()
     np.savez_compressed(os.path.join(OUT, "ipv4_cases.npz"), **ic)
+    i6 = ipv6_cases()
+    np.savez_compressed(os.path.join(OUT, "ipv6_cases.npz"), **i6)
+    print("ipv6 cases:", i6["net"].size, "RX verdicts:", np.unique(i6["rx_verdict"], return_counts=True))
     us = unit_socket_frames()
     np.savez_compressed(os.path.join(OUT, "unit_socket_frames.npz"), **us)
     print("kat:", len(k["checksum"]), "checksum,", len(k["dualbuffer"]), "dualbuffer,", len(k["fill"]), "fill")

@@ -54,3 +54,14 @@ def ipv4_desc(net: np.ndarray, avail: np.ndarray) -> np.ndarray:
     d["off"] = net
     d["len"] = avail
     return d
+
+
+def ipv6_cases() -> dict:
+    z = np.load(os.path.join(GOLDEN, "ipv6_cases.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def ipv6_desc(c: dict) -> np.ndarray:
+    d = ipv4_desc(c["net"], c["avail"])
+    d["seed"] = c["seed"]
+    return d

@@ -79,6 +79,10 @@ def test_argument_validation():
     # F_WRITE on an RX ipv4 batch
     assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_WRITE, None, None, None,
                                             None) == -_lib.EINVAL
+    assert lib.pico_ipv6_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_WRITE, None, None,
+                                            None) == -_lib.EINVAL
+    assert lib.pico_ipv6_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2004), 4, 0, None, None, None) \
+        == -_lib.EINVAL
     # NULL buffers
     assert lib.pico_checksum_batch_uniform_dev(None, 6000, 1500, 1500, 4, 0, vp(0x3000), None) == -_lib.EINVAL
     # frames past base_len

@@ -324,3 +324,42 @@ def test_host_batch_roundtrip():
     finally:
         hb.close()
     np.testing.assert_array_equal(got, want)
+
+
+# ------------------------------------------------------------------ IPv6 fused
+
+@pytest.mark.parametrize("c", [1, 2, 4, 8])
+def test_ipv6_golden_rx_tx(c):
+    cs = G.ipv6_cases()
+    desc = batch.desc_to_device(G.ipv6_desc(cs), DEV)
+    n = cs["net"].size
+    for fpw in (1, 13, 64):
+        batch.set_launch_override(1, c, fpw, 0, 1)
+        l4, v = batch.ipv6_checksum_batch(to_dev(cs["buf"]), desc, n)
+        np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"c={c} fpw={fpw}")
+        np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"c={c} fpw={fpw}")
+        l4, v = batch.ipv6_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
+        np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"], err_msg=f"TX c={c} fpw={fpw}")
+        np.testing.assert_array_equal(u16(l4), cs["tx_l4"], err_msg=f"TX c={c} fpw={fpw}")
+
+
+@pytest.mark.parametrize("proto,hbh,icmp_type", [(6, False, 0), (17, False, 0), (58, False, 135), (6, True, 0),
+                                                 (58, True, 131)])
+def test_ipv6_tx_write_then_rx_accepts(proto, hbh, icmp_type):
+    lens = np.maximum(synth.imix_lengths(20000, 3 + proto), 48 + 20).astype(np.uint32)
+    kw = dict(seed=proto + 7, proto=proto, eth=True, hbh=hbh)
+    if proto == 58:
+        kw["icmp_type"] = icmp_type
+    buf, net_off, avail, seeds = synth.ipv6_batch(lens, **kw)
+    desc_h = G.ipv4_desc(net_off, avail)
+    desc_h["seed"] = seeds
+    want_l4, want_v = O.batch_ipv6(buf, desc_h, tx=True)
+    assert (want_v == 1).all()
+    d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc_h, DEV)
+    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size, flags=batch.F_TX | batch.F_WRITE)
+    np.testing.assert_array_equal(u16(l4), want_l4)
+    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size)
+    assert (v.cpu().numpy() == 1).all()
+    assert (u16(l4) == 0).all()
+    ol, ov = O.batch_ipv6(d_buf.cpu().numpy(), desc_h)
+    assert (ov == 1).all()

@@ -53,6 +53,22 @@ def main():
         def launch(i):
             batch.checksum_batch(bufs[i % rot], d_desc, n, out=outs[i % rot])
         algo = n * ln + 18 * n
+    elif a.config == "c2v6":
+        n = 262144
+        lens = (synth.imix_lengths(n, 3) + 20).astype(np.uint32)
+        rot = 3
+        sets = []
+        for r in range(rot):
+            buf, net, avail, seeds = synth.ipv6_batch(lens, seed=10 + r, proto=6, eth=True)
+            d_buf = torch.from_numpy(buf).to(dev)
+            d_desc = batch.desc_to_device(batch.make_desc(net, avail, seeds), dev)
+            batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+            sets.append((d_buf, d_desc))
+
+        def launch(i):
+            b, d = sets[i % rot]
+            batch.ipv6_checksum_batch(b, d, n)
+        algo = int(lens.sum()) + 19 * n
     elif a.config in ("c2raw", "c2"):
         n = 262144
         lens = synth.imix_lengths(n, 3)
