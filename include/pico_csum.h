@@ -182,7 +182,8 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
  * only, cpl*unroll <= 8); fpw = frames per wave (multiple of 64/group, <= 64);
  * nt = 0 auto / 1 plain / 2 non-temporal loads (RAW batches); pipeline = 0 auto /
  * 1 off / 2 on (uniform batches whose frames fit one pass: double-buffered frame
- * sets).  group = 1 selects the flat work-list kernel (descriptor batches).
+ * sets).  group = 1 selects the flat work-list kernel, group = 2 the sorted-rounds
+ * kernel (descriptor batches only; unroll must be 0 for group 2).
  * Process-wide. */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);

@@ -132,9 +132,13 @@ def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     return out_l4, verdict
 
 
-def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int = 1, nt: int = 0,
+def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
-    """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic."""
+    """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic,
+    1 = flat work-list kernel, 2 = sorted-rounds kernel (unroll defaults to 0 there,
+    to 1 elsewhere)."""
+    if unroll is None:
+        unroll = 0 if group == 2 else 1
     if group == 0:
         unroll = fpw = cpl = nt = pipeline = 0
     _lib.check("pico_csum_set_launch_override",

@@ -35,6 +35,9 @@ int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint3
                           int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
                           uint32_t max_blocks, void *stream);
+int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
+                            uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
+                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -130,15 +133,20 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
     }
     if (pipeline > 2)
         return fail(PICO_CSUM_EINVAL, "pipeline must be 0 (auto), 1 (off) or 2 (on)");
-    if (!(group == 1 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
-        return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 4, 8, 16, 32 or 64");
+    if (!(group == 1 || group == 2 || group == 3 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
+        return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 2 (sorted rounds), 3 (per-wave adaptive), "
+                                        "4, 8, 16, 32 or 64");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
     if (group == 1 && unroll > 8)
         return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
-    if (group > 1 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
+    if (group == 2 && (unroll != 0 || !(cpl == 4 || cpl == 8)))
+        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: unroll must be 0 and cpl 4 or 8");
+    if (group == 3 && (unroll != 0 || cpl != 8 || fpw != 16))
+        return fail(PICO_CSUM_EINVAL, "per-wave adaptive kernel: unroll 0, cpl 8, fpw 16");
+    if (group > 3 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
         return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
-    if (fpw == 0 || fpw > 64 || (group > 1 && fpw % (64 / group) != 0))
+    if (fpw == 0 || fpw > 64 || (group > 3 && fpw % (64 / group) != 0))
         return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
     if (nt > 3)
         return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off), 2 (on) or 3 (on except frame edges)");
@@ -187,13 +195,17 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
         s.fpw = f < 2 * ng ? 2 * ng : f > 64 ? 64 : f;
     }
     if (!uniform) {
-        /* descriptor batches: flat work-list kernel (mixed lengths stream as one
-         * chunk list); 4 slots per pass, ~8K waves */
-        uint32_t f = n / 16384u;
-        s.G = 1;
-        s.CPL = 2;
-        s.U = 0;          /* flat kernel: 0 = one batch per wave (measured faster than persistent) */
-        s.fpw = f < 1 ? 1 : f > 64 ? 64 : f;
+        /* descriptor batches: sorted-rounds kernel (each wave sorts its frames by
+         * length and runs lane-group rounds sized per round).  8 chunks per lane
+         * (<= 128 VGPRs, 4 waves per SIMD); ~4K waves, so a 256K-frame batch is
+         * one residency round of 64-frame waves; non-temporal loads in the wide
+         * (>= 16-lane) rounds only.  Measured on MI355X: DESIGN.md "Launch shapes". */
+        uint32_t f = n / 4096u;
+        s.G = 2;
+        s.CPL = 8;
+        s.U = 0;
+        s.nt = 1;
+        s.fpw = f < 16 ? 16 : f > 64 ? 64 : f;
     }
     if (g_ovr_group) {
         s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
@@ -259,9 +271,13 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (!g_ovr_group)   /* default: lane groups sized per wave from its frames' lengths */
+    if (s.G == 3)       /* lane groups sized per wave from its frames' mean length */
         return launch_status(pico_csum_launch_desc_adaptive(d_base, base_len, d_desc, n, crc_off, flags, d_out,
                                                             d_bad, 0, stream),
+                             "pico_checksum_batch_dev");
+    if (s.G == 2)
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
+                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
@@ -288,8 +304,8 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, len, 1);
-    if (s.G == 1)
-        return fail(PICO_CSUM_EINVAL, "the flat kernel (group 1) serves descriptor batches only");
+    if (s.G <= 3)
+        return fail(PICO_CSUM_EINVAL, "groups 1-3 (flat, sorted, adaptive) serve descriptor batches only");
     if (s.pipe && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u)
         return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,
                                                          s.nt, s.fpw, stream),
@@ -318,6 +334,13 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (s.G == 3)
+        return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
+    if (s.G == 2)
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
+                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
+                                                     stream),
+                             "pico_ipv4_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
                                                    d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
@@ -347,7 +370,13 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (s.G != 1) {           /* the IPv6 mode exists in the flat kernel only */
+    if (s.G == 3)
+        return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
+    if (s.G == 2)
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
+                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, stream),
+                             "pico_ipv6_checksum_batch_dev");
+    if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
         s.G = 1;
         s.CPL = 2;
         s.U = 0;

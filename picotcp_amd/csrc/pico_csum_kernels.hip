@@ -1056,6 +1056,370 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
     }
 }
 
+// ---------------------------------------------------------------- sorted-rounds kernel
+//
+// Descriptor batches of any size mix, all modes (RAW / fused IPv4 / fused IPv6).
+// The lane-group body is the cheapest per chunk (an unmasked v_dot2 chain, edge
+// corrections only at frame edges) but a fixed group width G fits no size mix:
+// a wave waits for its largest frame.  Here a wave
+//   1. parses its (up to 64) frames, lane j = frame j (as the flat kernel);
+//   2. sorts them by chunk count with a 64-lane bitonic network (21 xor shuffles);
+//   3. walks the sorted list in rounds: each round takes the next 64/G frames with G
+//      the smallest width whose 8 chunks per lane cover the round's largest frame
+//      (sorted, so the last one), so every round holds frames of similar size and
+//      keeps its lanes busy; per-frame sums go to LDS;
+//   4. lane j finalizes frame j (one coalesced store per output).
+
+struct SortedWaveLds {
+    uint32_t acc_all[64];
+    uint32_t acc_x[64];
+    uint32_t acc_opt[64];
+    uint32_t nch[64];
+    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4}
+    uint2 xo[64];          // {field position (NONE), option end (0)}
+    uint4 fin[64];         // parse state for phase 4 (kept in LDS, not VGPRs, across the rounds):
+                           // {verdict | parsed << 4 | l4 << 5 | oob << 6 | proto << 8 | tl << 16,
+                           //  hl | ip crc << 16, pseudo sum (RAW: seed), header sum}
+};
+
+// One round: group g sums sorted frame pos + g (frame index = key & 63).
+template <int G, int CPL, bool PERM, bool NT, bool XO>
+__device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L, uint32_t key, uint32_t pos,
+                                             uint32_t m) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane / G, l = lane % G;
+    const uint32_t si = pos + g;
+    const uint32_t k_s = (uint32_t)__shfl((int)key, (int)min(si, 63u));
+    const bool valid = si < m;
+    const uint32_t j = k_s & 63u;
+    const uint32_t nch = valid ? L.nch[j] : 0u;
+    const uint4 fi = L.info[j];
+    const uint2 xo = XO ? L.xo[j] : make_uint2(NONE, 0u);
+    const uint32_t rr = fi.w & 15u;
+    const uint32_t sl = (fi.w & 16u) ? SEL_ODD : SEL_EVEN;
+    const uint32_t send = fi.z;
+    const uint8_t* a0 = p.base + ((((uint64_t)fi.y) << 32) | fi.x);
+    uint32_t acc = 0, accx = 0, acco = 0;
+    for (uint32_t kb = 0; kb < nch; kb += G * CPL) {
+        uint4 v[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = kb + l + G * c;
+            v[c] = k < nch ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = kb + l + G * c;
+            const uint32_t ch = k << 4;
+            if (k < nch && (ch < rr || ch + 16u > send)) acc += masked_chunk_sum<PERM>(v[c], ch, rr, send, sl);
+            else acc = add_full<PERM>(v[c], sl, acc);
+            if constexpr (XO) {
+                if (k < nch && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4)))
+                    accx += masked_chunk_sum<PERM>(v[c], ch, xo.x, xo.x + 2u, sl);
+                if (k < nch && xo.y != 0u && ch < xo.y)
+                    acco += masked_chunk_sum<PERM>(v[c], ch, rr + 20u, xo.y, sl);
+            }
+        }
+    }
+    acc = group_sum<G>(acc);
+    if constexpr (XO) {
+        accx = group_sum<G>(accx);
+        acco = group_sum<G>(acco);
+    }
+    if (valid && l == G - 1) {
+        L.acc_all[j] = acc;
+        if constexpr (XO) { L.acc_x[j] = accx; L.acc_opt[j] = acco; }
+    }
+}
+
+// Round width: the smallest G whose one pass (G lanes x CPL chunks) covers the
+// round's largest frame; 64 lanes per frame beyond that.  NT: non-temporal loads
+// in the rounds of G >= 16 (frames over ~1 KiB; measured: they cost on small ones).
+template <int CPL, bool PERM, bool NT, bool XO>
+__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, uint32_t key, uint32_t m) {
+    uint32_t pos = 0;
+    auto nch_at = [&](uint32_t s) { return (uint32_t)__builtin_amdgcn_readlane((int)key, (int)min(s, m - 1u)) >> 6; };
+    while (pos < m) {
+        if (nch_at(pos + 15u) <= 4u * CPL)        { sorted_round<4, CPL, PERM, false, XO>(p, L, key, pos, m);  pos += 16u; }
+        else if (nch_at(pos + 7u) <= 8u * CPL)    { sorted_round<8, CPL, PERM, false, XO>(p, L, key, pos, m);  pos += 8u; }
+        else if (nch_at(pos + 3u) <= 16u * CPL)   { sorted_round<16, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 4u; }
+        else if (nch_at(pos + 1u) <= 32u * CPL)   { sorted_round<32, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 2u; }
+        else                                      { sorted_round<64, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 1u; }
+    }
+}
+
+// MODE: 0 RAW (p.crc_off / p.flags / p.out / p.bad), 1 fused IPv4, 2 fused IPv6
+// (IPv4/IPv6 outputs in Ipv4Args-compatible fields of FlatArgs).
+// Phase 4: lane `lane` finalizes its frame (output index idx) from the LDS state.
+template <int MODE>
+__device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t idx,
+                                              bool tx) {
+    constexpr bool IPV6 = MODE == 2;
+    asm volatile("" ::: "memory");
+    const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
+    const uint4 info = L.info[lane], fin = L.fin[lane];
+    const uint32_t xpos = L.xo[lane].x;
+    const uint32_t r = info.w & 15u;
+    uint8_t* fp = p.base + (((((uint64_t)info.y) << 32) | info.x) + r);
+    uint32_t verdict = fin.x & 15u;
+    const bool parsed = fin.x & 16u, l4_needed = fin.x & 32u, oob = fin.x & 64u;
+    const uint32_t proto = (fin.x >> 8) & 0xFFu, tl = fin.x >> 16;
+    const uint32_t hl = fin.y & 0xFFFFu, ipcrc = fin.y >> 16;
+    const uint32_t pseudo = fin.z, seed = fin.z, hdr20 = fin.w;
+    if constexpr (MODE == 0) {
+        uint32_t ret = 0;
+        if (oob) {
+            if (p.bad) atomicAdd(p.bad, 1u);
+        } else {
+            ret = finalize(seed + acc_all - acc_x);
+            if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
+        }
+        p.out[idx] = (uint16_t)ret;
+    } else if constexpr (IPV6) {
+        uint32_t l4 = 0;
+        if (parsed) {
+            if (l4_needed) {
+                if (!tx) {
+                    if (proto == 6u || (proto == 17u && acc_x != 0u) || proto == 58u) {
+                        l4 = finalize(pseudo + acc_all);
+                        const uint32_t type = acc_x & 0xFFu;
+                        const bool checked = proto != 58u || (type >= 130u && type <= 137u) || type == 143u;
+                        if (l4 != 0 && checked) verdict |= V_L4_BAD;
+                    }
+                } else {
+                    l4 = finalize(pseudo + acc_all - acc_x);
+                }
+            }
+            if (verdict == 0) verdict = V_ACCEPT;
+        }
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l4_needed) store_crc(fp + (xpos - r), l4);
+        if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
+        if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
+    } else {
+        uint32_t net = 0, l4 = 0;
+        if (parsed) {
+            const uint32_t acc_hdr = hdr20 + acc_opt;
+            net = finalize(acc_hdr - (tx ? ipcrc : 0u));
+            if (!tx && net != 0) verdict |= V_NET_BAD;
+            const uint32_t tsum = acc_all - acc_hdr;
+            if (l4_needed) {
+                if (!tx) {
+                    if (proto == 6u || acc_x != 0u) {
+                        l4 = finalize(pseudo + tsum);
+                        if (l4 != 0) verdict |= V_L4_BAD;
+                    }
+                } else if (proto == 6u) {
+                    l4 = finalize(pseudo + tsum - acc_x);
+                } else {
+                    l4 = finalize(tsum - acc_x);
+                }
+            }
+            if (verdict == 0) verdict = V_ACCEPT;
+        }
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
+            store_crc(fp + 10, net);
+            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
+            else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+        }
+        if (p.out_net) p.out_net[idx] = (uint16_t)net;
+        if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
+        if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
+    }
+}
+
+// CPL 8 keeps 8 KiB of loads in flight per wave within 128 VGPRs (4 waves per
+// SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
+// fits 64 VGPRs (8 waves per SIMD).
+template <int MODE, bool NT, int CPL>
+__global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+    constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2;
+    __shared__ SortedWaveLds lds_all[4];
+    const uint32_t lane = threadIdx.x & 63u;
+    SortedWaveLds& L = lds_all[threadIdx.x >> 6];
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t f0 = wave * p.fpw;
+    if (f0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const bool tx = MODE != 0 && (p.flags & 2u) != 0;
+
+    // ---- 1. lane j = frame j
+    uint4 dcur = make_uint4(0, 0, 0, 0);
+    if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+    uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
+    uint32_t len = lane < cnt ? dcur.z : 0u;
+    const uint32_t seed = dcur.w;
+    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
+    if (oob || lane >= cnt) { len = 0; off = 0; }
+    uint8_t* fp = p.base + off;
+    uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+    uint64_t a0off = off - r;
+    uint32_t odd = r & 1u;
+
+    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
+    uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
+    bool parsed = false, l4_needed = false;
+    if constexpr (MODE == 0) {
+        span = ext = len;
+        if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
+    } else {
+        constexpr uint32_t HDR = IPV6 ? 40u : 20u;
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
+        if (len >= HDR) {
+            const uint8_t* a0 = p.base + a0off;
+            c0 = load_chunk(a0, 0);
+            if (r + HDR > 16) c1 = load_chunk(a0, 1);
+            if (r + HDR > 32) c2 = load_chunk(a0, 2);
+            if (IPV6 && r + HDR > 48) c3 = load_chunk(a0, 3);
+        }
+        const uint32_t avail = len;
+        if constexpr (IPV4) {
+            if (avail >= 20) {
+                const uint32_t D[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+                const uint32_t q = r >> 2, sh = r & 3u;
+                uint32_t E[6];
+#pragma unroll
+                for (int m = 0; m < 6; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+                uint32_t H[5];
+#pragma unroll
+                for (int m = 0; m < 5; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+                const uint32_t ihl = H[0] & 0x0Fu;
+                hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+                proto = (H[2] >> 8) & 0xFFu;
+                ipcrc = H[2] >> 16;
+                tl = (tot - hl) & 0xFFFFu;                              // uint16 wrap, pico_ipv4.c:395
+                const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;   // pico_ipv4.c:386
+                if (!(hl > avail || (!tx && tl > max_allowed) || hl + tl > avail)) {
+                    parsed = true;
+                    verdict = 0;
+                    span = ext = hl + tl;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
+                    pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
+                             (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
+                    if (hl > 20u) optend = r + hl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (hl + 8u > avail) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
+                        }
+                    } else {
+                        if (proto == 6u) {
+                            if (tl < 20u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 16u; }
+                        } else if (proto == 1u) {
+                            if (tl < 8u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 2u; }
+                        }
+                    }
+                }
+            }
+        } else {
+            if (avail >= 40) {
+                const uint32_t D[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+                const uint32_t q = r >> 2, sh = r & 3u;
+                uint32_t E[11];
+#pragma unroll
+                for (int m = 0; m < 11; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+                uint32_t H[10];
+#pragma unroll
+                for (int m = 0; m < 10; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+                uint32_t net_len = seed & 0xFFFFu;
+                proto = (seed >> 16) & 0xFFu;
+                if (seed == 0) { net_len = 40u; proto = (H[1] >> 16) & 0xFFu; }
+                tl = (plen - (net_len - 40u)) & 0xFFFFu;                // pico_ipv6.c:790
+                if (net_len >= 40u && net_len <= avail && net_len + tl <= avail) {
+                    uint32_t addr = 0, xrel = NONE;
+#pragma unroll
+                    for (int m = 2; m < 10; ++m) addr = dot2_add(H[m], addr);
+                    pseudo = addr + (((tl & 0xFFu) << 8) | (tl >> 8)) + (proto << 8);
+                    parsed = true;
+                    verdict = 0;
+                    ext = tl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (net_len + 8u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 6u; ext = max(tl, 8u); }
+                        } else if (proto == 58u) {
+                            if (net_len + 1u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 0u; ext = max(tl, 1u); }
+                        }
+                    } else {
+                        const uint32_t need = proto == 6u ? 20u : proto == 17u ? 8u : 4u;
+                        if (proto == 6u || proto == 17u || proto == 58u) {
+                            if (tl < need) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = proto == 6u ? 16u : proto == 17u ? 6u : 2u; }
+                        }
+                    }
+                    if (parsed) {
+                        off += net_len;
+                        fp = p.base + off;
+                        r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+                        a0off = off - r;
+                        odd = r & 1u;
+                        span = tl;
+                        if (xrel != NONE) xpos = r + xrel;
+                    } else {
+                        ext = 0;
+                    }
+                }
+            }
+        }
+    }
+    const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
+    const uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
+    L.acc_all[lane] = 0;
+    L.acc_x[lane] = 0;
+    L.acc_opt[lane] = 0;
+    L.nch[lane] = nch;
+    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4));
+    L.xo[lane] = make_uint2(xpos, optend);
+    L.fin[lane] = make_uint4(verdict | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) | (proto << 8) |
+                                 (tl << 16),
+                             hl | (ipcrc << 16), MODE == 0 ? seed : pseudo, hdr20);
+    const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
+    const bool any_xo = __builtin_amdgcn_ballot_w64(nch != 0 && (xpos != NONE || optend != 0)) != 0;
+
+    // ---- 2. bitonic sort of (chunk count, frame) keys; empty frames sort last
+    const uint32_t active = nch != 0;
+    uint32_t key = active ? (min(nch, (1u << 26) - 1u) << 6) | lane : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)jj);
+            const bool asc = (lane & k) == 0, lower = (lane & jj) == 0;
+            key = (lower == asc) ? min(key, other) : max(key, other);
+        }
+    }
+    const uint32_t m = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(active));
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- 3. rounds over the sorted frames
+    RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
+    if (m) {
+        if (any_odd) {
+            if (any_xo) sorted_rounds<CPL, true, NT, true>(ra, L, key, m);
+            else sorted_rounds<CPL, true, NT, false>(ra, L, key, m);
+        } else {
+            if (any_xo) sorted_rounds<CPL, false, NT, true>(ra, L, key, m);
+            else sorted_rounds<CPL, false, NT, false>(ra, L, key, m);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+
+    // ---- 4. lane j finalizes frame j (state reloaded from LDS)
+    if (lane >= cnt) return;
+    sorted_finish<MODE>(p, L, lane, f0 + lane, tx);
+}
+
 // ---------------------------------------------------------------- dispatch
 
 // (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
@@ -1089,6 +1453,28 @@ extern "C" {
 
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
+
+// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6.
+int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
+                            uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
+                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void* stream) {
+    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
+               crc_off, flags, out, bad, out_net, out_l4, verdict};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    using K = void (*)(FlatArgs);
+    static const K table[3][2][2] = {
+        {{csum_sorted_kernel<0, false, 4>, csum_sorted_kernel<0, false, 8>},
+         {csum_sorted_kernel<0, true, 4>, csum_sorted_kernel<0, true, 8>}},
+        {{csum_sorted_kernel<1, false, 4>, csum_sorted_kernel<1, false, 8>},
+         {csum_sorted_kernel<1, true, 4>, csum_sorted_kernel<1, true, 8>}},
+        {{csum_sorted_kernel<2, false, 4>, csum_sorted_kernel<2, false, 8>},
+         {csum_sorted_kernel<2, true, 4>, csum_sorted_kernel<2, true, 8>}}};
+    hipLaunchKernelGGL(table[mode][nt ? 1 : 0][cpl == 8 ? 1 : 0], grid, block, 0, s, a);
+    return (int)hipGetLastError();
+}
 
 // Per-wave adaptive descriptor kernel (16 frames per wave).
 int pico_csum_launch_desc_adaptive(void* base, uint64_t base_len, const void* desc, uint32_t n, int32_t crc_off,

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Parity first, then interleaved launch-shape sweeps on the descriptor configs.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -6,6 +7,10 @@ mkdir -p $O
 cd $R
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1
 echo "pytest ok"
-timeout -k 10 300 python tools/sweep.py --config c2v6 --rounds 3 --shapes 0,0,0,0,0 1,2,0,16,1 1,4,0,16,1 1,2,0,32,1 > $O/sweep_c2v6.jsonl 2>&1
-timeout -k 10 300 python bench.py --config c2v6 --steps 100 --warmup 10 > $O/bench_c2v6.json 2> $O/bench_c2v6.err
-echo ok
+COMMON="0,0,0,0,0 2,8,0,64,1 2,8,0,64,2 2,4,0,64,1 2,4,0,64,2 2,8,0,48,2"
+for cfg in c2raw u354d c1d c2 c2v6; do
+  EXTRA=""
+  case $cfg in c2|c2v6) ;; *) EXTRA="3,8,0,16,1";; esac
+  timeout -k 10 300 python tools/sweep.py --config $cfg --rounds 3 --shapes $COMMON $EXTRA > $O/sweep_$cfg.jsonl 2>&1
+  echo "sweep $cfg ok"
+done

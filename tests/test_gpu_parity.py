@@ -14,12 +14,23 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
-# descriptor batches also run on the flat work-list kernel (group 1)
-DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)]
+# descriptor batches also run on the flat work-list kernel (group 1) and the
+# sorted-rounds kernel (group 2)
+DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)] + [(2, 4), (2, 8)]
+# override per descriptor kernel for the kernel-parametrized tests
+KERNELS = {"auto": None, "adaptive": (3, 8, 16, 0, 1), "flat": (1, 4, 8, 1, 1), "sorted": (2, 8, 64, 0, 2), "sorted_fpw7": (2, 8, 7, 0, 1),
+           "sorted_c4": (2, 4, 13, 0, 1)}
 
 
 def fpws(g):
-    return (1, 13, 64) if g == 1 else sorted({64 // g, 64})
+    return (1, 13, 64) if g <= 2 else sorted({64 // g, 64})
+
+
+def use_kernel(name):
+    if KERNELS[name] is None:
+        batch.set_launch_override(0)
+    else:
+        batch.set_launch_override(*KERNELS[name])
 
 
 def u16(t: torch.Tensor) -> np.ndarray:
@@ -110,8 +121,8 @@ def test_desc_every_shape(g, c):
         np.testing.assert_array_equal(got, case["expected"], err_msg=f"g={g} c={c} fpw={fpw}")
 
 
-@pytest.mark.parametrize("flat", [False, True])
-def test_desc_big_regions(flat):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_desc_big_regions(kernel):
     """Regions over 64K chunks (> 1 MiB) take the flat kernel's whole-wave path; mixed with
     small ones, odd offsets, seeds and a crc field."""
     rng = np.random.default_rng(44)
@@ -119,8 +130,7 @@ def test_desc_big_regions(flat):
     offs = [1, 3 << 20, 5, (7 << 20) + 3, 100, 2000, 11 << 20]
     lens = [2 << 20, (3 << 20) + 1, 64, (1 << 20) + 17, 1500, 0, 123457]
     desc = batch.make_desc(offs, lens, rng.integers(0, 1 << 32, len(offs), dtype=np.uint64).astype(np.uint32))
-    if flat:
-        batch.set_launch_override(1, 4, 8, 1, 1)
+    use_kernel(kernel)
     for crc in (-1, 10):
         want = O.batch_raw(buf, desc, crc_off=crc)
         got = u16(batch.checksum_batch(to_dev(buf), batch.desc_to_device(desc, DEV), len(offs), crc_off=crc))
@@ -172,8 +182,8 @@ def test_desc_crc_field_and_write_roundtrip():
     np.testing.assert_array_equal(after[mask], buf[mask])
 
 
-@pytest.mark.parametrize("flat", [False, True])
-def test_desc_crc_write_both_kernels(flat):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_desc_crc_write_every_kernel(kernel):
     rng = np.random.default_rng(21)
     n = 2000
     lens = rng.integers(0, 3000, n)
@@ -183,8 +193,7 @@ def test_desc_crc_write_both_kernels(flat):
     buf = synth.random_bytes(17, int(offs[-1]) + int(lens[-1]) + 5)
     desc = batch.make_desc(offs, lens, rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32))
     want = O.batch_raw(buf, desc, crc_off=16)
-    if flat:
-        batch.set_launch_override(1, 4, 64, 1, 1)
+    use_kernel(kernel)
     d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
     got = u16(batch.checksum_batch(d_buf, d_desc, n, crc_off=16, flags=batch.F_WRITE))
     np.testing.assert_array_equal(got, want)
@@ -193,10 +202,9 @@ def test_desc_crc_write_both_kernels(flat):
     assert (verify[has] == 0).all()
 
 
-@pytest.mark.parametrize("flat", [False, True])
-def test_desc_out_of_bounds_both_kernels(flat):
-    if flat:
-        batch.set_launch_override(1, 2, 64, 1, 1)
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_desc_out_of_bounds_every_kernel(kernel):
+    use_kernel(kernel)
     test_desc_out_of_bounds_regions_are_not_read()
 
 
@@ -328,13 +336,13 @@ def test_host_batch_roundtrip():
 
 # ------------------------------------------------------------------ IPv6 fused
 
-@pytest.mark.parametrize("c", [1, 2, 4, 8])
-def test_ipv6_golden_rx_tx(c):
+@pytest.mark.parametrize("g,c", [(1, 1), (1, 2), (1, 4), (1, 8), (2, 4), (2, 8)])
+def test_ipv6_golden_rx_tx(g, c):
     cs = G.ipv6_cases()
     desc = batch.desc_to_device(G.ipv6_desc(cs), DEV)
     n = cs["net"].size
     for fpw in (1, 13, 64):
-        batch.set_launch_override(1, c, fpw, 0, 1)
+        batch.set_launch_override(g, c, fpw, 0, 1)
         l4, v = batch.ipv6_checksum_batch(to_dev(cs["buf"]), desc, n)
         np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"c={c} fpw={fpw}")
         np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"c={c} fpw={fpw}")
