@@ -1107,6 +1107,8 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
             const uint32_t k = kb + l + G * c;
             v[c] = k < nch ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
         }
+        // interior chunks unmasked; masked sums only where a chunk holds a region edge
+        // (a wave-uniform branch: skipped for slots no lane's edge falls in)
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const uint32_t k = kb + l + G * c;

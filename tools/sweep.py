@@ -42,9 +42,10 @@ def main():
         def launch(i):
             batch.checksum_uniform(bufs[i % rot], stride, ln, n, out=outs[i % rot])
         algo = n * ln + 2 * n
-    elif a.config in ("u354d", "c1d"):
-        # uniform frames fed as a descriptor batch (ablation: descriptor kernels vs uniform ones)
-        n, ln = {"u354d": (262144, 354), "c1d": (262144, 1500)}[a.config]
+    elif a.config == "c1d" or (a.config.startswith("u") and a.config.endswith("d")):
+        # uniform frames fed as a descriptor batch (ablation: descriptor kernels vs uniform
+        # ones): c1d = 256K x 1500 B, u<LEN>d = 256K x LEN bytes
+        n, ln = 262144, 1500 if a.config == "c1d" else int(a.config[1:-1])
         rot = 3
         bufs = [torch.randint(0, 256, (n * ln,), dtype=torch.uint8, device=dev) for _ in range(rot)]
         d_desc = batch.desc_to_device(batch.make_desc(np.arange(n, dtype=np.uint64) * ln, np.full(n, ln)), dev)
