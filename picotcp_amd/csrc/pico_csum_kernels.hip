@@ -1063,10 +1063,12 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
 // corrections only at frame edges) but a fixed group width G fits no size mix:
 // a wave waits for its largest frame.  Here a wave
 //   1. parses its (up to 64) frames, lane j = frame j (as the flat kernel);
-//   2. sorts them by chunk count with a 64-lane bitonic network (21 xor shuffles);
-//   3. walks the sorted list in rounds: each round takes the next 64/G frames with G
-//      the smallest width whose 8 chunks per lane cover the round's largest frame
-//      (sorted, so the last one), so every round holds frames of similar size and
+//   2. orders them by size class -- the narrowest width G in {4..64} whose one pass
+//      (G lanes x CPL chunks) covers the frame -- with 5 ballots and mbcnt (a
+//      64-lane bitonic sort by length measured the same round times at ~1K more
+//      cycles of shuffle latency per batch);
+//   3. walks that order in rounds: each round takes the next 64/G frames with G the
+//      class of the last of them, so every round holds frames of similar size and
 //      keeps its lanes busy; per-frame sums go to LDS;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
@@ -1077,21 +1079,20 @@ struct SortedWaveLds {
     uint32_t nch[64];
     uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4}
     uint2 xo[64];          // {field position (NONE), option end (0)}
+    uint32_t order[64];    // frames by size class: order[position] = frame (lane)
     uint4 fin[64];         // parse state for phase 4 (kept in LDS, not VGPRs, across the rounds):
                            // {verdict | parsed << 4 | l4 << 5 | oob << 6 | proto << 8 | tl << 16,
                            //  hl | ip crc << 16, pseudo sum (RAW: seed), header sum}
 };
 
-// One round: group g sums sorted frame pos + g (frame index = key & 63).
+// One round: group g sums the frame at position pos + g of the class order.
 template <int G, int CPL, bool PERM, bool NT, bool XO>
-__device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L, uint32_t key, uint32_t pos,
-                                             uint32_t m) {
+__device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L, uint32_t pos, uint32_t m) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t g = lane / G, l = lane % G;
     const uint32_t si = pos + g;
-    const uint32_t k_s = (uint32_t)__shfl((int)key, (int)min(si, 63u));
     const bool valid = si < m;
-    const uint32_t j = k_s & 63u;
+    const uint32_t j = L.order[min(si, 63u)] & 63u;
     const uint32_t nch = valid ? L.nch[j] : 0u;
     const uint4 fi = L.info[j];
     const uint2 xo = XO ? L.xo[j] : make_uint2(NONE, 0u);
@@ -1138,15 +1139,16 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
 // round's largest frame; 64 lanes per frame beyond that.  NT: non-temporal loads
 // in the rounds of G >= 16 (frames over ~1 KiB; measured: they cost on small ones).
 template <int CPL, bool PERM, bool NT, bool XO>
-__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, uint32_t key, uint32_t m) {
+__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, const uint32_t (&e)[4], uint32_t m) {
+    // position s holds a frame of class <= c iff s < e[c-1]; a round of width G may
+    // take the next 64/G positions when the last of them is of class <= G's class
     uint32_t pos = 0;
-    auto nch_at = [&](uint32_t s) { return (uint32_t)__builtin_amdgcn_readlane((int)key, (int)min(s, m - 1u)) >> 6; };
     while (pos < m) {
-        if (nch_at(pos + 15u) <= 4u * CPL)        { sorted_round<4, CPL, PERM, false, XO>(p, L, key, pos, m);  pos += 16u; }
-        else if (nch_at(pos + 7u) <= 8u * CPL)    { sorted_round<8, CPL, PERM, false, XO>(p, L, key, pos, m);  pos += 8u; }
-        else if (nch_at(pos + 3u) <= 16u * CPL)   { sorted_round<16, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 4u; }
-        else if (nch_at(pos + 1u) <= 32u * CPL)   { sorted_round<32, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 2u; }
-        else                                      { sorted_round<64, CPL, PERM, NT, XO>(p, L, key, pos, m); pos += 1u; }
+        if (min(pos + 15u, m - 1u) < e[0])        { sorted_round<4, CPL, PERM, false, XO>(p, L, pos, m);  pos += 16u; }
+        else if (min(pos + 7u, m - 1u) < e[1])    { sorted_round<8, CPL, PERM, false, XO>(p, L, pos, m);  pos += 8u; }
+        else if (min(pos + 3u, m - 1u) < e[2])    { sorted_round<16, CPL, PERM, NT, XO>(p, L, pos, m); pos += 4u; }
+        else if (min(pos + 1u, m - 1u) < e[3])    { sorted_round<32, CPL, PERM, NT, XO>(p, L, pos, m); pos += 2u; }
+        else                                      { sorted_round<64, CPL, PERM, NT, XO>(p, L, pos, m); pos += 1u; }
     }
 }
 
@@ -1233,14 +1235,8 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
 template <int MODE, bool NT, int CPL>
-__global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2;
-    __shared__ SortedWaveLds lds_all[4];
-    const uint32_t lane = threadIdx.x & 63u;
-    SortedWaveLds& L = lds_all[threadIdx.x >> 6];
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t f0 = wave * p.fpw;
-    if (f0 >= p.n) return;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = MODE != 0 && (p.flags & 2u) != 0;
 
@@ -1388,38 +1384,57 @@ __global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(Flat
     const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
     const bool any_xo = __builtin_amdgcn_ballot_w64(nch != 0 && (xpos != NONE || optend != 0)) != 0;
 
-    // ---- 2. bitonic sort of (chunk count, frame) keys; empty frames sort last
-    const uint32_t active = nch != 0;
-    uint32_t key = active ? (min(nch, (1u << 26) - 1u) << 6) | lane : 0xFFFFFFFFu;
+    // ---- 2. order the frames by size class (the narrowest round width that covers
+    //         them in one pass): ballots and bit counts, no data movement but one
+    //         LDS store per frame
+    const uint32_t cls = nch == 0 ? 5u : nch <= 4u * CPL ? 0u : nch <= 8u * CPL ? 1u : nch <= 16u * CPL ? 2u
+                                                                  : nch <= 32u * CPL ? 3u : 4u;
+    uint64_t bal[5];
 #pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1) {
+    for (int c = 0; c < 5; ++c) bal[c] = __builtin_amdgcn_ballot_w64(cls == (uint32_t)c);
+    uint32_t e[4];
+    e[0] = (uint32_t)__builtin_popcountll(bal[0]);
 #pragma unroll
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)jj);
-            const bool asc = (lane & k) == 0, lower = (lane & jj) == 0;
-            key = (lower == asc) ? min(key, other) : max(key, other);
-        }
+    for (int c = 1; c < 4; ++c) e[c] = e[c - 1] + (uint32_t)__builtin_popcountll(bal[c]);
+    const uint32_t m = e[3] + (uint32_t)__builtin_popcountll(bal[4]);
+    if (cls < 5u) {
+        const uint64_t mine = cls == 0 ? bal[0] : cls == 1 ? bal[1] : cls == 2 ? bal[2] : cls == 3 ? bal[3] : bal[4];
+        const uint32_t start = cls == 0 ? 0u : e[cls - 1];
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        L.order[start + rank] = lane;
     }
-    const uint32_t m = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(active));
     __builtin_amdgcn_wave_barrier();
 
     // ---- 3. rounds over the sorted frames
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
     if (m) {
         if (any_odd) {
-            if (any_xo) sorted_rounds<CPL, true, NT, true>(ra, L, key, m);
-            else sorted_rounds<CPL, true, NT, false>(ra, L, key, m);
+            if (any_xo) sorted_rounds<CPL, true, NT, true>(ra, L, e, m);
+            else sorted_rounds<CPL, true, NT, false>(ra, L, e, m);
         } else {
-            if (any_xo) sorted_rounds<CPL, false, NT, true>(ra, L, key, m);
-            else sorted_rounds<CPL, false, NT, false>(ra, L, key, m);
+            if (any_xo) sorted_rounds<CPL, false, NT, true>(ra, L, e, m);
+            else sorted_rounds<CPL, false, NT, false>(ra, L, e, m);
         }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
 
     // ---- 4. lane j finalizes frame j (state reloaded from LDS)
-    if (lane >= cnt) return;
-    sorted_finish<MODE>(p, L, lane, f0 + lane, tx);
+    if (lane < cnt) sorted_finish<MODE>(p, L, lane, f0 + lane, tx);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave per 64-frame batch; with a capped grid (persistent) waves loop over
+// batches and drift out of step, so one wave's descriptor/header latency overlaps
+// other waves' rounds.
+template <int MODE, bool NT, int CPL>
+__global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+    __shared__ SortedWaveLds lds_all[4];
+    const uint32_t lane = threadIdx.x & 63u;
+    SortedWaveLds& L = lds_all[threadIdx.x >> 6];
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w * p.fpw < p.n; w += waves)
+        sorted_batch<MODE, NT, CPL>(p, L, lane, w * p.fpw);
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -1459,12 +1474,16 @@ extern "C" {
 // Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6.
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void* stream) {
+                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t max_blocks,
+                            void* stream) {
     if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict};
-    const dim3 grid = grid_for(n, fpw), block(256);
+    dim3 grid = grid_for(n, fpw);
+    const dim3 block(256);
+    if (max_blocks == 0) return (int)hipErrorInvalidValue;
+    if (grid.x > max_blocks) grid.x = max_blocks;
     hipStream_t s = static_cast<hipStream_t>(stream);
     using K = void (*)(FlatArgs);
     static const K table[3][2][2] = {

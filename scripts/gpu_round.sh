@@ -18,9 +18,11 @@ done
 echo "bench configs ok"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c1_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu --no-e2e > $O/prof_c1_$TAG.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2_$TAG -o run --output-format csv -- python3 $R/bench.py --config c2 --steps 100 --warmup 10 --no-cpu --no-e2e > $O/prof_c2_$TAG.log 2>&1
+for cfg in c2 c2v6; do
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${cfg}_$TAG -o run --output-format csv -- python3 $R/bench.py --config $cfg --steps 100 --warmup 10 --no-cpu --no-e2e > $O/prof_${cfg}_$TAG.log 2>&1
+done
 echo "trace ok"
-for cfg in c1 c2; do
+for cfg in c1 c2 c2v6; do
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_${cfg}_$TAG -o run --output-format csv -- python3 $R/bench.py --config $cfg --steps 20 --warmup 2 --no-cpu --no-e2e > $O/pmc_fetch_${cfg}_$TAG.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_${cfg}_$TAG -o run --output-format csv -- python3 $R/bench.py --config $cfg --steps 20 --warmup 2 --no-cpu --no-e2e > $O/pmc_write_${cfg}_$TAG.log 2>&1
 done

@@ -19,7 +19,7 @@ SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
 DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)] + [(2, 4), (2, 8)]
 # override per descriptor kernel for the kernel-parametrized tests
 KERNELS = {"auto": None, "adaptive": (3, 8, 16, 0, 1), "flat": (1, 4, 8, 1, 1), "sorted": (2, 8, 64, 0, 2), "sorted_fpw7": (2, 8, 7, 0, 1),
-           "sorted_c4": (2, 4, 13, 0, 1)}
+           "sorted_c4": (2, 4, 13, 0, 1), "sorted_persistent": (2, 8, 5, 2, 2)}
 
 
 def fpws(g):

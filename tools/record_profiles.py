@@ -15,17 +15,17 @@ tag, rnd = sys.argv[1], sys.argv[2]
 src = "gpurun_out"
 dst = os.path.join("profiles", rnd)
 os.makedirs(dst, exist_ok=True)
-for cfg in ("c1", "c2"):
+for cfg in ("c1", "c2", "c2v6"):
     d = os.path.join(src, f"prof_{cfg}_{tag}")
     if os.path.isdir(d):
         shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{cfg}_kernel_stats.csv"))
-for cfg in ("c1", "c2", "c3", "c3_64k"):
+for cfg in ("c1", "c2", "c2v6", "c3", "c3_64k"):
     f = os.path.join(src, f"bench_{cfg}_{tag}.json")
     if os.path.exists(f):
         shutil.copy(f, os.path.join(dst, f"bench_{cfg}.json"))
 path = os.path.join("profiles", "pmc_traffic.json")
 rec = json.load(open(path)) if os.path.exists(path) else {}
-for cfg in ("c1", "c2"):
+for cfg in ("c1", "c2", "c2v6"):
     r = {}
     for kind, c in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         f = os.path.join(src, f"pmc_{kind}_{cfg}_{tag}", "run_counter_collection.csv")
