@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c3_64k|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c3|c3_64k|c3_frag|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
   c1 (default, the metric's config): 256K x 1500 B frames, raw pico_checksum per frame
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
+  c2tx: the same datagrams, fused TX (checksums computed and written in place)
+  c2v6: 256K IMIX+20 B IPv6/TCP datagrams, fused IPv6 pseudo-header RX verify
+  c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
   c3: 256K x 9000 B jumbo frames;  c3_64k: 16K x 64 KiB reassembled buffers
   c4: 4M x 1500 B frames sharded over the ranks (strong scaling)
 c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame batches
@@ -51,6 +54,12 @@ CONFIGS = {
     "c2v6": dict(kind="ipv6", frames=262144,
                  workload="C2 (IPv6, SURVEY 8f row 3): 256K simple-IMIX {64,576,1500}+20 B IPv6/TCP datagrams "
                           "(14 B Ethernet header in front), fused IPv6 pseudo-header TCP RX verify"),
+    "c2tx": dict(kind="ipv4", frames=262144, tx=True,
+                 workload="C2 compute mode: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams, fused TX: IPv4 "
+                          "header and TCP checksums computed with the crc fields read as zero and written in place"),
+    "c3_frag": dict(kind="ipv4", frames=16384, frame_bytes=64512,
+                    workload="C3 reassembled: 16K x 64512 B (PICO_IPV4_FRAG_MAX_SIZE) IPv4/TCP datagrams, fused "
+                             "IPv4 header + TCP pseudo-header RX verify"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -81,8 +90,8 @@ def make_uniform(n, ln, device, seed):
     return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=device, generator=g)
 
 
-def make_c2(n, device, seed):
-    lens = synth.imix_lengths(n, seed)
+def make_c2(n, device, seed, frame_bytes=0):
+    lens = synth.imix_lengths(n, seed) if not frame_bytes else np.full(n, frame_bytes, dtype=np.uint32)
     buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
     desc = batch.make_desc(net, avail)
     d_buf = torch.from_numpy(buf).to(device)
@@ -90,7 +99,7 @@ def make_c2(n, device, seed):
     # make every datagram valid with the TX kernel (untimed setup), so RX verify accepts
     batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum())
+    return d_buf, d_desc, int(lens.sum()), (buf, desc)
 
 
 def make_c2v6(n, device, seed):
@@ -101,7 +110,7 @@ def make_c2v6(n, device, seed):
     d_desc = batch.desc_to_device(desc, device)
     batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum())
+    return d_buf, d_desc, int(lens.sum()), (buf, desc)
 
 
 def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
@@ -128,6 +137,27 @@ def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
                   f"pico_checksum built -O3, pthreads over contiguous frame ranges; {res[threads][1]} passes on "
                   f"{threads} threads, {res[1][1]} on 1 thread; host {os.uname().machine}, {cores} usable cores",
     }
+
+
+def cpu_baseline_fused(host, ipv6: bool, tx: bool, target_s: float):
+    """The oracle's fused IPv4/IPv6 restatement (oracle/pico_csum_oracle.c, a port of the
+    reference's callers over its pico_checksum) on 1 host core over a bounded sample
+    of the same datagrams (the reference's own IPv4/TCP modules need the whole stack)."""
+    from oracle import oracle as O
+    buf, desc = host
+    k = min(desc.size, 65536)
+    sample, nbytes = desc[:k], int(desc["len"][:k].astype(np.int64).sum())
+    fn = (lambda: O.batch_ipv6(buf, sample, tx=tx)) if ipv6 else (lambda: O.batch_ipv4(buf, sample, tx=tx))
+    t0 = time.perf_counter()
+    fn()
+    reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} datagrams of the batch ({nbytes / 2**20:.0f} MiB), oracle fused "
+                      f"{'IPv6' if ipv6 else 'IPv4'} {'TX' if tx else 'RX'} restatement, gcc -O3, 1 thread, {reps} passes"}
 
 
 def e2e_rate(n, ln):
@@ -201,24 +231,30 @@ def main():
         algo_bytes = per + 2 * n                            # frames read + uint16 results written
     elif cfg["kind"] == "ipv4":
         n = cfg["frames"]
-        ln = 0
+        ln = cfg.get("frame_bytes", 0)
         rot = max(2, a.rotate)
-        sets = [make_c2(n, dev, 500 + 13 * rank + i) for i in range(rot)]
+        sets = [make_c2(n, dev, 500 + 13 * rank + i, ln) for i in range(rot)]
+        fl = batch.F_TX | batch.F_WRITE if cfg.get("tx") else 0
+        outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 
         def step(i):
-            b, d, _ = sets[i % rot]
-            batch.ipv4_checksum_batch(b, d, n)
+            b, d, _, _ = sets[i % rot]
+            batch.ipv4_checksum_batch(b, d, n, flags=fl, out=outs[i % rot])
         frame_bytes = sets[0][2]
-        algo_bytes = frame_bytes + 16 * n + 5 * n           # datagrams + descriptors + (2+2+1) B results
+        # datagrams + descriptors + (2+2+1) B results (+ the two 2-byte crc fields written in place on TX)
+        algo_bytes = frame_bytes + 16 * n + 5 * n + (4 * n if cfg.get("tx") else 0)
     else:
         n = cfg["frames"]
         ln = 0
         rot = max(2, a.rotate)
         sets = [make_c2v6(n, dev, 700 + 13 * rank + i) for i in range(rot)]
+        outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.uint8, device=dev))
+                for _ in range(rot)]
 
         def step(i):
-            b, d, _ = sets[i % rot]
-            batch.ipv6_checksum_batch(b, d, n)
+            b, d, _, _ = sets[i % rot]
+            batch.ipv6_checksum_batch(b, d, n, out=outs[i % rot])
         frame_bytes = sets[0][2]
         algo_bytes = frame_bytes + 16 * n + 3 * n           # datagrams + descriptors + (2+1) B results
 
@@ -282,6 +318,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(sample, ln, a.cpu_seconds)
         if not a.no_e2e:
             out["e2e_host_to_host"] = e2e_rate(n, ln)
+    elif rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_fused(sets[0][3], cfg["kind"] == "ipv6", bool(cfg.get("tx")),
+                                                 a.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

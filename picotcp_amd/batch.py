@@ -96,17 +96,23 @@ def checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, crc_off: int 
     return out
 
 
-def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None):
+def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None, out=None):
     """Fused IPv4 header + transport checksums (RX verify, or TX compute with F_TX).
-    Returns (out_net int16[n], out_transport int16[n], verdict uint8[n])."""
+    Returns (out_net int16[n], out_transport int16[n], verdict uint8[n]); `out` may pass
+    that triple preallocated."""
     _require_device(base, "base")
     _require_device(desc, "desc")
     if desc.numel() < 16 * n:
         raise ValueError("descriptor tensor shorter than n entries")
     dev = base.device
-    out_net = torch.empty(n, dtype=torch.int16, device=dev)
-    out_l4 = torch.empty(n, dtype=torch.int16, device=dev)
-    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+               torch.empty(n, dtype=torch.uint8, device=dev))
+    out_net, out_l4, verdict = out
+    for t, nm in ((out_net, "out_net"), (out_l4, "out_transport"), (verdict, "verdict")):
+        _require_device(t, nm)
+        if t.numel() < n:
+            raise ValueError(f"{nm} shorter than n")
     lib = _lib.load()
     _lib.check("pico_ipv4_checksum_batch_dev",
                lib.pico_ipv4_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_net),
@@ -114,17 +120,23 @@ def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     return out_net, out_l4, verdict
 
 
-def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None):
+def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, stream=None, out=None):
     """Fused IPv6 transport checksums (TCP / UDP / ICMPv6; RX verify, or TX compute with
     F_TX).  desc.seed = net_len | proto << 16 (0: no extension headers).
-    Returns (out_transport int16[n], verdict uint8[n])."""
+    Returns (out_transport int16[n], verdict uint8[n]); `out` may pass that pair
+    preallocated."""
     _require_device(base, "base")
     _require_device(desc, "desc")
     if desc.numel() < 16 * n:
         raise ValueError("descriptor tensor shorter than n entries")
     dev = base.device
-    out_l4 = torch.empty(n, dtype=torch.int16, device=dev)
-    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.uint8, device=dev))
+    out_l4, verdict = out
+    for t, nm in ((out_l4, "out_transport"), (verdict, "verdict")):
+        _require_device(t, nm)
+        if t.numel() < n:
+            raise ValueError(f"{nm} shorter than n")
     lib = _lib.load()
     _lib.check("pico_ipv6_checksum_batch_dev",
                lib.pico_ipv6_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_l4),

@@ -37,8 +37,7 @@ int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint3
                           uint32_t max_blocks, void *stream);
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
-                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t max_blocks,
-                            void *stream);
+                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -141,8 +140,8 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
     if (group == 1 && unroll > 8)
         return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
-    if (group == 2 && (unroll > 8 || !(cpl == 4 || cpl == 8)))
-        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8, unroll = persistent blocks per CU 0..8");
+    if (group == 2 && (unroll != 0 || !(cpl == 4 || cpl == 8)))
+        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8, unroll 0");
     if (group == 3 && (unroll != 0 || cpl != 8 || fpw != 16))
         return fail(PICO_CSUM_EINVAL, "per-wave adaptive kernel: unroll 0, cpl 8, fpw 16");
     if (group > 3 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
@@ -278,8 +277,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
                              "pico_checksum_batch_dev");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
-                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw,
-                                                     s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
@@ -340,8 +338,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
-                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                                     s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, stream),
                              "pico_ipv4_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
@@ -376,8 +373,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
-                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                                     s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, stream),
                              "pico_ipv6_checksum_batch_dev");
     if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
         s.G = 1;

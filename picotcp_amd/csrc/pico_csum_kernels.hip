@@ -1044,7 +1044,7 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
                 }
                 if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
                     store_crc(fp + 10, net);
-                    if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
+                    if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
                     else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
                 }
                 if (p.out_net) p.out_net[f0 + lane] = (uint16_t)net;
@@ -1054,6 +1054,19 @@ __global__ __launch_bounds__(256) void csum_flat_kernel(FlatArgs p) {
         }
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+// The 16-bit LE word at byte q of the register-held chunks D (q + 2 <= 4 * N).
+template <int N>
+__device__ __forceinline__ uint32_t word_at(const uint32_t (&D)[N], uint32_t q) {
+    const uint32_t i = q >> 2;
+    uint32_t lo = D[0], hi = D[1];
+#pragma unroll
+    for (int m = 1; m < N; ++m) {
+        lo = i == (uint32_t)m ? D[m] : lo;
+        hi = i == (uint32_t)m ? (m + 1 < N ? D[m + 1] : 0u) : hi;
+    }
+    return __builtin_amdgcn_alignbyte(hi, lo, q & 3u) & 0xFFFFu;
 }
 
 // ---------------------------------------------------------------- sorted-rounds kernel
@@ -1131,7 +1144,10 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
     }
     if (valid && l == G - 1) {
         L.acc_all[j] = acc;
-        if constexpr (XO) { L.acc_x[j] = accx; L.acc_opt[j] = acco; }
+        if constexpr (XO) {
+            if (xo.x != NONE) L.acc_x[j] = accx;     // else phase 1 stored the field value
+            if (xo.y != 0u) L.acc_opt[j] = acco;
+        }
     }
 }
 
@@ -1196,7 +1212,8 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
             }
             if (verdict == 0) verdict = V_ACCEPT;
         }
-        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l4_needed) store_crc(fp + (xpos - r), l4);
+        if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l4_needed)
+            store_crc(fp + (proto == 6u ? 16u : proto == 17u ? 6u : 2u), l4);
         if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
         if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
     } else {
@@ -1222,7 +1239,7 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
         }
         if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
             store_crc(fp + 10, net);
-            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + (xpos - r), l4);
+            if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
             else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
         }
         if (p.out_net) p.out_net[idx] = (uint16_t)net;
@@ -1253,26 +1270,34 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     uint64_t a0off = off - r;
     uint32_t odd = r & 1u;
 
-    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
+    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0, xval = 0;
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
     bool parsed = false, l4_needed = false;
     if constexpr (MODE == 0) {
         span = ext = len;
         if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
     } else {
-        constexpr uint32_t HDR = IPV6 ? 40u : 20u;
-        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
-        if (len >= HDR) {
+        // header chunks, plus those holding the usual isolated 2-byte field (TCP/UDP/ICMP
+        // crc or ICMPv6 type behind a 20 B IPv4 / 40 B IPv6 header): that field is read
+        // here, so the rounds need no per-chunk field test for it
+        constexpr uint32_t HDR = IPV6 ? 40u : 20u, XEND = HDR + 18u;
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0, c4 = c0;
+        // chunks loaded: through the header and the usual field, within the frame
+        const uint32_t nld = len >= HDR ? (r + min(len, XEND) + 15u) >> 4 : 0u;
+        if (nld) {
             const uint8_t* a0 = p.base + a0off;
             c0 = load_chunk(a0, 0);
-            if (r + HDR > 16) c1 = load_chunk(a0, 1);
-            if (r + HDR > 32) c2 = load_chunk(a0, 2);
-            if (IPV6 && r + HDR > 48) c3 = load_chunk(a0, 3);
+            if (nld > 1) c1 = load_chunk(a0, 1);
+            if (nld > 2) c2 = load_chunk(a0, 2);
+            if (nld > 3) c3 = load_chunk(a0, 3);
+            if (IPV6 && nld > 4) c4 = load_chunk(a0, 4);
         }
+        const uint32_t ld_end = 16u * nld;            // register-held bytes from a0
         const uint32_t avail = len;
         if constexpr (IPV4) {
             if (avail >= 20) {
-                const uint32_t D[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+                const uint32_t D[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
                 const uint32_t q = r >> 2, sh = r & 3u;
                 uint32_t E[6];
 #pragma unroll
@@ -1312,12 +1337,17 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                             else { l4_needed = true; xpos = r + hl + 2u; }
                         }
                     }
+                    if (xpos != NONE && xpos + 2u <= ld_end) {
+                        xval = word_at(D, xpos);
+                        xpos = NONE;
+                        ext = span;
+                    }
                 }
             }
         } else {
             if (avail >= 40) {
-                const uint32_t D[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+                const uint32_t D[20] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y,
+                                        c2.z, c2.w, c3.x, c3.y, c3.z, c3.w, c4.x, c4.y, c4.z, c4.w};
                 const uint32_t q = r >> 2, sh = r & 3u;
                 uint32_t E[11];
 #pragma unroll
@@ -1356,6 +1386,9 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                         }
                     }
                     if (parsed) {
+                        const uint32_t xh = r + net_len + xrel;   // field, header-relative
+                        const bool xfast = xrel != NONE && net_len == 40u && xh + 2u <= ld_end;
+                        if (xfast) { xval = word_at(D, xh); xrel = NONE; ext = tl; }
                         off += net_len;
                         fp = p.base + off;
                         r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
@@ -1373,7 +1406,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
     const uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
     L.acc_all[lane] = 0;
-    L.acc_x[lane] = 0;
+    L.acc_x[lane] = xval;
     L.acc_opt[lane] = 0;
     L.nch[lane] = nch;
     L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4));
@@ -1424,17 +1457,15 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     __builtin_amdgcn_wave_barrier();
 }
 
-// One wave per 64-frame batch; with a capped grid (persistent) waves loop over
-// batches and drift out of step, so one wave's descriptor/header latency overlaps
-// other waves' rounds.
+// One wave per batch of up to 64 frames.  (A persistent grid looping over batches
+// measured slower: every wave repeats the same serial descriptor -> rounds chain.)
 template <int MODE, bool NT, int CPL>
 __global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveLds lds_all[4];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveLds& L = lds_all[threadIdx.x >> 6];
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w * p.fpw < p.n; w += waves)
-        sorted_batch<MODE, NT, CPL>(p, L, lane, w * p.fpw);
+    const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL>(p, L, lane, f0);
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -1474,16 +1505,12 @@ extern "C" {
 // Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6.
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t max_blocks,
-                            void* stream) {
+                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void* stream) {
     if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict};
-    dim3 grid = grid_for(n, fpw);
-    const dim3 block(256);
-    if (max_blocks == 0) return (int)hipErrorInvalidValue;
-    if (grid.x > max_blocks) grid.x = max_blocks;
+    const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);
     using K = void (*)(FlatArgs);
     static const K table[3][2][2] = {

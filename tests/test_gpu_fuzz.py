@@ -31,7 +31,7 @@ def to_dev(a):
 
 
 # launch shapes exercised for descriptor batches: auto (adaptive), flat, lane groups
-DESC_SHAPES = [None, (3, 8, 16, 0, 1), (2, 8, 64, 0, 2), (2, 8, 3, 1, 2), (2, 8, 5, 0, 1), (2, 4, 33, 0, 1), (1, 1, 1, 0, 1), (1, 4, 64, 0, 2), (1, 2, 7, 2, 1), (4, 8, 16, 1, 1), (64, 2, 4, 1, 2),
+DESC_SHAPES = [None, (3, 8, 16, 0, 1), (2, 8, 64, 0, 2), (2, 8, 5, 0, 1), (2, 4, 33, 0, 1), (1, 1, 1, 0, 1), (1, 4, 64, 0, 2), (1, 2, 7, 2, 1), (4, 8, 16, 1, 1), (64, 2, 4, 1, 2),
                (16, 8, 12, 1, 1)]
 
 

@@ -70,7 +70,7 @@ def main():
             b, d = sets[i % rot]
             batch.ipv6_checksum_batch(b, d, n)
         algo = int(lens.sum()) + 19 * n
-    elif a.config in ("c2raw", "c2"):
+    elif a.config in ("c2raw", "c2", "c2tx", "c2txnw"):
         n = 262144
         lens = synth.imix_lengths(n, 3)
         rot = 3
@@ -87,9 +87,11 @@ def main():
                 b, d = sets[i % rot]
                 batch.checksum_batch(b, d, n, out=outs[i % rot])
         else:
+            fl = {"c2": 0, "c2tx": batch.F_TX | batch.F_WRITE, "c2txnw": batch.F_TX}[a.config]
+
             def launch(i):
                 b, d = sets[i % rot]
-                batch.ipv4_checksum_batch(b, d, n)
+                batch.ipv4_checksum_batch(b, d, n, flags=fl)
         algo = int(lens.sum()) + 16 * n + (2 if a.config == "c2raw" else 5) * n
     else:
         raise SystemExit("unknown config")
