@@ -30,14 +30,15 @@ int pico_csum_launch_desc_adaptive(void *base, uint64_t base_len, const void *de
                                    uint32_t flags, uint16_t *out, uint32_t *bad, uint32_t nt, void *stream);
 int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
-                                void *stream);
+                                uint32_t win, void *stream);
 int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode,
                           int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
                           uint32_t max_blocks, void *stream);
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
-                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void *stream);
+                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
+                            void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -131,8 +132,9 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = g_ovr_pipe = 0;
         return 0;
     }
-    if (pipeline > 2)
-        return fail(PICO_CSUM_EINVAL, "pipeline must be 0 (auto), 1 (off) or 2 (on)");
+    if (pipeline > 3)
+        return fail(PICO_CSUM_EINVAL, "pipeline must be 0 (auto), 1 (off), 2 (on) or 3 (on, global loads "
+                                        "instead of the buffer window)");
     if (!(group == 1 || group == 2 || group == 3 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
         return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 2 (sorted rounds), 3 (per-wave adaptive), "
                                         "4, 8, 16, 32 or 64");
@@ -140,8 +142,10 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
     if (group == 1 && unroll > 8)
         return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
-    if (group == 2 && (unroll != 0 || !(cpl == 4 || cpl == 8)))
-        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8, unroll 0");
+    if (group == 2 && (!(unroll == 0 || unroll == 1 || unroll == 4) || !(cpl == 4 || cpl == 8) ||
+                       (unroll == 1 && cpl != 8)))
+        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8; unroll = narrowest round width "
+                                        "0 (auto), 1 (cpl 8 only) or 4");
     if (group == 3 && (unroll != 0 || cpl != 8 || fpw != 16))
         return fail(PICO_CSUM_EINVAL, "per-wave adaptive kernel: unroll 0, cpl 8, fpw 16");
     if (group > 3 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
@@ -203,15 +207,18 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
         uint32_t f = n / 4096u;
         s.G = 2;
         s.CPL = 8;
-        s.U = 0;
+        s.U = 1;            /* narrowest round width: 1 = one frame per lane for <= 8-chunk frames */
         s.nt = 1;
         s.fpw = f < 16 ? 16 : f > 64 ? 64 : f;
     }
     if (g_ovr_group) {
+        uint32_t auto_u = s.U;
         s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
+        if (s.G == 2 && s.U == 0)
+            s.U = s.CPL == 8 ? auto_u : 4;
         s.nt = g_ovr_nt >= 2 ? g_ovr_nt - 1 : 0;
         if (g_ovr_pipe)
-            s.pipe = g_ovr_pipe == 2;
+            s.pipe = g_ovr_pipe >= 2;
     }
     return s;
 }
@@ -277,7 +284,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
                              "pico_checksum_batch_dev");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
-                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, stream),
+                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, s.U == 1, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
@@ -308,7 +315,7 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return fail(PICO_CSUM_EINVAL, "groups 1-3 (flat, sorted, adaptive) serve descriptor batches only");
     if (s.pipe && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u)
         return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,
-                                                         s.nt, s.fpw, stream),
+                                                         s.nt, s.fpw, g_ovr_pipe != 3, stream),
                              "pico_checksum_batch_uniform_dev");
     return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
                                               d_out, NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, stream),
@@ -338,7 +345,8 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
-                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, stream),
+                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
+                                                     stream),
                              "pico_ipv4_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
@@ -373,7 +381,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
-                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, stream),
+                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1, stream),
                              "pico_ipv6_checksum_batch_dev");
     if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
         s.G = 1;

@@ -154,6 +154,40 @@ __device__ __forceinline__ uint4 load_chunk_t(const uint8_t* a0, uint32_t k) {
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// ---- windowed buffer loads
+//
+// A wave's frames lie in a window of < 2 GiB.  A buffer resource over that window
+// (built from wave-uniform values: SGPRs, no waterfall) lets every lane issue every
+// load slot unconditionally: a slot past its frame gets voffset WIN_OOB, which the
+// range check turns into zeros without a memory access.  With no branch around the
+// loads the compiler can count them, so a wave consumes set i behind
+// s_waitcnt vmcnt(#set i+1) with set i+1 still in flight -- a `k < nch ? load : 0`
+// becomes an s_cbranch_execz around each load, after which hipcc only dares vmcnt(0).
+constexpr uint32_t WIN_OOB = 0x80000000u;    // >= every window's num_records
+
+struct Window {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint64_t base;                          // window start (16-byte aligned address)
+};
+
+// Window [lo, lo + bytes) over device addresses; lo and bytes must be wave-uniform
+// values (they are read from the first lane), bytes < 2^31.
+__device__ __forceinline__ Window make_window(uint64_t lo, uint32_t bytes) {
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lo);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lo >> 32));
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bytes);
+    Window w;
+    w.base = ((uint64_t)h << 32) | l;
+    w.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(w.base), 0, (int)nb, 0x00020000);
+    return w;
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 load_win(const Window& w, uint32_t voff) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, (int)voff, 0, NT ? 2 : 0);   // aux 2 = nt
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+
 }  // namespace
 
 // Device view of struct pico_csum_desc (include/pico_csum.h), 16 bytes.
@@ -345,8 +379,12 @@ __global__ __launch_bounds__(256) void csum_desc_adaptive_kernel(RawArgs p) {
 // NTM: 0 plain loads, 1 non-temporal, 2 non-temporal except the slots that hold a
 // frame's head or tail chunk (the 128-byte line two neighbouring frames share
 // stays in L2 for the second reader).
-template <int G, int CPL, int NTM>
+// BUF (NTM 0/1): loads through a buffer window over the wave's frames (see
+// make_window), so the two frame sets really overlap; the host guarantees the
+// window, (fpw - 1) * stride + len + 32 bytes, is below 2 GiB.
+template <int G, int CPL, int NTM, bool BUF = false>
 __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
+    static_assert(!BUF || NTM < 2, "windowed loads: NTM 0 or 1");
     constexpr uint32_t NG = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t g = lane / G, l = lane % G;
@@ -354,6 +392,10 @@ __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
     const uint64_t f0 = wave * p.fpw;
     if (f0 >= p.n) return;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    Window win{};
+    if constexpr (BUF)
+        win = make_window(reinterpret_cast<uint64_t>(p.base + f0 * p.stride) & ~15ull,
+                          (uint32_t)((uint64_t)(cnt - 1u) * p.stride + p.len + 32u));
 
     struct Frame {
         const uint8_t* a0;
@@ -380,6 +422,9 @@ __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
                 const bool edge_slot = __builtin_amdgcn_ballot_w64(k < f.nch && (k == 0 || k + 1 == f.nch)) != 0;
                 if (edge_slot) v[c] = k < f.nch ? load_chunk_t<false>(f.a0, k) : make_uint4(0, 0, 0, 0);
                 else v[c] = k < f.nch ? load_chunk_t<true>(f.a0, k) : make_uint4(0, 0, 0, 0);
+            } else if constexpr (BUF) {
+                const uint32_t rel = (uint32_t)(reinterpret_cast<uint64_t>(f.a0) - win.base);
+                v[c] = load_win<NTM == 1>(win, k < f.nch ? rel + (k << 4) : WIN_OOB);
             } else {
                 v[c] = k < f.nch ? load_chunk_t<NTM == 1>(f.a0, k) : make_uint4(0, 0, 0, 0);
             }
@@ -1154,17 +1199,24 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
 // Round width: the smallest G whose one pass (G lanes x CPL chunks) covers the
 // round's largest frame; 64 lanes per frame beyond that.  NT: non-temporal loads
 // in the rounds of G >= 16 (frames over ~1 KiB; measured: they cost on small ones).
-template <int CPL, bool PERM, bool NT, bool XO>
-__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, const uint32_t (&e)[4], uint32_t m) {
-    // position s holds a frame of class <= c iff s < e[c-1]; a round of width G may
+// SMALL adds a 1-lane class below the 4-lane one: frames of <= CPL chunks (<= 8 x 16 B,
+// e.g. 64-byte IMIX frames) are summed one frame per lane, 64 per round, so a wave
+// pays one dependent HBM round trip for all its small frames instead of one per 16.
+template <int CPL, bool PERM, bool NT, bool XO, bool SMALL>
+__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, const uint32_t (&e)[5], uint32_t m) {
+    // position s holds a frame of class <= c iff s < e[c]; a round of width G may
     // take the next 64/G positions when the last of them is of class <= G's class
+    constexpr int o = SMALL ? 1 : 0;
     uint32_t pos = 0;
+    if constexpr (SMALL) {
+        if (e[0]) { sorted_round<1, CPL, PERM, false, XO>(p, L, 0u, min(m, e[0])); pos = min(e[0], 64u); }
+    }
     while (pos < m) {
-        if (min(pos + 15u, m - 1u) < e[0])        { sorted_round<4, CPL, PERM, false, XO>(p, L, pos, m);  pos += 16u; }
-        else if (min(pos + 7u, m - 1u) < e[1])    { sorted_round<8, CPL, PERM, false, XO>(p, L, pos, m);  pos += 8u; }
-        else if (min(pos + 3u, m - 1u) < e[2])    { sorted_round<16, CPL, PERM, NT, XO>(p, L, pos, m); pos += 4u; }
-        else if (min(pos + 1u, m - 1u) < e[3])    { sorted_round<32, CPL, PERM, NT, XO>(p, L, pos, m); pos += 2u; }
-        else                                      { sorted_round<64, CPL, PERM, NT, XO>(p, L, pos, m); pos += 1u; }
+        if (min(pos + 15u, m - 1u) < e[o])            { sorted_round<4, CPL, PERM, false, XO>(p, L, pos, m);  pos += 16u; }
+        else if (min(pos + 7u, m - 1u) < e[o + 1])    { sorted_round<8, CPL, PERM, false, XO>(p, L, pos, m);  pos += 8u; }
+        else if (min(pos + 3u, m - 1u) < e[o + 2])   { sorted_round<16, CPL, PERM, NT, XO>(p, L, pos, m); pos += 4u; }
+        else if (min(pos + 1u, m - 1u) < e[o + 3])   { sorted_round<32, CPL, PERM, NT, XO>(p, L, pos, m); pos += 2u; }
+        else                                          { sorted_round<64, CPL, PERM, NT, XO>(p, L, pos, m); pos += 1u; }
     }
 }
 
@@ -1251,7 +1303,7 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
 // CPL 8 keeps 8 KiB of loads in flight per wave within 128 VGPRs (4 waves per
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
-template <int MODE, bool NT, int CPL>
+template <int MODE, bool NT, int CPL, bool SMALL>
 __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
@@ -1420,19 +1472,26 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     // ---- 2. order the frames by size class (the narrowest round width that covers
     //         them in one pass): ballots and bit counts, no data movement but one
     //         LDS store per frame
-    const uint32_t cls = nch == 0 ? 5u : nch <= 4u * CPL ? 0u : nch <= 8u * CPL ? 1u : nch <= 16u * CPL ? 2u
-                                                                  : nch <= 32u * CPL ? 3u : 4u;
-    uint64_t bal[5];
+    // classes by round width: (SMALL: 1,) 4, 8, 16, 32, 64 lanes; NC = no data
+    constexpr uint32_t NC = SMALL ? 6u : 5u;
+    const uint32_t cw = nch <= 4u * CPL ? 0u : nch <= 8u * CPL ? 1u : nch <= 16u * CPL ? 2u : nch <= 32u * CPL ? 3u : 4u;
+    const uint32_t cls = nch == 0 ? NC : SMALL ? (nch <= (uint32_t)CPL ? 0u : cw + 1u) : cw;
+    uint64_t bal[NC];
 #pragma unroll
-    for (int c = 0; c < 5; ++c) bal[c] = __builtin_amdgcn_ballot_w64(cls == (uint32_t)c);
-    uint32_t e[4];
+    for (uint32_t c = 0; c < NC; ++c) bal[c] = __builtin_amdgcn_ballot_w64(cls == c);
+    uint32_t e[5] = {0, 0, 0, 0, 0};     // e[c] = frames of class <= c
     e[0] = (uint32_t)__builtin_popcountll(bal[0]);
 #pragma unroll
-    for (int c = 1; c < 4; ++c) e[c] = e[c - 1] + (uint32_t)__builtin_popcountll(bal[c]);
-    const uint32_t m = e[3] + (uint32_t)__builtin_popcountll(bal[4]);
-    if (cls < 5u) {
-        const uint64_t mine = cls == 0 ? bal[0] : cls == 1 ? bal[1] : cls == 2 ? bal[2] : cls == 3 ? bal[3] : bal[4];
-        const uint32_t start = cls == 0 ? 0u : e[cls - 1];
+    for (uint32_t c = 1; c + 1 < NC; ++c) e[c] = e[c - 1] + (uint32_t)__builtin_popcountll(bal[c]);
+    const uint32_t m = e[NC - 2] + (uint32_t)__builtin_popcountll(bal[NC - 1]);
+    if (cls < NC) {
+        uint64_t mine = bal[0];
+        uint32_t start = 0;
+#pragma unroll
+        for (uint32_t c = 1; c < NC; ++c) {
+            mine = cls == c ? bal[c] : mine;
+            start = cls == c ? e[c - 1] : start;
+        }
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
         L.order[start + rank] = lane;
     }
@@ -1442,11 +1501,11 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
     if (m) {
         if (any_odd) {
-            if (any_xo) sorted_rounds<CPL, true, NT, true>(ra, L, e, m);
-            else sorted_rounds<CPL, true, NT, false>(ra, L, e, m);
+            if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
+            else sorted_rounds<CPL, true, NT, false, SMALL>(ra, L, e, m);
         } else {
-            if (any_xo) sorted_rounds<CPL, false, NT, true>(ra, L, e, m);
-            else sorted_rounds<CPL, false, NT, false>(ra, L, e, m);
+            if (any_xo) sorted_rounds<CPL, false, NT, true, SMALL>(ra, L, e, m);
+            else sorted_rounds<CPL, false, NT, false, SMALL>(ra, L, e, m);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1459,13 +1518,13 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
-template <int MODE, bool NT, int CPL>
+template <int MODE, bool NT, int CPL, bool SMALL = false>
 __global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveLds lds_all[4];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveLds& L = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
-    if (f0 < p.n) sorted_batch<MODE, NT, CPL>(p, L, lane, f0);
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, L, lane, f0);
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -1502,25 +1561,27 @@ extern "C" {
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
 
-// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6.
+// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6; small: 1-lane
+// rounds for frames of <= 8 chunks (cpl 8 only).
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, void* stream) {
-    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
+                            void* stream) {
+    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 2 || (small && cpl != 8))
+        return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict};
     const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);
     using K = void (*)(FlatArgs);
-    static const K table[3][2][2] = {
-        {{csum_sorted_kernel<0, false, 4>, csum_sorted_kernel<0, false, 8>},
-         {csum_sorted_kernel<0, true, 4>, csum_sorted_kernel<0, true, 8>}},
-        {{csum_sorted_kernel<1, false, 4>, csum_sorted_kernel<1, false, 8>},
-         {csum_sorted_kernel<1, true, 4>, csum_sorted_kernel<1, true, 8>}},
-        {{csum_sorted_kernel<2, false, 4>, csum_sorted_kernel<2, false, 8>},
-         {csum_sorted_kernel<2, true, 4>, csum_sorted_kernel<2, true, 8>}}};
-    hipLaunchKernelGGL(table[mode][nt ? 1 : 0][cpl == 8 ? 1 : 0], grid, block, 0, s, a);
+    // [mode][nt][cpl 4 | cpl 8 | cpl 8 with the 1-lane class]
+#define SK(m, t) {csum_sorted_kernel<m, t, 4>, csum_sorted_kernel<m, t, 8>, csum_sorted_kernel<m, t, 8, true>}
+    static const K table[3][2][3] = {{SK(0, false), SK(0, true)}, {SK(1, false), SK(1, true)},
+                                     {SK(2, false), SK(2, true)}};
+#undef SK
+    const int v = cpl == 4 ? 0 : small ? 2 : 1;
+    hipLaunchKernelGGL(table[mode][nt ? 1 : 0][v], grid, block, 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -1540,19 +1601,24 @@ int pico_csum_launch_desc_adaptive(void* base, uint64_t base_len, const void* de
 // Software-pipelined uniform kernel (one pass per frame: G*CPL*16 >= len + 15).
 int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t* out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
-                                void* stream) {
+                                uint32_t win, void* stream) {
     if (!shape_ok(G, CPL, fpw) || (uint64_t)G * CPL * 16u < (uint64_t)len + 15u) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     RawArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), base_len, nullptr, stride, len, n, seed, -1, 0u, fpw,
               out, nullptr};
     const dim3 grid = grid_for(n, fpw), block(256);
     hipStream_t s = static_cast<hipStream_t>(stream);
-#define X(g, c)                                                                                     \
-    if (G == g && CPL == c) {                                                                       \
-        if (nt == 2) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 2>), grid, block, 0, s, a);   \
-        else if (nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 1>), grid, block, 0, s, a);   \
-        else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 0>), grid, block, 0, s, a);          \
-        return (int)hipGetLastError();                                                              \
+    // windowed loads unless the override asks for the global-load form (A/B) or the
+    // wave's window would reach 2 GiB
+    const bool buf = win && nt < 2 && (uint64_t)(fpw - 1) * stride + len + 32u < (1ull << 31);
+#define X(g, c)                                                                                          \
+    if (G == g && CPL == c) {                                                                            \
+        if (nt == 2) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 2>), grid, block, 0, s, a);        \
+        else if (buf && nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 1, true>), grid, block, 0, s, a); \
+        else if (buf) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 0, true>), grid, block, 0, s, a); \
+        else if (nt) hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 1>), grid, block, 0, s, a);        \
+        else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 0>), grid, block, 0, s, a);               \
+        return (int)hipGetLastError();                                                                   \
     }
     PICO_FOR_SHAPES(X)
 #undef X

@@ -101,14 +101,18 @@ def test_launch_override_validation():
     assert lib.pico_csum_set_launch_override(16, 2, 1, 6, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 4, 4, 16, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 4, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 1, 3) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 1, 4) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 1, 3) == 0
     assert lib.pico_csum_set_launch_override(16, 2, 4, 16, 2, 2) == 0
     assert lib.pico_csum_set_launch_override(1, 4, 1, 7, 1, 0) == 0
     assert lib.pico_csum_set_launch_override(1, 4, 8, 7, 1, 0) == 0
     assert lib.pico_csum_set_launch_override(1, 4, 9, 7, 1, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(1, 4, 0, 7, 1, 0) == 0
     assert lib.pico_csum_set_launch_override(2, 8, 0, 37, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 8, 1, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 8, 2, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 4, 1, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 8, 1, 16, 2, 0) == 0
+    assert lib.pico_csum_set_launch_override(2, 8, 4, 16, 2, 0) == 0
     assert lib.pico_csum_set_launch_override(2, 2, 0, 16, 2, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(3, 8, 0, 16, 1, 0) == 0
     assert lib.pico_csum_set_launch_override(3, 8, 0, 32, 1, 0) == -_lib.EINVAL
