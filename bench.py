@@ -90,7 +90,16 @@ def make_uniform(n, ln, device, seed):
     return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=device, generator=g)
 
 
-def make_c2(n, device, seed, frame_bytes=0):
+IMIX_MEAN = 354          # simple-IMIX mean datagram length (7:4:1 of 64/576/1500 B)
+
+
+def rotation(batch_bytes: int) -> int:
+    """Batch copies to rotate so that >= 1 GiB lies between two uses of one batch: the
+    256 MiB Infinity Cache then cannot serve a repeat (MI355X_MICROARCH.md, L3)."""
+    return max(3, -(-(1 << 30) // max(1, batch_bytes)))
+
+
+def make_c2(n, device, seed, frame_bytes=0, keep_host=True):
     lens = synth.imix_lengths(n, seed) if not frame_bytes else np.full(n, frame_bytes, dtype=np.uint32)
     buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
     desc = batch.make_desc(net, avail)
@@ -99,10 +108,10 @@ def make_c2(n, device, seed, frame_bytes=0):
     # make every datagram valid with the TX kernel (untimed setup), so RX verify accepts
     batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum()), (buf, desc)
+    return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
 
 
-def make_c2v6(n, device, seed):
+def make_c2v6(n, device, seed, keep_host=True):
     lens = (synth.imix_lengths(n, seed) + 20).astype(np.uint32)
     buf, net, avail, seeds = synth.ipv6_batch(lens, seed=seed + 1, proto=6, eth=True)
     desc = batch.make_desc(net, avail, seeds)
@@ -110,7 +119,7 @@ def make_c2v6(n, device, seed):
     d_desc = batch.desc_to_device(desc, device)
     batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum()), (buf, desc)
+    return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
 
 
 def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
@@ -221,7 +230,7 @@ def main():
         else:
             first, n = rank * cfg["frames"], cfg["frames"]
         per = n * ln
-        rot = a.rotate or max(2, -(-(1 << 30) // per))
+        rot = a.rotate or rotation(per)
         bufs = [make_uniform(n, ln, dev, 1000 + 17 * rank + i) for i in range(rot)]
         outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
 
@@ -232,8 +241,8 @@ def main():
     elif cfg["kind"] == "ipv4":
         n = cfg["frames"]
         ln = cfg.get("frame_bytes", 0)
-        rot = max(2, a.rotate)
-        sets = [make_c2(n, dev, 500 + 13 * rank + i, ln) for i in range(rot)]
+        rot = a.rotate or rotation(n * ((ln or IMIX_MEAN) + 14))
+        sets = [make_c2(n, dev, 500 + 13 * rank + i, ln, keep_host=i == 0) for i in range(rot)]
         fl = batch.F_TX | batch.F_WRITE if cfg.get("tx") else 0
         outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                  torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
@@ -247,8 +256,8 @@ def main():
     else:
         n = cfg["frames"]
         ln = 0
-        rot = max(2, a.rotate)
-        sets = [make_c2v6(n, dev, 700 + 13 * rank + i) for i in range(rot)]
+        rot = a.rotate or rotation(n * (IMIX_MEAN + 20 + 14))
+        sets = [make_c2v6(n, dev, 700 + 13 * rank + i, keep_host=i == 0) for i in range(rot)]
         outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.uint8, device=dev))
                 for _ in range(rot)]
 

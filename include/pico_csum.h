@@ -79,6 +79,7 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_NET_BAD   2u  /* pico_ipv4_crc_check would discard (pico_ipv4.c:249-253) */
 #define PICO_CSUM_V_L4_BAD    4u  /* pico_transport_crc_check would discard (pico_socket.c:1929,1953) */
 #define PICO_CSUM_V_MALFORMED 8u  /* infeasible length (pico_ipv4.c:402-405) or a region past the buffer */
+#define PICO_CSUM_V_EXPIRED  16u  /* forwarding: TTL reached 0 (pico_ipv4.c:1549-1552) */
 
 /* ---------------------------------------------------------------- layer 1 */
 
@@ -156,6 +157,16 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream);
 
+/* Forwarding step of pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) for a batch
+ * of IPv4 datagrams routed through this host (desc.off -> IPv4 header, desc.len =
+ * bytes available, >= 20): hdr->ttl is decremented in place; a datagram whose TTL
+ * reaches 0 is PICO_CSUM_V_EXPIRED (the reference drops it, crc untouched); every
+ * other one gets the reference's `hdr->crc++` (:1556, a native little-endian
+ * increment of the stored field) and PICO_CSUM_V_ACCEPT.  Regions past base_len or
+ * shorter than 20 bytes are MALFORMED and untouched.  d_verdict may be NULL. */
+int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                uint8_t *d_verdict, void *stream);
+
 /* ---------------------------------------------------------------- layer 3 */
 
 struct pico_csum_ctx;   /* device, two streams, double-buffered staging */
@@ -181,9 +192,11 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
  * per pass (1,2,4,8); unroll = frames in flight per group (1,2,4; RAW batches
  * only, cpl*unroll <= 8); fpw = frames per wave (multiple of 64/group, <= 64);
  * nt = 0 auto / 1 plain / 2 non-temporal loads (RAW batches); pipeline = 0 auto /
- * 1 off / 2 on (uniform batches whose frames fit one pass: double-buffered frame
- * sets).  group = 1 selects the flat work-list kernel, group = 2 the sorted-rounds
- * kernel (descriptor batches only; unroll must be 0 for group 2).
+ * 1 off / 2 on / 3 on with global instead of buffer-window loads (uniform batches
+ * whose frames fit one pass: double-buffered frame sets).  group = 1 selects the
+ * flat work-list kernel, group = 2 the sorted-rounds kernel (descriptor batches
+ * only; there unroll = the narrowest round width: 0 auto, 1 = one frame per lane
+ * for frames of <= 8 chunks (cpl 8), 4), group = 3 the per-wave adaptive kernel.
  * Process-wide. */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);

@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_ipv6_pseudo_sum.argtypes = [_vp, _vp, ctypes.c_uint8, _u32]
         L.oracle_batch_ipv6.restype = None
         L.oracle_batch_ipv6.argtypes = [_vp, _vp, _u32, _vp, _vp, _u32]
+        L.oracle_batch_ipv4_forward.restype = None
+        L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
         L.oracle_uniform_mt.argtypes = [_vp, _vp, _u64, _u32, _u32, _vp, _u32]
         _olib = L
@@ -131,6 +133,14 @@ def batch_ipv6(base: np.ndarray, desc: np.ndarray, tx: bool = False):
     ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint8)
     lib().oracle_batch_ipv6(_p(base), _p(desc), n, _p(ol), _p(v), ORACLE_IPV4_TX if tx else 0)
     return ol, v
+
+
+def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:
+    """pico_ipv4_forward's TTL step, in place on `base` (a writable uint8 array); verdicts."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    v = np.zeros(desc.shape[0], np.uint8)
+    lib().oracle_batch_ipv4_forward(_p(base), _p(desc), desc.shape[0], _p(v))
+    return v
 
 
 # ---------------------------------------------------------------- reference

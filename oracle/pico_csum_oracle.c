@@ -318,6 +318,32 @@ void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint
     }
 }
 
+/* modules/pico_ipv4.c:1547-1556 (pico_ipv4_forward): hdr->ttl = (uint8_t)(hdr->ttl - 1);
+ * if (hdr->ttl < 1) -> expired, dropped; else hdr->crc++ (uint16_t field, native LE
+ * increment of the stored big-endian checksum).  In place on base; verdict per
+ * datagram: ACCEPT (forwarded), EXPIRED, MALFORMED (< 20 bytes: untouched). */
+void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict)
+{
+    uint32_t i;
+    for (i = 0; i < n; i++) {
+        uint8_t *h = base + d[i].off;
+        uint16_t crc;
+        if (d[i].len < 20) {
+            verdict[i] = PICO_CSUM_V_MALFORMED;
+            continue;
+        }
+        h[8] = (uint8_t)(h[8] - 1);
+        if (h[8] < 1) {
+            verdict[i] = PICO_CSUM_V_EXPIRED;
+            continue;
+        }
+        memcpy(&crc, h + 10, 2);
+        crc++;
+        memcpy(h + 10, &crc, 2);
+        verdict[i] = PICO_CSUM_V_ACCEPT;
+    }
+}
+
 /* ---- multi-threaded CPU baseline driver (bench.py cpu_baseline leg) ---- */
 
 struct mt_job {

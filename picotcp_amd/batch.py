@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import F_TX, F_WRITE, V_ACCEPT, V_L4_BAD, V_MALFORMED, V_NET_BAD  # noqa: F401
+from ._lib import F_TX, F_WRITE, V_ACCEPT, V_EXPIRED, V_L4_BAD, V_MALFORMED, V_NET_BAD  # noqa: F401
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
 assert DESC_DTYPE.itemsize == 16
@@ -142,6 +142,24 @@ def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
                lib.pico_ipv6_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_l4),
                                                 _ptr(verdict), _stream_handle(stream)))
     return out_l4, verdict
+
+
+def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: torch.Tensor | None = None,
+                       stream=None) -> torch.Tensor:
+    """pico_ipv4_forward's TTL step (pico_ipv4.c:1547-1556) in place on n datagrams:
+    ttl - 1, then the reference's crc++ unless the TTL expired.  Returns the verdicts
+    (V_ACCEPT = forwarded, V_EXPIRED, V_MALFORMED)."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    if verdict is None:
+        verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
+    lib = _lib.load()
+    _lib.check("pico_ipv4_forward_batch_dev",
+               lib.pico_ipv4_forward_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, _ptr(verdict),
+                                               _stream_handle(stream)))
+    return verdict
 
 
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,

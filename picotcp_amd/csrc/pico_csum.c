@@ -39,6 +39,8 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
                             void *stream);
+int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
+                                  void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -393,6 +395,22 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                                d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
                                                s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
                          "pico_ipv6_checksum_batch_dev");
+}
+
+int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                uint8_t *d_verdict, void *stream)
+{
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if ((rc = need_device()) != 0)
+        return rc;
+    return launch_status(pico_csum_launch_ipv4_forward(d_base, base_len, d_desc, n, d_verdict, stream),
+                         "pico_ipv4_forward_batch_dev");
 }
 
 /* ------------------------------------------------------------------ layer 3 */

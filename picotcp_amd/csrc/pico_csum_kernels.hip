@@ -469,7 +469,7 @@ struct Ipv4Args {
     uint8_t* verdict;
 };
 
-constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u;
+constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u, V_EXPIRED = 16u;
 
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
@@ -1130,13 +1130,15 @@ __device__ __forceinline__ uint32_t word_at(const uint32_t (&D)[N], uint32_t q) 
 //      keeps its lanes busy; per-frame sums go to LDS;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
+constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1
+
 struct SortedWaveLds {
     uint32_t acc_all[64];
     uint32_t acc_x[64];
     uint32_t acc_opt[64];
     uint32_t nch[64];
-    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4}
-    uint2 xo[64];          // {field position (NONE), option end (0)}
+    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4 | k0 << 5}
+    uint2 xo[64];          // {field position (NONE), option end (0)}, relative to a0 + 16 k0
     uint32_t order[64];    // frames by size class: order[position] = frame (lane)
     uint4 fin[64];         // parse state for phase 4 (kept in LDS, not VGPRs, across the rounds):
                            // {verdict | parsed << 4 | l4 << 5 | oob << 6 | proto << 8 | tl << 16,
@@ -1154,10 +1156,12 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
     const uint32_t nch = valid ? L.nch[j] : 0u;
     const uint4 fi = L.info[j];
     const uint2 xo = XO ? L.xo[j] : make_uint2(NONE, 0u);
-    const uint32_t rr = fi.w & 15u;
+    // the rounds start k0 chunks into the region (phase 1 summed the head window)
+    const uint32_t k0 = (fi.w >> 5) & 15u;
+    const uint32_t rr = k0 ? 0u : fi.w & 15u;
     const uint32_t sl = (fi.w & 16u) ? SEL_ODD : SEL_EVEN;
-    const uint32_t send = fi.z;
-    const uint8_t* a0 = p.base + ((((uint64_t)fi.y) << 32) | fi.x);
+    const uint32_t send = fi.z > 16u * k0 ? fi.z - 16u * k0 : 0u;
+    const uint8_t* a0 = p.base + ((((uint64_t)fi.y) << 32) | fi.x) + 16u * k0;
     uint32_t acc = 0, accx = 0, acco = 0;
     for (uint32_t kb = 0; kb < nch; kb += G * CPL) {
         uint4 v[CPL];
@@ -1187,11 +1191,11 @@ __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L,
         accx = group_sum<G>(accx);
         acco = group_sum<G>(acco);
     }
-    if (valid && l == G - 1) {
-        L.acc_all[j] = acc;
+    if (valid && l == G - 1) {           // added to phase 1's head-window sums
+        L.acc_all[j] += acc;
         if constexpr (XO) {
-            if (xo.x != NONE) L.acc_x[j] = accx;     // else phase 1 stored the field value
-            if (xo.y != 0u) L.acc_opt[j] = acco;
+            if (xo.x != NONE) L.acc_x[j] += accx;
+            if (xo.y != 0u) L.acc_opt[j] += acco;
         }
     }
 }
@@ -1322,29 +1326,30 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     uint64_t a0off = off - r;
     uint32_t odd = r & 1u;
 
-    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0, xval = 0;
+    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0;
     bool parsed = false, l4_needed = false;
+    const uint64_t a0h = a0off;                  // the head window's first chunk (fused modes)
+    uint4 hw[HW];
+    uint32_t nlh = 0;                            // head-window chunks loaded
+    uint32_t k0 = 0, p_all = 0, p_x = 0, p_opt = 0;
     if constexpr (MODE == 0) {
         span = ext = len;
         if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
     } else {
-        // header chunks, plus those holding the usual isolated 2-byte field (TCP/UDP/ICMP
-        // crc or ICMPv6 type behind a 20 B IPv4 / 40 B IPv6 header): that field is read
-        // here, so the rounds need no per-chunk field test for it
-        constexpr uint32_t HDR = IPV6 ? 40u : 20u, XEND = HDR + 18u;
-        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0, c4 = c0;
-        // chunks loaded: through the header and the usual field, within the frame
-        const uint32_t nld = len >= HDR ? (r + min(len, XEND) + 15u) >> 4 : 0u;
-        if (nld) {
+        // the head window: the frame's first HW chunks (128 bytes from the header's
+        // 16-byte line), loaded once here.  They hold the header (parsed below), the
+        // usual isolated 2-byte field and the IPv4 options, and, for small datagrams
+        // (64-byte IMIX frames), the whole datagram: their sums are taken here and the
+        // rounds start behind the window (or are skipped).
+        constexpr uint32_t HDR = IPV6 ? 40u : 20u;
+        nlh = len >= HDR ? min(HW, (r + len + 15u) >> 4) : 0u;
+        {
             const uint8_t* a0 = p.base + a0off;
-            c0 = load_chunk(a0, 0);
-            if (nld > 1) c1 = load_chunk(a0, 1);
-            if (nld > 2) c2 = load_chunk(a0, 2);
-            if (nld > 3) c3 = load_chunk(a0, 3);
-            if (IPV6 && nld > 4) c4 = load_chunk(a0, 4);
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) hw[i] = i < nlh ? load_chunk(a0, i) : make_uint4(0, 0, 0, 0);
         }
-        const uint32_t ld_end = 16u * nld;            // register-held bytes from a0
+        const uint4 c0 = hw[0], c1 = hw[1], c2 = hw[2], c3 = hw[3], c4 = hw[4];
         const uint32_t avail = len;
         if constexpr (IPV4) {
             if (avail >= 20) {
@@ -1388,11 +1393,6 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                             if (tl < 8u) verdict |= V_MALFORMED;
                             else { l4_needed = true; xpos = r + hl + 2u; }
                         }
-                    }
-                    if (xpos != NONE && xpos + 2u <= ld_end) {
-                        xval = word_at(D, xpos);
-                        xpos = NONE;
-                        ext = span;
                     }
                 }
             }
@@ -1438,9 +1438,6 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                         }
                     }
                     if (parsed) {
-                        const uint32_t xh = r + net_len + xrel;   // field, header-relative
-                        const bool xfast = xrel != NONE && net_len == 40u && xh + 2u <= ld_end;
-                        if (xfast) { xval = word_at(D, xh); xrel = NONE; ext = tl; }
                         off += net_len;
                         fp = p.base + off;
                         r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
@@ -1456,12 +1453,41 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         }
     }
     const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
-    const uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
-    L.acc_all[lane] = 0;
-    L.acc_x[lane] = xval;
-    L.acc_opt[lane] = 0;
+    uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
+    if constexpr (MODE != 0) {
+        // sums over the head window: the region's chunks [0, k0) = window chunks
+        // [d, d + k0) (d: where the region's chunk grid starts in the window -- IPv6:
+        // behind the header); the rounds take region chunks [k0, nch).  A field
+        // straddling the cut moves the cut down a chunk (a field is summed whole on one
+        // side); options not inside the window (never, for IPv4) leave it all to the rounds.
+        const uint32_t d = (uint32_t)min((a0off - a0h) >> 4, (uint64_t)HW);
+        k0 = nlh > d ? min(nlh - d, nch) : 0u;
+        if (xpos != NONE && xpos < 16u * k0 && xpos + 2u > 16u * k0) k0 = xpos >> 4;
+        if (optend != 0u && optend > 16u * (d + k0)) k0 = 0;
+        const uint32_t P = 16u * (d + k0), rs = 16u * d + r;
+        const uint32_t re = min(rs + span, P);
+        const bool xin = xpos != NONE && 16u * d + xpos + 2u <= P;
+        const uint32_t xs = 16u * d + xpos;
+        const bool oin = optend != 0u && k0 != 0u;
+        const uint32_t sl = odd ? SEL_ODD : SEL_EVEN;
+#pragma unroll
+        for (uint32_t i = 0; i < HW; ++i) {
+            if (i >= d && i < d + k0) {
+                p_all += masked_chunk_sum<true>(hw[i], 16u * i, min(rs, re), re, sl);
+                if (xin) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
+                if (oin) p_opt += masked_chunk_sum<true>(hw[i], 16u * i, r + 20u, optend, sl);
+            }
+        }
+        if (xin) xpos = NONE;
+        else if (xpos != NONE) xpos -= 16u * k0;
+        if (oin) optend = 0;
+        nch -= k0;
+    }
+    L.acc_all[lane] = p_all;
+    L.acc_x[lane] = p_x;
+    L.acc_opt[lane] = p_opt;
     L.nch[lane] = nch;
-    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4));
+    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (k0 << 5));
     L.xo[lane] = make_uint2(xpos, optend);
     L.fin[lane] = make_uint4(verdict | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) | (proto << 8) |
                                  (tl << 16),
@@ -1527,6 +1553,48 @@ __global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(Flat
     if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, L, lane, f0);
 }
 
+// ---------------------------------------------------------------- IPv4 forwarding step
+//
+// pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) on a batch of datagrams that are
+// routed through this host: hdr->ttl = ttl - 1 (written back whatever follows);
+// ttl < 1 -> expired (pico_notify_ttl_expired, the frame is dropped, crc untouched);
+// else hdr->crc++ -- the reference's "HACK: increase crc to compensate decreased
+// TTL": a native (little-endian) uint16 increment of the stored big-endian field.
+// That is the incremental update of RFC 1141 (+0x0100 on the checksum for -1 on the
+// TTL byte) except where it carries out of the first byte, and it is kept exactly
+// so, bit-compatible with the reference.  One lane per datagram; the 4 bytes at
+// header offset 8..11 (ttl, proto, crc) are read and written, nothing else.
+struct FwdArgs {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint8_t* verdict;
+};
+
+__global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint4 d = *reinterpret_cast<const uint4*>(p.desc + i);
+    const uint64_t off = ((uint64_t)d.y << 32) | d.x;
+    uint32_t v = V_MALFORMED;
+    if (off <= p.base_len && d.z <= p.base_len - off && d.z >= 20u) {
+        uint8_t* h = p.base + off;
+        const uint8_t ttl = (uint8_t)(h[8] - 1u);
+        h[8] = ttl;
+        if (ttl < 1u) {
+            v = V_EXPIRED;
+        } else {
+            const uint32_t crc = (uint32_t)h[10] | ((uint32_t)h[11] << 8);
+            const uint32_t inc = (crc + 1u) & 0xFFFFu;
+            h[10] = (uint8_t)inc;
+            h[11] = (uint8_t)(inc >> 8);
+            v = V_ACCEPT;
+        }
+    }
+    if (p.verdict) p.verdict[i] = (uint8_t)v;
+}
+
 // ---------------------------------------------------------------- dispatch
 
 // (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
@@ -1557,6 +1625,15 @@ inline dim3 grid_for(uint32_t n, uint32_t fpw) {
 }  // namespace
 
 extern "C" {
+
+int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, uint8_t* verdict,
+                                  void* stream) {
+    if (n == 0) return (int)hipSuccess;
+    FwdArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, verdict};
+    const dim3 grid((unsigned)(((uint64_t)n + 255u) / 256u)), block(256);
+    hipLaunchKernelGGL(ipv4_forward_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
+}
 
 // Launchers used by the C host layer (picotcp_amd/csrc/pico_csum.c).  They
 // validate the launch shape, enqueue, and return the hipError_t as int.
