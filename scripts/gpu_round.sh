@@ -12,7 +12,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1
 echo "pytest ok"
 timeout -k 10 400 python bench.py > $O/bench_c1_$TAG.json 2> $O/bench_c1_$TAG.err
 echo "bench c1 ok"
-for c in c2 c2v6 c3 c3_64k; do
+for c in c2 c2tx c2v6 c3 c3_64k c3_frag; do
   timeout -k 10 300 python bench.py --config $c --steps 100 --warmup 10 --no-cpu --no-e2e > $O/bench_${c}_$TAG.json 2> $O/bench_${c}_$TAG.err
 done
 echo "bench configs ok"

@@ -19,7 +19,7 @@ for cfg in ("c1", "c2", "c2v6"):
     d = os.path.join(src, f"prof_{cfg}_{tag}")
     if os.path.isdir(d):
         shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{cfg}_kernel_stats.csv"))
-for cfg in ("c1", "c2", "c2v6", "c3", "c3_64k"):
+for cfg in ("c1", "c2", "c2tx", "c2v6", "c3", "c3_64k", "c3_frag"):
     f = os.path.join(src, f"bench_{cfg}_{tag}.json")
     if os.path.exists(f):
         shutil.copy(f, os.path.join(dst, f"bench_{cfg}.json"))
