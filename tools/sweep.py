@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", nargs="*", default=[])
+    ap.add_argument("--rotate", type=int, default=12, help="descriptor configs: batch copies rotated "
+                    "(12 x ~93 MB >= 1 GiB: the Infinity Cache cannot serve repeats)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     UNI = {"c1": (262144, 1500, 1500), "c3": (262144, 9000, 9000), "c3_64k": (16384, 65536, 65536),
@@ -46,7 +48,7 @@ def main():
         # uniform frames fed as a descriptor batch (ablation: descriptor kernels vs uniform
         # ones): c1d = 256K x 1500 B, u<LEN>d = 256K x LEN bytes
         n, ln = 262144, 1500 if a.config == "c1d" else int(a.config[1:-1])
-        rot = 3
+        rot = max(3, -(-(1 << 30) // (n * ln)))
         bufs = [torch.randint(0, 256, (n * ln,), dtype=torch.uint8, device=dev) for _ in range(rot)]
         d_desc = batch.desc_to_device(batch.make_desc(np.arange(n, dtype=np.uint64) * ln, np.full(n, ln)), dev)
         outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
@@ -57,7 +59,7 @@ def main():
     elif a.config == "c2v6":
         n = 262144
         lens = (synth.imix_lengths(n, 3) + 20).astype(np.uint32)
-        rot = 3
+        rot = a.rotate
         sets = []
         for r in range(rot):
             buf, net, avail, seeds = synth.ipv6_batch(lens, seed=10 + r, proto=6, eth=True)
@@ -73,7 +75,7 @@ def main():
     elif a.config in ("c2raw", "c2", "c2tx", "c2txnw"):
         n = 262144
         lens = synth.imix_lengths(n, 3)
-        rot = 3
+        rot = a.rotate
         sets = []
         for r in range(rot):
             buf, net, avail = synth.ipv4_batch(lens, seed=10 + r, proto=6, eth=True)
