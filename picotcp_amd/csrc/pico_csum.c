@@ -225,6 +225,15 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
     return s;
 }
 
+/* Ablation bits for the sorted-rounds kernel (PICO_CSUM_ABLATE, measurement only):
+ * 1 = skip the rounds, 2 = skip the head-window loads.  Passed in flags bits 8+, which
+ * the public API rejects. */
+static uint32_t ablate_flags(void)
+{
+    const char *e = getenv("PICO_CSUM_ABLATE");
+    return e ? ((uint32_t)strtoul(e, NULL, 0) & 0xFFu) << 8 : 0u;
+}
+
 static int g_dev_state; /* 0 unknown, 1 ok, -1 none */
 static uint32_t g_cus = 256; /* compute units of device 0 (MI355X: 256) */
 
@@ -285,7 +294,8 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
                                                             d_bad, 0, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
+                                                     d_out, d_bad,
                                                      NULL, NULL, NULL, s.CPL, s.nt, s.fpw, s.U == 1, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
@@ -346,7 +356,8 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 3)
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
+                                                     NULL,
                                                      d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
                                                      stream),
                              "pico_ipv4_checksum_batch_dev");
@@ -382,7 +393,8 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 3)
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
     if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
+        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
+                                                     NULL, NULL,
                                                      d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1, stream),
                              "pico_ipv6_checksum_batch_dev");
     if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */

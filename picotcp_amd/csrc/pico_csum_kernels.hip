@@ -113,10 +113,16 @@ __device__ __forceinline__ uint32_t finalize(uint32_t s) {
     return ((c >> 8) | (c << 8)) & 0xFFFFu;
 }
 
-// The 16-bit checksum word as it sits in memory: hdr->crc = short_be(ret).
+// The 16-bit checksum word as it sits in memory: hdr->crc = short_be(ret).  One 16-bit
+// store when the field is 2-byte aligned (every IPv4 / TCP / UDP crc behind a 2-aligned
+// header), two byte stores otherwise.
 __device__ __forceinline__ void store_crc(uint8_t* p, uint32_t ret) {
-    p[0] = (uint8_t)(ret >> 8);
-    p[1] = (uint8_t)(ret & 0xFFu);
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
+        *reinterpret_cast<uint16_t*>(p) = (uint16_t)(((ret >> 8) & 0xFFu) | ((ret & 0xFFu) << 8));
+    } else {
+        p[0] = (uint8_t)(ret >> 8);
+        p[1] = (uint8_t)(ret & 0xFFu);
+    }
 }
 
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* a0, uint32_t k) {
@@ -1145,6 +1151,20 @@ struct SortedWaveLds {
                            //  hl | ip crc << 16, pseudo sum (RAW: seed), header sum}
 };
 
+// A wave's LDS.  Fused modes: the phase-1 head-window staging (64 frames x HW chunks,
+// rows padded to HW+1) shares the space with the state it is parsed into -- 9 KiB a wave,
+// 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
+template <bool STAGE>
+union SortedWaveSmem {
+    SortedWaveLds s;
+    uint4 stage[64 * (HW + 1)];
+};
+template <>
+union SortedWaveSmem<false> {
+    SortedWaveLds s;
+    uint4 stage[1];
+};
+
 // One round: group g sums the frame at position pos + g of the class order.
 template <int G, int CPL, bool PERM, bool NT, bool XO>
 __device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L, uint32_t pos, uint32_t m) {
@@ -1308,7 +1328,8 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
 template <int MODE, bool NT, int CPL, bool SMALL>
-__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t f0) {
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, uint32_t lane,
+                                             uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = MODE != 0 && (p.flags & 2u) != 0;
@@ -1343,11 +1364,55 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         // (64-byte IMIX frames), the whole datagram: their sums are taken here and the
         // rounds start behind the window (or are skipped).
         constexpr uint32_t HDR = IPV6 ? 40u : 20u;
-        nlh = len >= HDR ? min(HW, (r + len + 15u) >> 4) : 0u;
+        nlh = len >= HDR && !(p.flags & 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;   // 0x200: ablation
         {
+            // Buffer loads through a window over the batch (from base's 16-byte line to
+            // base_len rounded up -- the bytes load_chunk may touch -- at most 2 GiB, from
+            // 1 GiB below the wave's first frame): all HW slots issue back to back and
+            // slots past the frame read zeros.  (`i < nlh ? load : 0` compiled to branched
+            // flat loads with a vmcnt(0) behind the second: two dependent HBM round trips
+            // per wave.)  A frame outside the window (a wave spanning > 1 GiB of a batch
+            // over 2 GiB) is loaded in a second, branched pass.
             const uint8_t* a0 = p.base + a0off;
+            const uint64_t a0a = reinterpret_cast<uintptr_t>(a0);
+            const uint64_t wb = reinterpret_cast<uintptr_t>(p.base) & ~(uint64_t)15;
+            const uint64_t wn = (reinterpret_cast<uintptr_t>(p.base) + p.base_len + 15u - wb) & ~(uint64_t)15;
+            const uint64_t act = __builtin_amdgcn_ballot_w64(nlh != 0);
+            const int first = act ? __builtin_ffsll((long long)act) - 1 : 0;
+            const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(a0a >> 32), first) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0a, first);
+            const uint64_t lo = anchor >= wb + (1ull << 30) ? anchor - (1ull << 30) : wb;
+            const uint64_t wsz = min(wn - min(lo - wb, wn), (uint64_t)0x7FFFFFF0u);
+            const bool inside = a0a >= lo && a0a - lo + 16u * nlh <= wsz;
+            const Window w = make_window(lo, (uint32_t)wsz);
+            const uint32_t v0 = (uint32_t)(a0a - lo);
+            const uint32_t nin = inside ? nlh : 0u;
+            // Transposed: load k covers frames FPL*k .. FPL*k+FPL-1 with HW lanes each, so one
+            // instruction reads FPL whole 128-byte windows (a lane per frame touched 64
+            // lines per instruction and re-fetched each line for every chunk: L1 thrash).
+            // The chunks meet their frame's lane through LDS (row stride HW+1: no conflicts).
+            constexpr uint32_t FPL = 64u / HW;
+            const uint32_t gi = lane / HW, ci = lane % HW;
+            uint4 t[HW];
 #pragma unroll
-            for (uint32_t i = 0; i < HW; ++i) hw[i] = i < nlh ? load_chunk(a0, i) : make_uint4(0, 0, 0, 0);
+            for (uint32_t k = 0; k < HW; ++k) {
+                const uint32_t g = FPL * k + gi;
+                const uint32_t gv0 = (uint32_t)__shfl((int)v0, (int)g);
+                const uint32_t gn = (uint32_t)__shfl((int)nin, (int)g);
+                t[k] = load_win<false>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < HW; ++k) stage[(FPL * k + gi) * (HW + 1) + ci] = t[k];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * (HW + 1) + i];
+            // the staging rows alias the wave's SortedWaveLds (written at the end of phase 1)
+            asm volatile("" ::: "memory");
+            if (__builtin_amdgcn_ballot_w64(!inside && nlh != 0)) {
+#pragma unroll
+                for (uint32_t i = 0; i < HW; ++i)
+                    if (!inside && i < nlh) hw[i] = load_chunk(a0, i);
+            }
         }
         const uint4 c0 = hw[0], c1 = hw[1], c2 = hw[2], c3 = hw[3], c4 = hw[4];
         const uint32_t avail = len;
@@ -1525,7 +1590,9 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
     // ---- 3. rounds over the sorted frames
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
-    if (m) {
+    // ablation only (PICO_CSUM_ABLATE): flags bit 8 skips the rounds (times phases 1, 2, 4);
+    // bit 9 skips the head-window loads (then nothing parses: descriptors + stores alone)
+    if (m && !(p.flags & 0x100u)) {
         if (any_odd) {
             if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
             else sorted_rounds<CPL, true, NT, false, SMALL>(ra, L, e, m);
@@ -1545,12 +1612,12 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
 template <int MODE, bool NT, int CPL, bool SMALL = false>
-__global__ __launch_bounds__(256, CPL == 8 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
-    __shared__ SortedWaveLds lds_all[4];
+__global__ __launch_bounds__(256, CPL == 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<MODE != 0> lds_all[4];
     const uint32_t lane = threadIdx.x & 63u;
-    SortedWaveLds& L = lds_all[threadIdx.x >> 6];
+    SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
-    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, L, lane, f0);
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
 }
 
 // ---------------------------------------------------------------- IPv4 forwarding step

@@ -90,10 +90,12 @@ def main():
                 batch.checksum_batch(b, d, n, out=outs[i % rot])
         else:
             fl = {"c2": 0, "c2tx": batch.F_TX | batch.F_WRITE, "c2txnw": batch.F_TX}[a.config]
+            o3 = [(outs[r], torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.uint8, device=dev))
+                  for r in range(rot)]
 
             def launch(i):
                 b, d = sets[i % rot]
-                batch.ipv4_checksum_batch(b, d, n, flags=fl)
+                batch.ipv4_checksum_batch(b, d, n, flags=fl, out=o3[i % rot])
         algo = int(lens.sum()) + 16 * n + (2 if a.config == "c2raw" else 5) * n
     else:
         raise SystemExit("unknown config")
