@@ -1313,7 +1313,7 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
             }
             if (verdict == 0) verdict = V_ACCEPT;
         }
-        if (tx && (p.flags & 1u) && verdict == V_ACCEPT) {
+        if (tx && (p.flags & 0x401u) == 1u && verdict == V_ACCEPT) {   // 0x400: ablation
             store_crc(fp + 10, net);
             if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
             else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
@@ -1353,6 +1353,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     const uint64_t a0h = a0off;                  // the head window's first chunk (fused modes)
     uint4 hw[HW];
     uint32_t nlh = 0;                            // head-window chunks loaded
+    bool staged = false;                         // the window also sits in this lane's LDS row
     uint32_t k0 = 0, p_all = 0, p_x = 0, p_opt = 0;
     if constexpr (MODE == 0) {
         span = ext = len;
@@ -1384,6 +1385,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
             const uint64_t lo = anchor >= wb + (1ull << 30) ? anchor - (1ull << 30) : wb;
             const uint64_t wsz = min(wn - min(lo - wb, wn), (uint64_t)0x7FFFFFF0u);
             const bool inside = a0a >= lo && a0a - lo + 16u * nlh <= wsz;
+            staged = inside;
             const Window w = make_window(lo, (uint32_t)wsz);
             const uint32_t v0 = (uint32_t)(a0a - lo);
             const uint32_t nin = inside ? nlh : 0u;
@@ -1539,10 +1541,18 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         for (uint32_t i = 0; i < HW; ++i) {
             if (i >= d && i < d + k0) {
                 p_all += masked_chunk_sum<true>(hw[i], 16u * i, min(rs, re), re, sl);
-                if (xin) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
+                if (xin && !staged) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
                 if (oin) p_opt += masked_chunk_sum<true>(hw[i], 16u * i, r + 20u, optend, sl);
             }
         }
+        // The isolated field is one word of the region's pairing: whatever the start's
+        // parity, its share is byte[xs] | byte[xs+1] << 8 in the accumulators' (byte-
+        // swapped) domain -- two LDS byte reads instead of HW masked sums.
+        if (xin && staged) {
+            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * (HW + 1));
+            p_x = (uint32_t)row[xs] | ((uint32_t)row[xs + 1u] << 8);
+        }
+        asm volatile("" ::: "memory");   // stage rows are read before the state below overwrites them
         if (xin) xpos = NONE;
         else if (xpos != NONE) xpos -= 16u * k0;
         if (oin) optend = 0;
@@ -1591,7 +1601,8 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     // ---- 3. rounds over the sorted frames
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
     // ablation only (PICO_CSUM_ABLATE): flags bit 8 skips the rounds (times phases 1, 2, 4);
-    // bit 9 skips the head-window loads (then nothing parses: descriptors + stores alone)
+    // bit 9 skips the head-window loads (then nothing parses: descriptors + stores alone);
+    // bit 10 skips the IPv4 TX in-place crc writes
     if (m && !(p.flags & 0x100u)) {
         if (any_odd) {
             if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
