@@ -1152,12 +1152,12 @@ struct SortedWaveLds {
 };
 
 // A wave's LDS.  Fused modes: the phase-1 head-window staging (64 frames x HW chunks,
-// rows padded to HW+1) shares the space with the state it is parsed into -- 9 KiB a wave,
-// 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
+// chunk slots XOR-swizzled) shares the space with the state it is parsed into -- 8 KiB a
+// wave, 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
 template <bool STAGE>
 union SortedWaveSmem {
     SortedWaveLds s;
-    uint4 stage[64 * (HW + 1)];
+    uint4 stage[64 * HW];
 };
 template <>
 union SortedWaveSmem<false> {
@@ -1392,7 +1392,8 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
             // Transposed: load k covers frames FPL*k .. FPL*k+FPL-1 with HW lanes each, so one
             // instruction reads FPL whole 128-byte windows (a lane per frame touched 64
             // lines per instruction and re-fetched each line for every chunk: L1 thrash).
-            // The chunks meet their frame's lane through LDS (row stride HW+1: no conflicts).
+            // The chunks meet their frame's lane through LDS (row g holds chunk c in slot
+            // c ^ (g & 7): 8 lanes reading chunk i of 8 rows hit 8 different bank groups).
             constexpr uint32_t FPL = 64u / HW;
             const uint32_t gi = lane / HW, ci = lane % HW;
             uint4 t[HW];
@@ -1404,10 +1405,13 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                 t[k] = load_win<false>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
             }
 #pragma unroll
-            for (uint32_t k = 0; k < HW; ++k) stage[(FPL * k + gi) * (HW + 1) + ci] = t[k];
+            for (uint32_t k = 0; k < HW; ++k) {
+                const uint32_t g = FPL * k + gi;
+                stage[g * HW + (ci ^ (g & (HW - 1)))] = t[k];
+            }
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * (HW + 1) + i];
+            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * HW + (i ^ (lane & (HW - 1)))];
             // the staging rows alias the wave's SortedWaveLds (written at the end of phase 1)
             asm volatile("" ::: "memory");
             if (__builtin_amdgcn_ballot_w64(!inside && nlh != 0)) {
@@ -1549,8 +1553,9 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         // parity, its share is byte[xs] | byte[xs+1] << 8 in the accumulators' (byte-
         // swapped) domain -- two LDS byte reads instead of HW masked sums.
         if (xin && staged) {
-            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * (HW + 1));
-            p_x = (uint32_t)row[xs] | ((uint32_t)row[xs + 1u] << 8);
+            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
+            const uint32_t sw = (lane & (HW - 1)) << 4, x1 = xs + 1u;   // chunk slots are XOR-swizzled
+            p_x = (uint32_t)row[xs ^ sw] | ((uint32_t)row[x1 ^ sw] << 8);
         }
         asm volatile("" ::: "memory");   // stage rows are read before the state below overwrites them
         if (xin) xpos = NONE;
