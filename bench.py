@@ -28,6 +28,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -76,7 +78,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     p.add_argument("--rotate", type=int, default=0, help="rotating batch copies (0 = enough for >= 1 GiB)")
-    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU-baseline wall per leg")
+    p.add_argument("--cpu-seconds", type=float, default=4.0, help="target CPU-baseline wall per leg")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
@@ -122,30 +124,57 @@ def make_c2v6(n, device, seed, keep_host=True):
     return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return os.uname().machine
+
+
+def cpu_threads() -> tuple[int, int]:
+    """(threads used, usable cores).  The GPU box gives one GPU's job a 16-core share of
+    the host (OMP_NUM_THREADS=16 there; sched_getaffinity shows the whole machine), so
+    the multi-thread leg runs on that share, capped at the usable cores."""
+    cores = len(os.sched_getaffinity(0))
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))), cores
+
+
 def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
-    """The reference's pico_checksum (oracle/_ref, -O3 = reference PERF=1) over a bounded
-    sample of the same frames: 1 thread and all usable host cores (<= 16 on the box)."""
+    """The reference's pico_checksum (oracle/_ref: stack/pico_frame.c built -O3 = the
+    reference's PERF=1, and -Os = its release default) over a bounded sample of the same
+    frames, on 1 thread and on the job's host-core share."""
     from oracle import oracle as O
     kind = "reference" if O.ref_available() else "port"
     n = sample.size // ln
-    cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    threads, cores = cpu_threads()
     res = {}
-    for t in (1, threads):
-        secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind)   # first pass: page-in / warm
+    legs = [(1, False), (threads, False)]
+    if kind == "reference" and O.ref_available(os_flags=True):
+        legs += [(1, True), (threads, True)]
+    for t, osf in legs:
+        secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind, os_flags=osf)   # page-in / warm
         reps = max(1, int(target_s / max(secs, 1e-3)))
         tot = 0.0
         for _ in range(reps):
-            secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind)
+            secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind, os_flags=osf)
             tot += secs
-        res[t] = (n * ln * reps / tot / GIB, reps)
-    return {
-        "value": round(res[threads][0], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-        "single_core_value": round(res[1][0], 3),
+        res[(t, osf)] = (n * ln * reps / tot / GIB, reps)
+    out = {
+        "value": round(res[(threads, False)][0], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "single_core_value": round(res[(1, False)][0], 3),
         "sample": f"{n} x {ln} B frames ({n * ln / 2**20:.0f} MiB, DRAM-resident), reference stack/pico_frame.c "
-                  f"pico_checksum built -O3, pthreads over contiguous frame ranges; {res[threads][1]} passes on "
-                  f"{threads} threads, {res[1][1]} on 1 thread; host {os.uname().machine}, {cores} usable cores",
+                  f"pico_checksum built -O3 (PERF=1), pthreads over contiguous frame ranges; "
+                  f"{res[(threads, False)][1]} passes on {threads} threads, {res[(1, False)][1]} on 1 thread",
+        "cpu_model": cpu_model(), "usable_cores": cores,
     }
+    if (1, True) in res:
+        out["Os_value"] = round(res[(threads, True)][0], 3)
+        out["Os_single_core_value"] = round(res[(1, True)][0], 3)
+    return out
 
 
 def cpu_baseline_fused(host, ipv6: bool, tx: bool, target_s: float):
@@ -200,8 +229,46 @@ def load_traffic(config: str):
         return None
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> None:
+    """`--gpus N` is honoured, never silently dropped.  Under torch.distributed.run
+    (WORLD_SIZE set) it must equal WORLD_SIZE.  Without a launcher and N > 1, this
+    process starts the N ranks itself (one per GPU, 127.0.0.1 rendezvous) as a child
+    `torch.distributed.run`, before anything here touches the GPU, and exits with its
+    status.  torch.cuda.device_count() does not initialise the device."""
+    same_dev = os.environ.get("PICO_BENCH_SAME_DEVICE") == "1"
+    if a.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {a.gpus})")
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws}: refusing to measure a different GPU count")
+        return
+    if a.gpus == 1:
+        return
+    have = torch.cuda.device_count()
+    if have < a.gpus and not same_dev:
+        sys.exit(f"bench.py: --gpus {a.gpus} but only {have} HIP device(s) visible")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
     a = parse()
+    launch_ranks(a)
+    if os.environ.get("PICO_BENCH_DRY") == "1":      # launcher test (tests/test_bench_launch.py): no GPU use
+        print(json.dumps({"rank": int(os.environ.get("RANK", 0)), "world": int(os.environ.get("WORLD_SIZE", 1)),
+                          "gpus": a.gpus}), flush=True)
+        return
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -99,8 +99,13 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
 
 /* ---------------------------------------------------------------- layer 2 */
 
-/* Every device batch takes the size of the buffer behind d_base (base_len):
- * no byte outside [d_base, d_base + base_len) is ever read or written.
+/* Every device batch takes the size of the buffer behind d_base (base_len).
+ * Nothing outside [d_base, d_base + base_len) is ever written, and no byte outside it
+ * contributes to a result.  The kernels load whole 16-byte-aligned blocks, so the
+ * 16-byte-aligned blocks that overlap [d_base, d_base + base_len) may be read in full
+ * (up to 15 bytes before d_base and after its end; such a block never crosses a page,
+ * so this cannot fault).  A caller that writes those neighbouring bytes from another
+ * stream concurrently gets correct results all the same: they are masked out.
  *
  * Batch of pico_checksum / pico_dualbuffer_checksum calls:
  *   d_out[i] = finalize(adder(desc[i].seed, d_base + desc[i].off, desc[i].len))
@@ -197,7 +202,7 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
  * flat work-list kernel, group = 2 the sorted-rounds kernel (descriptor batches
  * only; there unroll = the narrowest round width: 0 auto, 1 = one frame per lane
  * for frames of <= 8 chunks (cpl 8), 4), group = 3 the per-wave adaptive kernel.
- * Process-wide. */
+ * Applies to launches from the calling thread only (thread-local). */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);
 

@@ -62,6 +62,18 @@ def _require_device(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name} must be a HIP device tensor (the batched path is GPU-only)")
 
 
+def _check_out(out: torch.Tensor, n: int, name: str, device, itemsize: int = 2) -> None:
+    """A caller-supplied result tensor: on the batch's device, contiguous, the right
+    element size and at least n elements (the kernels write n results through its pointer)."""
+    _require_device(out, name)
+    if out.device != device:
+        raise ValueError(f"{name} is on {out.device}, the batch on {device}")
+    if not out.is_contiguous() or out.element_size() != itemsize:
+        raise ValueError(f"{name} must be a contiguous tensor of {itemsize}-byte elements")
+    if out.numel() < n:
+        raise ValueError(f"{name} has {out.numel()} elements, the batch {n}")
+
+
 def checksum_uniform(base: torch.Tensor, stride: int, length: int, n: int, seed: int = 0,
                      out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """out[i] = pico_checksum(base + i*stride, length) (+ seed as pico_dualbuffer_checksum's
@@ -71,6 +83,7 @@ def checksum_uniform(base: torch.Tensor, stride: int, length: int, n: int, seed:
         raise ValueError("frames exceed the base tensor")
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=base.device)
+    _check_out(out, n, "out", base.device)
     lib = _lib.load()
     _lib.check("pico_checksum_batch_uniform_dev",
                lib.pico_checksum_batch_uniform_dev(_ptr(base), base.numel(), stride, length, n, seed & 0xFFFFFFFF,
@@ -89,6 +102,9 @@ def checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, crc_off: int 
         raise ValueError("descriptor tensor shorter than n entries")
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=base.device)
+    _check_out(out, n, "out", base.device)
+    if bad is not None:
+        _check_out(bad, 1, "bad", base.device, itemsize=4)
     lib = _lib.load()
     _lib.check("pico_checksum_batch_dev",
                lib.pico_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, crc_off, flags, _ptr(out),
@@ -109,10 +125,8 @@ def ipv4_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
         out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                torch.empty(n, dtype=torch.uint8, device=dev))
     out_net, out_l4, verdict = out
-    for t, nm in ((out_net, "out_net"), (out_l4, "out_transport"), (verdict, "verdict")):
-        _require_device(t, nm)
-        if t.numel() < n:
-            raise ValueError(f"{nm} shorter than n")
+    for t, nm, sz in ((out_net, "out_net", 2), (out_l4, "out_transport", 2), (verdict, "verdict", 1)):
+        _check_out(t, n, nm, dev, sz)
     lib = _lib.load()
     _lib.check("pico_ipv4_checksum_batch_dev",
                lib.pico_ipv4_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_net),
@@ -133,10 +147,8 @@ def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     if out is None:
         out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.uint8, device=dev))
     out_l4, verdict = out
-    for t, nm in ((out_l4, "out_transport"), (verdict, "verdict")):
-        _require_device(t, nm)
-        if t.numel() < n:
-            raise ValueError(f"{nm} shorter than n")
+    for t, nm, sz in ((out_l4, "out_transport", 2), (verdict, "verdict", 1)):
+        _check_out(t, n, nm, dev, sz)
     lib = _lib.load()
     _lib.check("pico_ipv6_checksum_batch_dev",
                lib.pico_ipv6_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_l4),
@@ -155,6 +167,7 @@ def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: 
         raise ValueError("descriptor tensor shorter than n entries")
     if verdict is None:
         verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
+    _check_out(verdict, n, "verdict", base.device, 1)
     lib = _lib.load()
     _lib.check("pico_ipv4_forward_batch_dev",
                lib.pico_ipv4_forward_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, _ptr(verdict),
@@ -190,12 +203,24 @@ class HostBatch:
                          seed: int = 0, out: np.ndarray | None = None) -> np.ndarray:
         if out is None:
             out = np.empty(n, dtype=np.uint16)
+        if not (isinstance(out, np.ndarray) and out.dtype == np.uint16 and out.flags.c_contiguous
+                and out.size >= n):
+            raise ValueError("out must be a contiguous uint16 array of at least n elements")
+        need = (n - 1) * stride + length if n else 0
         if isinstance(frames, torch.Tensor):
             if frames.is_cuda:
                 raise ValueError("HostBatch takes host memory")
+            if not frames.is_contiguous():
+                raise ValueError("frames must be contiguous")
+            nbytes = frames.numel() * frames.element_size()
             src = frames.data_ptr()
         else:
+            if not frames.flags.c_contiguous:
+                raise ValueError("frames must be contiguous")
+            nbytes = frames.nbytes
             src = frames.ctypes.data
+        if nbytes < need:
+            raise ValueError(f"frames hold {nbytes} bytes, the batch spans {need}")
         _lib.check("pico_checksum_batch_uniform_host",
                    self._lib.pico_checksum_batch_uniform_host(self._ctx, ctypes.c_void_p(src), stride, length, n,
                                                               seed & 0xFFFFFFFF,

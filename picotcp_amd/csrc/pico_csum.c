@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdarg.h>
+#include <pthread.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -125,7 +126,9 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
 
 /* ------------------------------------------------------------------ layer 2 */
 
-static uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
+/* Launch-shape override: per calling thread (a test or sweep setting it cannot race a
+ * launch from another thread). */
+static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline)
@@ -234,22 +237,43 @@ static uint32_t ablate_flags(void)
     return e ? ((uint32_t)strtoul(e, NULL, 0) & 0xFFu) << 8 : 0u;
 }
 
-static int g_dev_state; /* 0 unknown, 1 ok, -1 none */
-static uint32_t g_cus = 256; /* compute units of device 0 (MI355X: 256) */
+/* Device discovery runs once per process (pthread_once); compute-unit counts are read
+ * per device, for the device current on the calling thread at launch. */
+#define MAX_DEVS 64
+static pthread_once_t g_dev_once = PTHREAD_ONCE_INIT;
+static int g_dev_count;                     /* 0: no usable HIP device */
+static uint32_t g_dev_cus[MAX_DEVS];        /* compute units per device (MI355X: 256) */
+
+static void probe_devices(void)
+{
+    int count = 0, d;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return;
+    if (count > MAX_DEVS)
+        count = MAX_DEVS;
+    for (d = 0; d < count; d++) {
+        int cus = 0;
+        g_dev_cus[d] = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess &&
+                       cus > 0 ? (uint32_t)cus : 256u;
+    }
+    g_dev_count = count;
+}
 
 static int need_device(void)
 {
-    int count = 0, cus = 0;
-    if (g_dev_state == 1)
-        return 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
-        g_dev_state = -1;
+    pthread_once(&g_dev_once, probe_devices);
+    if (g_dev_count <= 0)
         return fail(PICO_CSUM_ENODEV, "no HIP device: the batched checksum path runs only on the GPU");
-    }
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && cus > 0)
-        g_cus = (uint32_t)cus;
-    g_dev_state = 1;
     return 0;
+}
+
+/* compute units of the calling thread's current device */
+static uint32_t cur_cus(void)
+{
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= g_dev_count)
+        return 256u;
+    return g_dev_cus[d];
 }
 
 static int launch_status(int herr, const char *what)
@@ -301,7 +325,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
                                                    NULL, NULL, NULL, s.CPL, s.nt, s.fpw,
-                                                   s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                                   s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
                              "pico_checksum_batch_dev");
     return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
                                               d_bad, s.G, s.CPL, s.U, s.nt, s.fpw, 0, stream),
@@ -364,7 +388,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
                                                    d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                                   s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                                   s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
                              "pico_ipv4_checksum_batch_dev");
     return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
                                                d_verdict, s.G, s.CPL, s.fpw, stream),
@@ -405,7 +429,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     }
     return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
                                                d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                               s.U ? s.U * g_cus : 0xFFFFFFFFu, stream),
+                                               s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
                          "pico_ipv6_checksum_batch_dev");
 }
 
