@@ -96,6 +96,13 @@ uint32_t pico_checksum_partial(uint32_t sum, const void *buf, uint32_t len);
  * build it (pico_tcp.c:428-443, pico_udp.c:42-57).  src/dst as stored in
  * struct pico_ip4 (network byte order). */
 uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t proto, uint16_t transport_len);
+/* Accumulator value of the 40-byte struct pico_ipv6_pseudo_hdr (modules/pico_ipv6.h:46-53:
+ * src, dst, long_be(len), 3 zero bytes, nxthdr) as pico_tcp_checksum_ipv6 /
+ * pico_udp_checksum_ipv6 / pico_icmp6_checksum / pico_mld_checksum build it
+ * (pico_tcp.c:449-475, pico_udp.c:63-92, pico_icmp6.c:38-55, pico_mld.c:421-437).
+ * A raw batch seeded with it serves the MLD router-alert variant (transport + 8,
+ * length - 8) and TX datagrams whose addresses come from the socket. */
+uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t nxthdr, uint32_t transport_len);
 
 /* ---------------------------------------------------------------- layer 2 */
 

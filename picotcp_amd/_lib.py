@@ -19,6 +19,7 @@ EXPORTED = (
     "pico_dualbuffer_checksum",
     "pico_checksum_partial",
     "pico_ipv4_pseudo_partial",
+    "pico_ipv6_pseudo_partial",
     "pico_checksum_batch_dev",
     "pico_checksum_batch_uniform_dev",
     "pico_ipv4_checksum_batch_dev",
@@ -72,6 +73,7 @@ def load() -> ctypes.CDLL:
     sig("pico_dualbuffer_checksum", u16, vp, u32, vp, u32)
     sig("pico_checksum_partial", u32, u32, vp, u32)
     sig("pico_ipv4_pseudo_partial", u32, u32, u32, ctypes.c_uint8, ctypes.c_uint16)
+    sig("pico_ipv6_pseudo_partial", u32, vp, vp, ctypes.c_uint8, u32)
     sig("pico_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, i32, u32, vp, vp, vp)
     sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u64, u32, u32, u32, vp, vp)
     sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp)

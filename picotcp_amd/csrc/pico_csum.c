@@ -124,6 +124,17 @@ uint32_t pico_ipv4_pseudo_partial(uint32_t src_addr, uint32_t dst_addr, uint8_t 
     return s;
 }
 
+uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t nxthdr, uint32_t transport_len)
+{
+    /* struct pico_ipv6_pseudo_hdr bytes: src(16) dst(16) len_be(4) zero(3) nxthdr as LE words */
+    uint32_t s = (uint32_t)(word_sum((const uint8_t *)src16, 16) + word_sum((const uint8_t *)dst16, 16));
+    uint32_t be = ((transport_len & 0xFFu) << 24) | ((transport_len & 0xFF00u) << 8) |
+                  ((transport_len >> 8) & 0xFF00u) | (transport_len >> 24);
+    s += (be & 0xFFFFu) + (be >> 16);
+    s += (uint32_t)nxthdr << 8;
+    return s;
+}
+
 /* ------------------------------------------------------------------ layer 2 */
 
 /* Launch-shape override: per calling thread (a test or sweep setting it cannot race a

@@ -65,3 +65,9 @@ def ipv6_desc(c: dict) -> np.ndarray:
     d = ipv4_desc(c["net"], c["avail"])
     d["seed"] = c["seed"]
     return d
+
+
+def ref_callers() -> dict:
+    """Transport checksums from the reference's own compiled callers (make_ref_callers.py)."""
+    z = np.load(os.path.join(GOLDEN, "ref_callers.npz"))
+    return {k: z[k] for k in z.files}
