@@ -80,6 +80,11 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_L4_BAD    4u  /* pico_transport_crc_check would discard (pico_socket.c:1929,1953) */
 #define PICO_CSUM_V_MALFORMED 8u  /* infeasible length (pico_ipv4.c:402-405) or a region past the buffer */
 #define PICO_CSUM_V_EXPIRED  16u  /* forwarding: TTL reached 0 (pico_ipv4.c:1549-1552) */
+#define PICO_CSUM_V_DROP_L2  32u  /* Ethernet batch: discarded by the link layer -- foreign destination MAC
+                                     (pico_ethernet.c:221-231), unknown ethertype (:201-202) or an IP
+                                     version that does not match it (:143-150, :162-176) */
+#define PICO_CSUM_V_ARP      64u  /* Ethernet batch: ARP frame, handed to pico_arp_receive (:186-187) */
+#define PICO_CSUM_V_IPV6    128u  /* Ethernet batch: set on every IPv6 frame (ethertype 0x86DD) */
 
 /* ---------------------------------------------------------------- layer 1 */
 
@@ -168,6 +173,22 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
 int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream);
+
+/* Ethernet front end of the fused RX verify, one frame per descriptor,
+ * IPv4, IPv6, ARP and other ethertypes mixed in ONE launch: desc.off -> the Ethernet header
+ * (f->datalink_hdr), desc.len = frame bytes (f->buffer_len), desc.seed = the IPv6 net_len |
+ * proto << 16 as for pico_ipv6_checksum_batch_dev (IPv6 frames; 0 otherwise).
+ * Per frame, as pico_ethernet_receive / pico_eth_receive (modules/pico_ethernet.c:180-235):
+ *   RX destination filter when mac != NULL (host pointer to the device's 6-byte address,
+ *   f->dev->eth->mac): own address, 01:00:5e / 33:33 multicast or broadcast, else V_DROP_L2;
+ *   ethertype 0x0806 -> V_ARP (no checksum); 0x0800 -> the IPv4 batch semantics on
+ *   (off + 14, len - 14) if the version nibble is 4; 0x86DD -> the IPv6 batch semantics if
+ *   it is 6, verdict | V_IPV6; anything else V_DROP_L2.  Frames shorter than 15 bytes are
+ *   MALFORMED.  d_out_net is 0 for every non-IPv4 frame.  TX (F_TX, no MAC filter) computes
+ *   and, with F_WRITE, stores the IPv4 / IPv6 checksums of the frames the stack built. */
+int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
+                                uint8_t *d_verdict, void *stream);
 
 /* Forwarding step of pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) for a batch
  * of IPv4 datagrams routed through this host (desc.off -> IPv4 header, desc.len =

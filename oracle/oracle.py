@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_ipv6_pseudo_sum.argtypes = [_vp, _vp, ctypes.c_uint8, _u32]
         L.oracle_batch_ipv6.restype = None
         L.oracle_batch_ipv6.argtypes = [_vp, _vp, _u32, _vp, _vp, _u32]
+        L.oracle_batch_eth.restype = None
+        L.oracle_batch_eth.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]
         L.oracle_batch_ipv4_forward.restype = None
         L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
@@ -133,6 +135,17 @@ def batch_ipv6(base: np.ndarray, desc: np.ndarray, tx: bool = False):
     ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint8)
     lib().oracle_batch_ipv6(_p(base), _p(desc), n, _p(ol), _p(v), ORACLE_IPV4_TX if tx else 0)
     return ol, v
+
+
+def batch_eth(base: np.ndarray, desc: np.ndarray, mac: bytes | None = None, tx: bool = False):
+    """Ethernet dispatch + fused IPv4 / IPv6 (oracle_batch_eth); mac None = no destination filter."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    n = desc.shape[0]
+    on, ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8)
+    m = None if mac is None else _buf(mac)
+    lib().oracle_batch_eth(_p(base), _p(desc), n, None if m is None else _p(m), _p(on), _p(ol), _p(v),
+                           ORACLE_IPV4_TX if tx else 0)
+    return on, ol, v
 
 
 def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:

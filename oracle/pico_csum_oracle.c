@@ -318,6 +318,72 @@ void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint
     }
 }
 
+/*
+ * Ethernet front end of the fused RX verify (SURVEY.md 8f row 1 "Ethernet -> IPv4 ..."),
+ * one frame per descriptor: desc.off -> the Ethernet header (f->datalink_hdr), desc.len =
+ * frame bytes, desc.seed = the IPv6 net_len | proto << 16 (IPv6 frames only, as for
+ * oracle_batch_ipv6).
+ *   RX destination filter   pico_ethernet_receive  modules/pico_ethernet.c:215-235
+ *     (own MAC, 01:00:5e IPv4 multicast, 33:33 IPv6 multicast, broadcast; mac == NULL:
+ *     no filter; never on TX) -> PICO_CSUM_V_DROP_L2
+ *   ethertype dispatch      pico_eth_receive       modules/pico_ethernet.c:180-203
+ *     0x0806 ARP -> PICO_CSUM_V_ARP (pico_arp_receive: no checksum)
+ *     0x0800 -> IS_IPV4 (pico_ethernet.c:143-150, else DROP_L2) -> oracle_batch_ipv4 on
+ *               (off + 14, len - 14)
+ *     0x86DD -> IS_IPV6 (:162-176, else DROP_L2) -> oracle_batch_ipv6, verdict | V_IPV6
+ *     other  -> DROP_L2 (:201-202)
+ *   A frame shorter than the 14-byte header, or with no byte behind it to read the IP
+ *   version from, is MALFORMED.
+ */
+void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const uint8_t *mac,
+                      uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
+{
+    static const uint8_t mc4[3] = {0x01, 0x00, 0x5e}, mc6[2] = {0x33, 0x33},
+                         all[6] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+    uint32_t i;
+    int tx = (flags & ORACLE_IPV4_TX) != 0;
+    for (i = 0; i < n; i++) {
+        const uint8_t *e = base + d[i].off;
+        struct pico_csum_desc sub;
+        uint16_t etype;
+        out_net[i] = 0;
+        out_l4[i] = 0;
+        verdict[i] = PICO_CSUM_V_MALFORMED;
+        if (d[i].len < 14)
+            continue;
+        if (!tx && mac && memcmp(e, mac, 6) != 0 && memcmp(e, mc4, 3) != 0 && memcmp(e, mc6, 2) != 0 &&
+            memcmp(e, all, 6) != 0) {
+            verdict[i] = PICO_CSUM_V_DROP_L2;
+            continue;
+        }
+        etype = (uint16_t)((e[12] << 8) | e[13]);
+        if (etype == 0x0806) {
+            verdict[i] = PICO_CSUM_V_ARP;
+            continue;
+        }
+        if (etype != 0x0800 && etype != 0x86DD) {
+            verdict[i] = PICO_CSUM_V_DROP_L2;
+            continue;
+        }
+        if (d[i].len < 15)
+            continue;
+        if ((e[14] & 0xF0) != (etype == 0x0800 ? 0x40 : 0x60)) {
+            verdict[i] = PICO_CSUM_V_DROP_L2;
+            continue;
+        }
+        sub.off = d[i].off + 14;
+        sub.len = d[i].len - 14;
+        sub.seed = d[i].seed;
+        if (etype == 0x0800) {
+            sub.seed = 0;
+            oracle_batch_ipv4(base, &sub, 1, out_net + i, out_l4 + i, verdict + i, flags);
+        } else {
+            oracle_batch_ipv6(base, &sub, 1, out_l4 + i, verdict + i, flags);
+            verdict[i] |= PICO_CSUM_V_IPV6;
+        }
+    }
+}
+
 /* modules/pico_ipv4.c:1547-1556 (pico_ipv4_forward): hdr->ttl = (uint8_t)(hdr->ttl - 1);
  * if (hdr->ttl < 1) -> expired, dropped; else hdr->crc++ (uint16_t field, native LE
  * increment of the stored big-endian checksum).  In place on base; verdict per

@@ -18,6 +18,9 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_L4_BAD    4u
 #define PICO_CSUM_V_MALFORMED 8u
 #define PICO_CSUM_V_EXPIRED  16u
+#define PICO_CSUM_V_DROP_L2  32u
+#define PICO_CSUM_V_ARP      64u
+#define PICO_CSUM_V_IPV6    128u
 
 #define ORACLE_IPV4_TX 1u
 
@@ -37,6 +40,8 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
 uint32_t oracle_ipv6_pseudo_sum(const uint8_t src[16], const uint8_t dst[16], uint8_t nxthdr, uint32_t transport_len);
 void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
                        uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
+void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const uint8_t *mac,
+                      uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
 void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
                          uint32_t n, uint16_t *out, uint32_t nthreads);

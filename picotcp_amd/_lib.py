@@ -24,6 +24,7 @@ EXPORTED = (
     "pico_checksum_batch_uniform_dev",
     "pico_ipv4_checksum_batch_dev",
     "pico_ipv6_checksum_batch_dev",
+    "pico_eth_checksum_batch_dev",
     "pico_ipv4_forward_batch_dev",
     "pico_csum_ctx_create",
     "pico_csum_ctx_destroy",
@@ -38,6 +39,7 @@ EXPORTED = (
 F_WRITE = 0x1
 F_TX = 0x2
 V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
+V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
 EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12
 
 
@@ -78,6 +80,7 @@ def load() -> ctypes.CDLL:
     sig("pico_checksum_batch_uniform_dev", ctypes.c_int, vp, u64, u64, u32, u32, u32, vp, vp)
     sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp)
     sig("pico_ipv6_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp)
+    sig("pico_eth_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
     sig("pico_csum_ctx_destroy", None, vp)

@@ -24,7 +24,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import F_TX, F_WRITE, V_ACCEPT, V_EXPIRED, V_L4_BAD, V_MALFORMED, V_NET_BAD  # noqa: F401
+from ._lib import (F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_IPV6, V_L4_BAD,  # noqa: F401
+                   V_MALFORMED, V_NET_BAD)
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
 assert DESC_DTYPE.itemsize == 16
@@ -154,6 +155,33 @@ def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
                lib.pico_ipv6_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, _ptr(out_l4),
                                                 _ptr(verdict), _stream_handle(stream)))
     return out_l4, verdict
+
+
+def eth_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, mac: bytes | None = None,
+                       stream=None, out=None):
+    """Ethernet front end + fused IPv4 / IPv6 checksums in one launch (pico_ethernet.c:180-235):
+    desc.off -> Ethernet header, desc.len = frame bytes, desc.seed = IPv6 net_len | proto << 16.
+    mac = the device address (6 bytes) for the RX destination filter, None = no filter.
+    Returns (out_net int16[n], out_transport int16[n], verdict uint8[n])."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    if mac is not None and len(mac) != 6:
+        raise ValueError("mac must be 6 bytes")
+    dev = base.device
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+               torch.empty(n, dtype=torch.uint8, device=dev))
+    out_net, out_l4, verdict = out
+    for t, nm, sz in ((out_net, "out_net", 2), (out_l4, "out_transport", 2), (verdict, "verdict", 1)):
+        _check_out(t, n, nm, dev, sz)
+    lib = _lib.load()
+    m = None if mac is None else ctypes.create_string_buffer(bytes(mac), 6)
+    _lib.check("pico_eth_checksum_batch_dev",
+               lib.pico_eth_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, m, _ptr(out_net),
+                                               _ptr(out_l4), _ptr(verdict), _stream_handle(stream)))
+    return out_net, out_l4, verdict
 
 
 def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: torch.Tensor | None = None,

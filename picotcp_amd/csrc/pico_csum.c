@@ -39,7 +39,7 @@ int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint3
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
-                            void *stream);
+                            uint64_t mac48, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
                                   void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
@@ -331,7 +331,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
                                                      d_out, d_bad,
-                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, s.U == 1, stream),
+                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, s.U == 1, 0, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
@@ -394,7 +394,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
                                                      NULL,
                                                      d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
-                                                     stream),
+                                                     0, stream),
                              "pico_ipv4_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
@@ -430,7 +430,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
                                                      NULL, NULL,
-                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1, stream),
+                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1, 0, stream),
                              "pico_ipv6_checksum_batch_dev");
     if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
         s.G = 1;
@@ -442,6 +442,48 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                                d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
                                                s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
                          "pico_ipv6_checksum_batch_dev");
+}
+
+/* kernel flag: filter destination MACs (Ethernet mode; the public flags reject it) */
+#define KF_MACF 0x10000u
+
+int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
+                                uint8_t *d_verdict, void *stream)
+{
+    struct shape s;
+    uint64_t mac48 = 0;
+    int rc, i;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+    if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
+    if ((rc = need_device()) != 0)
+        return rc;
+    if (mac) {
+        for (i = 0; i < 6; i++)
+            mac48 |= (uint64_t)mac[i] << (8 * i);
+        flags |= KF_MACF;
+    }
+    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
+    if (s.G != 2) {           /* the Ethernet mode exists in the sorted-rounds kernel only */
+        uint32_t f = n / 4096u;
+        s.G = 2;
+        s.CPL = 8;
+        s.U = 1;
+        s.nt = 1;
+        s.fpw = f < 16 ? 16 : f > 64 ? 64 : f;
+    }
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags | ablate_flags(), NULL, NULL,
+                                                 d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
+                                                 mac48, stream),
+                         "pico_eth_checksum_batch_dev");
 }
 
 int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,

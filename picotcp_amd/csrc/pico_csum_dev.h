@@ -1,0 +1,334 @@
+// pico_csum_dev.h -- device helpers shared by the gfx950 kernel TUs of libpicocsum
+// (pico_csum_k_raw.hip, pico_csum_k_flat.hip, pico_csum_k_sorted.hip).  Header-only,
+// internal; everything lives in an anonymous namespace (one copy per TU).
+//
+// The kernels of picoTCP's Internet checksum.
+//
+// What is computed (bit-exact with stack/pico_frame.c:279-328):
+//   S = sum_{i<n/2} (b[2i] | b[2i+1]<<8) + (n odd ? b[n-1] : 0)    word pairing relative to the frame start
+//   s = (seed + S) mod 2^32;  ret = bswap16(~fold16(s))
+//
+// How (DESIGN.md "Kernels"):
+//   * S = E + 256*O, E/O = sums of the bytes at even/odd offsets from the frame
+//     start.  A 16-byte-aligned chunk is loaded with one global_load_dwordx4
+//     whatever the frame's alignment; bytes outside the frame (or inside a
+//     crc field) are masked to zero; for an odd frame start v_perm_b32 swaps
+//     the bytes of each 16-bit half so the pairing is frame-relative again;
+//     v_dot2_u32_u16 (x . {1,1}) then adds both halves into a 32-bit
+//     per-lane accumulator -- exact, two VALU ops per dword.  All later
+//     additions are plain 32-bit wrapping adds, which is exactly the
+//     reference's uint32_t accumulator, so the 131076-byte wrap matches too.
+//   * A frame is owned by a lane group of G lanes (G = 4..64): lane l reads
+//     chunks l, l+G, ... (G*16 contiguous bytes per group per load), CPL
+//     chunks per lane per pass are issued back to back.  The group's partial
+//     sums are folded with DPP row ops (quad_perm, row_half_mirror,
+//     row_mirror) and, above 16 lanes, ds_swizzle/bpermute shuffles.
+//   * A wave owns FPW consecutive frames: descriptors are read with one
+//     coalesced load per wave, results are collected one per lane and written
+//     with one coalesced store per wave.
+//   * No MFMA: this is an HBM-bound byte reduction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+namespace {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint32_t SEL_EVEN = 0x03020100u;  // v_perm: identity
+constexpr uint32_t SEL_ODD  = 0x02030001u;  // v_perm: swap bytes inside each 16-bit half
+
+__device__ __forceinline__ uint32_t dot2_add(uint32_t x, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), (u16x2){1, 1}, acc, false);
+}
+
+// 4 mask bits -> 4 byte masks (0x00 / 0xFF); the shifted copies never overlap.
+__device__ __forceinline__ uint32_t nib_to_bytes(uint32_t nib) {
+    return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+
+// Adds the bytes of chunk v selected by the 16-bit mask m16 (bit i = byte i).
+__device__ __forceinline__ uint32_t add_chunk(const uint4 v, uint32_t m16, uint32_t sel, uint32_t acc) {
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.x & nib_to_bytes(m16 & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.y & nib_to_bytes((m16 >> 4) & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.z & nib_to_bytes((m16 >> 8) & 15u), sel), acc);
+    acc = dot2_add(__builtin_amdgcn_perm(0u, v.w & nib_to_bytes((m16 >> 12) & 15u), sel), acc);
+    return acc;
+}
+
+// Adds all 16 bytes of chunk v (frame-relative pairing via sel when PERM).
+template <bool PERM>
+__device__ __forceinline__ uint32_t add_full(const uint4 v, uint32_t sel, uint32_t acc) {
+    if constexpr (PERM) {
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.x, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.y, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.z, sel), acc);
+        acc = dot2_add(__builtin_amdgcn_perm(0u, v.w, sel), acc);
+    } else {
+        acc = dot2_add(v.x, acc);
+        acc = dot2_add(v.y, acc);
+        acc = dot2_add(v.z, acc);
+        acc = dot2_add(v.w, acc);
+    }
+    return acc;
+}
+
+// Bits [lo, hi) of a 16-bit chunk mask; lo, hi in [0, 16].
+__device__ __forceinline__ uint32_t bits16(uint32_t lo, uint32_t hi) {
+    return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+
+// Mask of the bytes of chunk k (chunk 0 starts at a0 = start & ~15, r = start - a0)
+// that lie in [r + x0, r + x1), x0 <= x1 relative to the frame start.
+__device__ __forceinline__ uint32_t chunk_range_mask(uint32_t k, uint64_t x0r, uint64_t x1r) {
+    const uint64_t c = (uint64_t)k << 4;
+    const uint32_t lo = x0r <= c ? 0u : (x0r - c >= 16 ? 16u : (uint32_t)(x0r - c));
+    const uint32_t hi = x1r <= c ? 0u : (x1r - c >= 16 ? 16u : (uint32_t)(x1r - c));
+    return hi > lo ? bits16(lo, hi) : 0u;
+}
+
+// Clears the two bits of a 2-byte field at chunk-relative position d (may be
+// outside [-1, 15], then nothing is cleared).
+__device__ __forceinline__ uint32_t clear_field(uint32_t m, int64_t d) {
+    const uint32_t sh = (d >= -1 && d <= 15) ? (uint32_t)(d + 1) : 20u;
+    return m & ~((3u << sh) >> 1);
+}
+
+// Sum over a lane group of G lanes (G | 64, groups aligned).  The total lands in
+// the group's LAST lane (lane g*G + G-1); for G <= 16 every lane of the group has it.
+// DPP only: quad_perm xor1/xor2, row_half_mirror, row_mirror, then row_bcast:15
+// (rows 1,3 += lane 15 of the row below) and row_bcast:31 (rows 2,3 += lane 31).
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+    if constexpr (G >= 2)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8)  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    if constexpr (G >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+// stack/pico_frame.c:301-307: fold with end-around carry, complement, short_be.
+__device__ __forceinline__ uint32_t finalize(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    const uint32_t c = (~s) & 0xFFFFu;
+    return ((c >> 8) | (c << 8)) & 0xFFFFu;
+}
+
+// The 16-bit checksum word as it sits in memory: hdr->crc = short_be(ret).  One 16-bit
+// store when the field is 2-byte aligned (every IPv4 / TCP / UDP crc behind a 2-aligned
+// header), two byte stores otherwise.
+__device__ __forceinline__ void store_crc(uint8_t* p, uint32_t ret) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
+        *reinterpret_cast<uint16_t*>(p) = (uint16_t)(((ret >> 8) & 0xFFu) | ((ret & 0xFFu) << 8));
+    } else {
+        p[0] = (uint8_t)(ret >> 8);
+        p[1] = (uint8_t)(ret & 0xFFu);
+    }
+}
+
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* a0, uint32_t k) {
+    return *reinterpret_cast<const uint4*>(a0 + ((uint64_t)k << 4));
+}
+
+// Hands the group results of one iteration to lanes base..base+NG-1: lane base+g
+// receives the value group g holds in its last lane.  Lane j of the wave thus ends
+// up with the result of the wave's frame j (one coalesced store per wave later).
+template <int G>
+__device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t lane, uint32_t base) {
+    constexpr uint32_t NG = 64 / G;
+    if constexpr (NG <= 4) {
+#pragma unroll
+        for (uint32_t g = 0; g < NG; ++g) {
+            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)val, (int)(g * G + G - 1));
+            res = (lane == base + g) ? s : res;
+        }
+        return res;
+    } else {
+        const uint32_t src = ((lane - base) & (NG - 1)) * G + (G - 1);
+        const uint32_t got = (uint32_t)__shfl((int)val, (int)src);
+        return (lane >= base && lane < base + NG) ? got : res;
+    }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 load_chunk_t(const uint8_t* a0, uint32_t k) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(a0 + ((uint64_t)k << 4));
+    u32x4 x;
+    if constexpr (NT) x = __builtin_nontemporal_load(q);
+    else x = *q;
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// ---- windowed buffer loads
+//
+// A wave's frames lie in a window of < 2 GiB.  A buffer resource over that window
+// (built from wave-uniform values: SGPRs, no waterfall) lets every lane issue every
+// load slot unconditionally: a slot past its frame gets voffset WIN_OOB, which the
+// range check turns into zeros without a memory access.  With no branch around the
+// loads the compiler can count them, so a wave consumes set i behind
+// s_waitcnt vmcnt(#set i+1) with set i+1 still in flight -- a `k < nch ? load : 0`
+// becomes an s_cbranch_execz around each load, after which hipcc only dares vmcnt(0).
+constexpr uint32_t WIN_OOB = 0x80000000u;    // >= every window's num_records
+
+struct Window {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint64_t base;                          // window start (16-byte aligned address)
+};
+
+// Window [lo, lo + bytes) over device addresses; lo and bytes must be wave-uniform
+// values (they are read from the first lane), bytes < 2^31.
+__device__ __forceinline__ Window make_window(uint64_t lo, uint32_t bytes) {
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lo);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lo >> 32));
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bytes);
+    Window w;
+    w.base = ((uint64_t)h << 32) | l;
+    w.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(w.base), 0, (int)nb, 0x00020000);
+    return w;
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 load_win(const Window& w, uint32_t voff) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, (int)voff, 0, NT ? 2 : 0);   // aux 2 = nt
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+}  // namespace
+
+// Device view of struct pico_csum_desc (include/pico_csum.h), 16 bytes.
+struct pico_csum_desc_dev {
+    uint64_t off;
+    uint32_t len;
+    uint32_t seed;
+};
+
+namespace {
+
+struct RawArgs {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t n;
+    uint32_t seed;
+    int32_t crc_off;
+    uint32_t flags;
+    uint32_t fpw;
+    uint16_t* out;
+    uint32_t* bad;
+};
+
+
+struct Ipv4Args {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint32_t flags;
+    uint32_t fpw;
+    uint16_t* out_net;
+    uint16_t* out_l4;
+    uint8_t* verdict;
+};
+
+constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u, V_EXPIRED = 16u;
+constexpr uint32_t V_DROP_L2 = 32u, V_ARP = 64u, V_IPV6 = 128u;   // Ethernet mode (include/pico_csum.h)
+constexpr uint32_t F_MACF = 0x10000u;   // kernel flag (set by the host layer): filter destination MACs
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+}
+
+
+// Inclusive prefix sum over the 64 lanes (DPP row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+// Sum of the bytes of chunk v (chunk start at relative position ch) that lie in
+// [x0, x1) (relative to the same origin), frame-relative pairing via sel.
+// Branch-free: the 16-byte validity mask is built as two 64-bit masks.
+template <bool PERM>
+__device__ __forceinline__ uint32_t masked_chunk_sum(const uint4 v, uint32_t ch, uint32_t x0, uint32_t x1,
+                                                     uint32_t sel) {
+    const uint32_t lo = x0 <= ch ? 0u : min(x0 - ch, 16u);
+    const uint32_t hi = x1 <= ch ? 0u : min(x1 - ch, 16u);
+    const uint64_t ALL = ~0ull;
+    uint64_t m0 = lo >= 8u ? 0ull : (ALL << (8u * lo));
+    m0 &= hi >= 8u ? ALL : ~(ALL << (8u * hi));
+    uint64_t m1 = lo >= 16u ? 0ull : (lo <= 8u ? ALL : (ALL << (8u * (lo - 8u))));
+    m1 &= hi >= 16u ? ALL : (hi <= 8u ? 0ull : ~(ALL << (8u * (hi - 8u))));
+    uint32_t a = v.x & (uint32_t)m0, b = v.y & (uint32_t)(m0 >> 32);
+    uint32_t c = v.z & (uint32_t)m1, d = v.w & (uint32_t)(m1 >> 32);
+    if constexpr (PERM) {
+        a = __builtin_amdgcn_perm(0u, a, sel);
+        b = __builtin_amdgcn_perm(0u, b, sel);
+        c = __builtin_amdgcn_perm(0u, c, sel);
+        d = __builtin_amdgcn_perm(0u, d, sel);
+    }
+    return dot2_add(d, dot2_add(c, dot2_add(b, dot2_add(a, 0u))));
+}
+
+struct FlatArgs {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint32_t fpw;
+    int32_t crc_off;      // RAW
+    uint32_t flags;
+    uint16_t* out;        // RAW
+    uint32_t* bad;        // RAW
+    uint16_t* out_net;    // IPV4
+    uint16_t* out_l4;
+    uint8_t* verdict;
+    uint32_t mac_lo;      // ETH: the device's MAC as stored (bytes 0-3, 4-5), with F_MACF
+    uint32_t mac_hi;
+};
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t BIG_CHUNKS = 1u << 16;   // frames above this stream on their own
+
+
+// ---------------------------------------------------------------- dispatch
+
+// (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
+// group) and NT (non-temporal loads), with CPL*U <= 8 (<= 32 data VGPRs).
+#define PICO_FOR_SHAPES(X) \
+    X(64, 1) X(64, 2) X(64, 4) X(64, 8) \
+    X(32, 1) X(32, 2) X(32, 4) X(32, 8) \
+    X(16, 1) X(16, 2) X(16, 4) X(16, 8) \
+    X(8, 1)  X(8, 2)  X(8, 4)  X(8, 8)  \
+    X(4, 1)  X(4, 2)  X(4, 4)  X(4, 8)
+
+#define PICO_FOR_CU(Y, g) \
+    Y(g, 1, 1) Y(g, 2, 1) Y(g, 4, 1) Y(g, 8, 1) Y(g, 1, 2) Y(g, 2, 2) Y(g, 4, 2) Y(g, 1, 4) Y(g, 2, 4)
+
+#define PICO_FOR_RAW(Y) PICO_FOR_CU(Y, 64) PICO_FOR_CU(Y, 32) PICO_FOR_CU(Y, 16) PICO_FOR_CU(Y, 8) PICO_FOR_CU(Y, 4)
+
+inline bool shape_ok(uint32_t G, uint32_t CPL, uint32_t fpw) {
+    if (!(G == 4 || G == 8 || G == 16 || G == 32 || G == 64)) return false;
+    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8)) return false;
+    return fpw >= 1 && fpw <= 64 && fpw % (64 / G) == 0;
+}
+
+inline dim3 grid_for(uint32_t n, uint32_t fpw) {
+    const uint64_t waves = ((uint64_t)n + fpw - 1) / fpw;
+    return dim3((unsigned)((waves + 3) / 4));
+}
+
+
+}  // namespace

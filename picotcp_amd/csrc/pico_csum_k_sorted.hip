@@ -1,0 +1,654 @@
+// pico_csum_k_sorted.hip -- the sorted-rounds descriptor kernel (K4: RAW / fused IPv4 / IPv6 /
+// Ethernet front end), the IPv4 forwarding step (K5), and their launchers.
+// Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
+#include "pico_csum_dev.h"
+
+namespace {
+
+// ---------------------------------------------------------------- sorted-rounds kernel
+//
+// Descriptor batches of any size mix, all modes (RAW / fused IPv4 / fused IPv6).
+// The lane-group body is the cheapest per chunk (an unmasked v_dot2 chain, edge
+// corrections only at frame edges) but a fixed group width G fits no size mix:
+// a wave waits for its largest frame.  Here a wave
+//   1. parses its (up to 64) frames, lane j = frame j (as the flat kernel);
+//   2. orders them by size class -- the narrowest width G in {4..64} whose one pass
+//      (G lanes x CPL chunks) covers the frame -- with 5 ballots and mbcnt (a
+//      64-lane bitonic sort by length measured the same round times at ~1K more
+//      cycles of shuffle latency per batch);
+//   3. walks that order in rounds: each round takes the next 64/G frames with G the
+//      class of the last of them, so every round holds frames of similar size and
+//      keeps its lanes busy; per-frame sums go to LDS;
+//   4. lane j finalizes frame j (one coalesced store per output).
+
+constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1
+
+struct SortedWaveLds {
+    uint32_t acc_all[64];
+    uint32_t acc_x[64];
+    uint32_t acc_opt[64];
+    uint32_t nch[64];
+    uint4 info[64];        // {a0 offset lo, hi, span_end = r + span, r | odd << 4 | k0 << 5}
+    uint2 xo[64];          // {field position (NONE), option end (0)}, relative to a0 + 16 k0
+    uint32_t order[64];    // frames by size class: order[position] = frame (lane)
+    uint4 fin[64];         // parse state for phase 4 (kept in LDS, not VGPRs, across the rounds):
+                           // {verdict | parsed << 4 | l4 << 5 | oob << 6 | proto << 8 | tl << 16,
+                           //  hl | ip crc << 16, pseudo sum (RAW: seed), header sum}
+};
+
+// A wave's LDS.  Fused modes: the phase-1 head-window staging (64 frames x HW chunks,
+// chunk slots XOR-swizzled) shares the space with the state it is parsed into -- 8 KiB a
+// wave, 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
+template <bool STAGE>
+union SortedWaveSmem {
+    SortedWaveLds s;
+    uint4 stage[64 * HW];
+};
+template <>
+union SortedWaveSmem<false> {
+    SortedWaveLds s;
+    uint4 stage[1];
+};
+
+// One round: group g sums the frame at position pos + g of the class order.
+template <int G, int CPL, bool PERM, bool NT, bool XO>
+__device__ __forceinline__ void sorted_round(const RawArgs& p, SortedWaveLds& L, uint32_t pos, uint32_t m) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane / G, l = lane % G;
+    const uint32_t si = pos + g;
+    const bool valid = si < m;
+    const uint32_t j = L.order[min(si, 63u)] & 63u;
+    const uint32_t nch = valid ? L.nch[j] : 0u;
+    const uint4 fi = L.info[j];
+    const uint2 xo = XO ? L.xo[j] : make_uint2(NONE, 0u);
+    // the rounds start k0 chunks into the region (phase 1 summed the head window)
+    const uint32_t k0 = (fi.w >> 5) & 15u;
+    const uint32_t rr = k0 ? 0u : fi.w & 15u;
+    const uint32_t sl = (fi.w & 16u) ? SEL_ODD : SEL_EVEN;
+    const uint32_t send = fi.z > 16u * k0 ? fi.z - 16u * k0 : 0u;
+    const uint8_t* a0 = p.base + ((((uint64_t)fi.y) << 32) | fi.x) + 16u * k0;
+    uint32_t acc = 0, accx = 0, acco = 0;
+    for (uint32_t kb = 0; kb < nch; kb += G * CPL) {
+        uint4 v[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = kb + l + G * c;
+            v[c] = k < nch ? load_chunk_t<NT>(a0, k) : make_uint4(0, 0, 0, 0);
+        }
+        // interior chunks unmasked; masked sums only where a chunk holds a region edge
+        // (a wave-uniform branch: skipped for slots no lane's edge falls in)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const uint32_t k = kb + l + G * c;
+            const uint32_t ch = k << 4;
+            if (k < nch && (ch < rr || ch + 16u > send)) acc += masked_chunk_sum<PERM>(v[c], ch, rr, send, sl);
+            else acc = add_full<PERM>(v[c], sl, acc);
+            if constexpr (XO) {
+                if (k < nch && xo.x != NONE && (k == (xo.x >> 4) || k == ((xo.x + 1u) >> 4)))
+                    accx += masked_chunk_sum<PERM>(v[c], ch, xo.x, xo.x + 2u, sl);
+                if (k < nch && xo.y != 0u && ch < xo.y)
+                    acco += masked_chunk_sum<PERM>(v[c], ch, rr + 20u, xo.y, sl);
+            }
+        }
+    }
+    acc = group_sum<G>(acc);
+    if constexpr (XO) {
+        accx = group_sum<G>(accx);
+        acco = group_sum<G>(acco);
+    }
+    if (valid && l == G - 1) {           // added to phase 1's head-window sums
+        L.acc_all[j] += acc;
+        if constexpr (XO) {
+            if (xo.x != NONE) L.acc_x[j] += accx;
+            if (xo.y != 0u) L.acc_opt[j] += acco;
+        }
+    }
+}
+
+// Round width: the smallest G whose one pass (G lanes x CPL chunks) covers the
+// round's largest frame; 64 lanes per frame beyond that.  NT: non-temporal loads
+// in the rounds of G >= 16 (frames over ~1 KiB; measured: they cost on small ones).
+// SMALL adds a 1-lane class below the 4-lane one: frames of <= CPL chunks (<= 8 x 16 B,
+// e.g. 64-byte IMIX frames) are summed one frame per lane, 64 per round, so a wave
+// pays one dependent HBM round trip for all its small frames instead of one per 16.
+template <int CPL, bool PERM, bool NT, bool XO, bool SMALL>
+__device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L, const uint32_t (&e)[5], uint32_t m) {
+    // position s holds a frame of class <= c iff s < e[c]; a round of width G may
+    // take the next 64/G positions when the last of them is of class <= G's class
+    constexpr int o = SMALL ? 1 : 0;
+    uint32_t pos = 0;
+    if constexpr (SMALL) {
+        if (e[0]) { sorted_round<1, CPL, PERM, false, XO>(p, L, 0u, min(m, e[0])); pos = min(e[0], 64u); }
+    }
+    while (pos < m) {
+        if (min(pos + 15u, m - 1u) < e[o])            { sorted_round<4, CPL, PERM, false, XO>(p, L, pos, m);  pos += 16u; }
+        else if (min(pos + 7u, m - 1u) < e[o + 1])    { sorted_round<8, CPL, PERM, false, XO>(p, L, pos, m);  pos += 8u; }
+        else if (min(pos + 3u, m - 1u) < e[o + 2])   { sorted_round<16, CPL, PERM, NT, XO>(p, L, pos, m); pos += 4u; }
+        else if (min(pos + 1u, m - 1u) < e[o + 3])   { sorted_round<32, CPL, PERM, NT, XO>(p, L, pos, m); pos += 2u; }
+        else                                          { sorted_round<64, CPL, PERM, NT, XO>(p, L, pos, m); pos += 1u; }
+    }
+}
+
+// MODE: 0 RAW (p.crc_off / p.flags / p.out / p.bad), 1 fused IPv4, 2 fused IPv6,
+// 3 Ethernet front end (per frame: destination filter, ethertype -> IPv4 / IPv6 / ARP / drop;
+// pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in Ipv4Args-compatible fields of FlatArgs.
+// Phase 4: lane `lane` finalizes its frame (output index idx) from the LDS state.
+template <int MODE>
+__device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t idx,
+                                              bool tx) {
+    asm volatile("" ::: "memory");
+    const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
+    const uint4 info = L.info[lane], fin = L.fin[lane];
+    const uint32_t xpos = L.xo[lane].x;
+    const uint32_t r = info.w & 15u;
+    uint8_t* fp = p.base + (((((uint64_t)info.y) << 32) | info.x) + r);
+    uint32_t verdict = fin.x & 15u;
+    const bool parsed = fin.x & 16u, l4_needed = fin.x & 32u, oob = fin.x & 64u;
+    const bool fam6 = MODE == 2 || (MODE == 3 && (fin.x & 128u));
+    const uint32_t proto = (fin.x >> 8) & 0xFFu, tl = fin.x >> 16;
+    const uint32_t hl = fin.y & 0xFFu, l2v = (fin.y >> 8) & 0xFFu, ipcrc = fin.y >> 16;
+    const uint32_t pseudo = fin.z, seed = fin.z, hdr20 = fin.w;
+    if constexpr (MODE == 0) {
+        uint32_t ret = 0;
+        if (oob) {
+            if (p.bad) atomicAdd(p.bad, 1u);
+        } else {
+            ret = finalize(seed + acc_all - acc_x);
+            if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
+        }
+        p.out[idx] = (uint16_t)ret;
+    } else {
+        uint32_t net = 0, l4 = 0;
+        if (MODE == 3 && l2v) {
+            verdict = l2v;                   // dropped by the Ethernet layer, or ARP: no checksum
+        } else if (fam6) {
+            if (parsed) {
+                if (l4_needed) {
+                    if (!tx) {
+                        if (proto == 6u || (proto == 17u && acc_x != 0u) || proto == 58u) {
+                            l4 = finalize(pseudo + acc_all);
+                            const uint32_t type = acc_x & 0xFFu;   // ICMPv6 type (x field = [0, 2))
+                            const bool checked = proto != 58u || (type >= 130u && type <= 137u) || type == 143u;
+                            if (l4 != 0 && checked) verdict |= V_L4_BAD;
+                        }
+                    } else {
+                        l4 = finalize(pseudo + acc_all - acc_x);
+                    }
+                }
+                if (verdict == 0) verdict = V_ACCEPT;
+            }
+            if (tx && (p.flags & 1u) && verdict == V_ACCEPT && l4_needed)
+                store_crc(fp + (proto == 6u ? 16u : proto == 17u ? 6u : 2u), l4);
+            if (MODE == 3) verdict |= V_IPV6;
+        } else {
+            if (parsed) {
+                const uint32_t acc_hdr = hdr20 + acc_opt;
+                net = finalize(acc_hdr - (tx ? ipcrc : 0u));
+                if (!tx && net != 0) verdict |= V_NET_BAD;
+                const uint32_t tsum = acc_all - acc_hdr;
+                if (l4_needed) {
+                    if (!tx) {
+                        if (proto == 6u || acc_x != 0u) {
+                            l4 = finalize(pseudo + tsum);
+                            if (l4 != 0) verdict |= V_L4_BAD;
+                        }
+                    } else if (proto == 6u) {
+                        l4 = finalize(pseudo + tsum - acc_x);
+                    } else {
+                        l4 = finalize(tsum - acc_x);
+                    }
+                }
+                if (verdict == 0) verdict = V_ACCEPT;
+            }
+            if (tx && (p.flags & 0x401u) == 1u && verdict == V_ACCEPT) {   // 0x400: ablation
+                store_crc(fp + 10, net);
+                if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
+                else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+            }
+        }
+        if (MODE != 2 && p.out_net) p.out_net[idx] = (uint16_t)net;
+        if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
+        if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
+    }
+}
+
+// The NW little-endian dwords at byte position pos of a frame's head window (pos < 16, or
+// pos < 32 with SHIFT): whole-chunk shift, then a 4-way dword select and alignbyte.
+template <int NW, bool SHIFT>
+__device__ __forceinline__ void window_words(const uint4 (&hw)[HW], uint32_t pos, uint32_t (&H)[NW]) {
+    constexpr int NC = (4 * (NW + 4) + 15) / 16;      // chunks the selects below may touch
+    static_assert(NC + (SHIFT ? 1 : 0) <= (int)HW, "head window too small");
+    // a bit-mask blend, not `s1 ? hw[c + 1] : hw[c]` (which LLVM turns into a dynamic index
+    // into hw -- the array then lives in scratch memory)
+    const uint32_t s1 = SHIFT && pos >= 16u ? 0xFFFFFFFFu : 0u;
+    uint32_t D[4 * NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint4 a = hw[c], b = hw[SHIFT ? c + 1 : c];
+        D[4 * c] = (a.x & ~s1) | (b.x & s1);
+        D[4 * c + 1] = (a.y & ~s1) | (b.y & s1);
+        D[4 * c + 2] = (a.z & ~s1) | (b.z & s1);
+        D[4 * c + 3] = (a.w & ~s1) | (b.w & s1);
+    }
+    const uint32_t q = (pos >> 2) & 3u, sh = pos & 3u;
+    uint32_t E[NW + 1];
+#pragma unroll
+    for (int m = 0; m <= NW; ++m) E[m] = sel4(q, D[m], D[m + 1], D[m + 2], D[m + 3]);
+#pragma unroll
+    for (int m = 0; m < NW; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+}
+
+// CPL 8 keeps 8 KiB of loads in flight per wave within 128 VGPRs (4 waves per
+// SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
+// fits 64 VGPRs (8 waves per SIMD).
+template <int MODE, bool NT, int CPL, bool SMALL>
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, uint32_t lane,
+                                             uint64_t f0) {
+    constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2, ETH = MODE == 3;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const bool tx = MODE != 0 && (p.flags & 2u) != 0;
+
+    // ---- 1. lane j = frame j
+    uint4 dcur = make_uint4(0, 0, 0, 0);
+    if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+    uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
+    uint32_t len = lane < cnt ? dcur.z : 0u;
+    const uint32_t seed = dcur.w;
+    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
+    if (oob || lane >= cnt) { len = 0; off = 0; }
+    uint8_t* fp = p.base + off;
+    uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+    uint64_t a0off = off - r;
+    uint32_t odd = r & 1u;
+
+    uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
+    uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, l2v = 0;
+    bool parsed = false, l4_needed = false, is6 = false;
+    const uint64_t a0h = a0off;                  // the head window's first chunk (fused modes)
+    uint4 hw[HW];
+    uint32_t nlh = 0;                            // head-window chunks loaded
+    bool staged = false;                         // the window also sits in this lane's LDS row
+    uint32_t k0 = 0, p_all = 0, p_x = 0, p_opt = 0;
+    if constexpr (MODE == 0) {
+        span = ext = len;
+        if (p.crc_off >= 0 && (uint64_t)p.crc_off + 2u <= len) xpos = r + (uint32_t)p.crc_off;
+    } else {
+        // the head window: the frame's first HW chunks (128 bytes from the header's
+        // 16-byte line), loaded once here.  They hold the header (parsed below), the
+        // usual isolated 2-byte field and the IPv4 options, and, for small datagrams
+        // (64-byte IMIX frames), the whole datagram: their sums are taken here and the
+        // rounds start behind the window (or are skipped).
+        constexpr uint32_t HDR = IPV6 ? 40u : IPV4 ? 20u : 14u;
+        nlh = len >= HDR && !(p.flags & 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;   // 0x200: ablation
+        {
+            // Buffer loads through a window over the batch (from base's 16-byte line to
+            // base_len rounded up -- the bytes load_chunk may touch -- at most 2 GiB, from
+            // 1 GiB below the wave's first frame): all HW slots issue back to back and
+            // slots past the frame read zeros.  (`i < nlh ? load : 0` compiled to branched
+            // flat loads with a vmcnt(0) behind the second: two dependent HBM round trips
+            // per wave.)  A frame outside the window (a wave spanning > 1 GiB of a batch
+            // over 2 GiB) is loaded in a second, branched pass.
+            const uint8_t* a0 = p.base + a0off;
+            const uint64_t a0a = reinterpret_cast<uintptr_t>(a0);
+            const uint64_t wb = reinterpret_cast<uintptr_t>(p.base) & ~(uint64_t)15;
+            const uint64_t wn = (reinterpret_cast<uintptr_t>(p.base) + p.base_len + 15u - wb) & ~(uint64_t)15;
+            const uint64_t act = __builtin_amdgcn_ballot_w64(nlh != 0);
+            const int first = act ? __builtin_ffsll((long long)act) - 1 : 0;
+            const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(a0a >> 32), first) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0a, first);
+            const uint64_t lo = anchor >= wb + (1ull << 30) ? anchor - (1ull << 30) : wb;
+            const uint64_t wsz = min(wn - min(lo - wb, wn), (uint64_t)0x7FFFFFF0u);
+            const bool inside = a0a >= lo && a0a - lo + 16u * nlh <= wsz;
+            staged = inside;
+            const Window w = make_window(lo, (uint32_t)wsz);
+            const uint32_t v0 = (uint32_t)(a0a - lo);
+            const uint32_t nin = inside ? nlh : 0u;
+            // Transposed: load k covers frames FPL*k .. FPL*k+FPL-1 with HW lanes each, so one
+            // instruction reads FPL whole 128-byte windows (a lane per frame touched 64
+            // lines per instruction and re-fetched each line for every chunk: L1 thrash).
+            // The chunks meet their frame's lane through LDS (row g holds chunk c in slot
+            // c ^ (g & 7): 8 lanes reading chunk i of 8 rows hit 8 different bank groups).
+            constexpr uint32_t FPL = 64u / HW;
+            const uint32_t gi = lane / HW, ci = lane % HW;
+            uint4 t[HW];
+#pragma unroll
+            for (uint32_t k = 0; k < HW; ++k) {
+                const uint32_t g = FPL * k + gi;
+                const uint32_t gv0 = (uint32_t)__shfl((int)v0, (int)g);
+                const uint32_t gn = (uint32_t)__shfl((int)nin, (int)g);
+                t[k] = load_win<false>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < HW; ++k) {
+                const uint32_t g = FPL * k + gi;
+                stage[g * HW + (ci ^ (g & (HW - 1)))] = t[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * HW + (i ^ (lane & (HW - 1)))];
+            // the staging rows alias the wave's SortedWaveLds (written at the end of phase 1)
+            asm volatile("" ::: "memory");
+            if (__builtin_amdgcn_ballot_w64(!inside && nlh != 0)) {
+#pragma unroll
+                for (uint32_t i = 0; i < HW; ++i)
+                    if (!inside && i < nlh) hw[i] = load_chunk(a0, i);
+            }
+        }
+        // MODE 3: the Ethernet header first (pico_ethernet_receive / pico_eth_receive,
+        // pico_ethernet.c:180-235), then the IP header at +14 (the region moves there).
+        uint32_t fam = IPV6 ? 6u : 4u, pos = r, avail = len;
+        if constexpr (ETH) {
+            fam = 0;
+            if (len >= 14u) {
+                uint32_t M[2], T[1];
+                window_words<2, true>(hw, r, M);
+                window_words<1, true>(hw, r + 12u, T);
+                const uint32_t m0 = M[0], m1 = M[1] & 0xFFFFu, et = T[0] & 0xFFFFu;   // ethertype, LE word
+                const bool mine = !(p.flags & F_MACF) || tx || (m0 == p.mac_lo && m1 == p.mac_hi) ||
+                                  (m0 & 0xFFFFFFu) == 0x5E0001u || (m0 & 0xFFFFu) == 0x3333u ||
+                                  (m0 == 0xFFFFFFFFu && m1 == 0xFFFFu);
+                if (!mine) l2v = V_DROP_L2;
+                else if (et == 0x0608u) l2v = V_ARP;          // 0x0806 -> pico_arp_receive
+                else if (et == 0x0008u) fam = 4u;             // 0x0800
+                else if (et == 0xDD86u) fam = 6u;             // 0x86DD
+                else l2v = V_DROP_L2;
+                if (fam) {
+                    pos = r + 14u;
+                    off += 14u;
+                    avail = len - 14u;
+                    fp = p.base + off;
+                    r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+                    a0off = off - r;
+                    odd = r & 1u;
+                    uint32_t V[1];
+                    window_words<1, true>(hw, pos, V);
+                    // IS_IPV4 / IS_IPV6 (pico_ethernet.c:145,164); no byte to read: MALFORMED
+                    if (avail == 0u) fam = 0;
+                    else if ((V[0] & 0xF0u) != (fam << 4)) { fam = 0; l2v = V_DROP_L2; }
+                }
+            }
+        }
+        if (IPV4 || (ETH && fam == 4u)) {
+            if (avail >= 20) {
+                uint32_t H[5];
+                window_words<5, ETH>(hw, pos, H);
+                const uint32_t ihl = H[0] & 0x0Fu;
+                hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+                proto = (H[2] >> 8) & 0xFFu;
+                ipcrc = H[2] >> 16;
+                tl = (tot - hl) & 0xFFFFu;                              // uint16 wrap, pico_ipv4.c:395
+                const uint32_t max_allowed = (avail - 20u) & 0xFFFFu;   // pico_ipv4.c:386
+                if (!(hl > avail || (!tx && tl > max_allowed) || hl + tl > avail)) {
+                    parsed = true;
+                    verdict = 0;
+                    span = ext = hl + tl;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
+                    pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
+                             (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
+                    if (hl > 20u) optend = r + hl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (hl + 8u > avail) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
+                        }
+                    } else {
+                        if (proto == 6u) {
+                            if (tl < 20u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 16u; }
+                        } else if (proto == 1u) {
+                            if (tl < 8u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 2u; }
+                        }
+                    }
+                }
+            }
+        } else if (IPV6 || (ETH && fam == 6u)) {
+            if (avail >= 40) {
+                uint32_t H[10];
+                window_words<10, ETH>(hw, pos, H);
+                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+                uint32_t net_len = seed & 0xFFFFu;
+                proto = (seed >> 16) & 0xFFu;
+                if (seed == 0) { net_len = 40u; proto = (H[1] >> 16) & 0xFFu; }
+                tl = (plen - (net_len - 40u)) & 0xFFFFu;                // pico_ipv6.c:790
+                if (net_len >= 40u && net_len <= avail && net_len + tl <= avail) {
+                    uint32_t addr = 0, xrel = NONE;
+#pragma unroll
+                    for (int m = 2; m < 10; ++m) addr = dot2_add(H[m], addr);
+                    pseudo = addr + (((tl & 0xFFu) << 8) | (tl >> 8)) + (proto << 8);
+                    parsed = true;
+                    verdict = 0;
+                    ext = tl;
+                    if (!tx) {
+                        if (proto == 6u) {
+                            l4_needed = true;
+                        } else if (proto == 17u) {
+                            if (net_len + 8u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 6u; ext = max(tl, 8u); }
+                        } else if (proto == 58u) {
+                            if (net_len + 1u > avail) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = 0u; ext = max(tl, 1u); }
+                        }
+                    } else {
+                        const uint32_t need = proto == 6u ? 20u : proto == 17u ? 8u : 4u;
+                        if (proto == 6u || proto == 17u || proto == 58u) {
+                            if (tl < need) { parsed = false; verdict = V_MALFORMED; }
+                            else { l4_needed = true; xrel = proto == 6u ? 16u : proto == 17u ? 6u : 2u; }
+                        }
+                    }
+                    if (parsed) {
+                        off += net_len;
+                        fp = p.base + off;
+                        r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
+                        a0off = off - r;
+                        odd = r & 1u;
+                        span = tl;
+                        if (xrel != NONE) xpos = r + xrel;
+                    } else {
+                        ext = 0;
+                    }
+                }
+            }
+        }
+        is6 = fam == 6u;
+    }
+    const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
+    uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
+    if constexpr (MODE != 0) {
+        // sums over the head window: the region's chunks [0, k0) = window chunks
+        // [d, d + k0) (d: where the region's chunk grid starts in the window -- IPv6:
+        // behind the header); the rounds take region chunks [k0, nch).  A field
+        // straddling the cut moves the cut down a chunk (a field is summed whole on one
+        // side); options not inside the window (never, for IPv4) leave it all to the rounds.
+        const uint32_t d = (uint32_t)min((a0off - a0h) >> 4, (uint64_t)HW);
+        k0 = nlh > d ? min(nlh - d, nch) : 0u;
+        if (xpos != NONE && xpos < 16u * k0 && xpos + 2u > 16u * k0) k0 = xpos >> 4;
+        if (optend != 0u && optend > 16u * (d + k0)) k0 = 0;
+        const uint32_t P = 16u * (d + k0), rs = 16u * d + r;
+        const uint32_t re = min(rs + span, P);
+        const bool xin = xpos != NONE && 16u * d + xpos + 2u <= P;
+        const uint32_t xs = 16u * d + xpos;
+        const bool oin = optend != 0u && k0 != 0u;
+        const uint32_t sl = odd ? SEL_ODD : SEL_EVEN;
+#pragma unroll
+        for (uint32_t i = 0; i < HW; ++i) {
+            if (i >= d && i < d + k0) {
+                p_all += masked_chunk_sum<true>(hw[i], 16u * i, min(rs, re), re, sl);
+                if (xin && !staged) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
+                if (oin) p_opt += masked_chunk_sum<true>(hw[i], 16u * i, r + 20u, optend, sl);
+            }
+        }
+        // The isolated field is one word of the region's pairing: whatever the start's
+        // parity, its share is byte[xs] | byte[xs+1] << 8 in the accumulators' (byte-
+        // swapped) domain -- two LDS byte reads instead of HW masked sums.
+        if (xin && staged) {
+            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
+            const uint32_t sw = (lane & (HW - 1)) << 4, x1 = xs + 1u;   // chunk slots are XOR-swizzled
+            p_x = (uint32_t)row[xs ^ sw] | ((uint32_t)row[x1 ^ sw] << 8);
+        }
+        asm volatile("" ::: "memory");   // stage rows are read before the state below overwrites them
+        if (xin) xpos = NONE;
+        else if (xpos != NONE) xpos -= 16u * k0;
+        if (oin) optend = 0;
+        nch -= k0;
+    }
+    L.acc_all[lane] = p_all;
+    L.acc_x[lane] = p_x;
+    L.acc_opt[lane] = p_opt;
+    L.nch[lane] = nch;
+    L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (k0 << 5));
+    L.xo[lane] = make_uint2(xpos, optend);
+    L.fin[lane] = make_uint4(verdict | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
+                                 (is6 ? 128u : 0u) | (proto << 8) | (tl << 16),
+                             hl | (l2v << 8) | (ipcrc << 16), MODE == 0 ? seed : pseudo, hdr20);
+    const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
+    const bool any_xo = __builtin_amdgcn_ballot_w64(nch != 0 && (xpos != NONE || optend != 0)) != 0;
+
+    // ---- 2. order the frames by size class (the narrowest round width that covers
+    //         them in one pass): ballots and bit counts, no data movement but one
+    //         LDS store per frame
+    // classes by round width: (SMALL: 1,) 4, 8, 16, 32, 64 lanes; NC = no data
+    constexpr uint32_t NC = SMALL ? 6u : 5u;
+    const uint32_t cw = nch <= 4u * CPL ? 0u : nch <= 8u * CPL ? 1u : nch <= 16u * CPL ? 2u : nch <= 32u * CPL ? 3u : 4u;
+    const uint32_t cls = nch == 0 ? NC : SMALL ? (nch <= (uint32_t)CPL ? 0u : cw + 1u) : cw;
+    uint64_t bal[NC];
+#pragma unroll
+    for (uint32_t c = 0; c < NC; ++c) bal[c] = __builtin_amdgcn_ballot_w64(cls == c);
+    uint32_t e[5] = {0, 0, 0, 0, 0};     // e[c] = frames of class <= c
+    e[0] = (uint32_t)__builtin_popcountll(bal[0]);
+#pragma unroll
+    for (uint32_t c = 1; c + 1 < NC; ++c) e[c] = e[c - 1] + (uint32_t)__builtin_popcountll(bal[c]);
+    const uint32_t m = e[NC - 2] + (uint32_t)__builtin_popcountll(bal[NC - 1]);
+    if (cls < NC) {
+        uint64_t mine = bal[0];
+        uint32_t start = 0;
+#pragma unroll
+        for (uint32_t c = 1; c < NC; ++c) {
+            mine = cls == c ? bal[c] : mine;
+            start = cls == c ? e[c - 1] : start;
+        }
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        L.order[start + rank] = lane;
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- 3. rounds over the sorted frames
+    RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
+    // ablation only (PICO_CSUM_ABLATE): flags bit 8 skips the rounds (times phases 1, 2, 4);
+    // bit 9 skips the head-window loads (then nothing parses: descriptors + stores alone);
+    // bit 10 skips the IPv4 TX in-place crc writes
+    if (m && !(p.flags & 0x100u)) {
+        if (any_odd) {
+            if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
+            else sorted_rounds<CPL, true, NT, false, SMALL>(ra, L, e, m);
+        } else {
+            if (any_xo) sorted_rounds<CPL, false, NT, true, SMALL>(ra, L, e, m);
+            else sorted_rounds<CPL, false, NT, false, SMALL>(ra, L, e, m);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+
+    // ---- 4. lane j finalizes frame j (state reloaded from LDS)
+    if (lane < cnt) sorted_finish<MODE>(p, L, lane, f0 + lane, tx);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave per batch of up to 64 frames.  (A persistent grid looping over batches
+// measured slower: every wave repeats the same serial descriptor -> rounds chain.)
+template <int MODE, bool NT, int CPL, bool SMALL = false>
+__global__ __launch_bounds__(256, CPL == 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<MODE != 0> lds_all[4];
+    const uint32_t lane = threadIdx.x & 63u;
+    SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
+    const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+}
+
+// ---------------------------------------------------------------- IPv4 forwarding step
+//
+// pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) on a batch of datagrams that are
+// routed through this host: hdr->ttl = ttl - 1 (written back whatever follows);
+// ttl < 1 -> expired (pico_notify_ttl_expired, the frame is dropped, crc untouched);
+// else hdr->crc++ -- the reference's "HACK: increase crc to compensate decreased
+// TTL": a native (little-endian) uint16 increment of the stored big-endian field.
+// That is the incremental update of RFC 1141 (+0x0100 on the checksum for -1 on the
+// TTL byte) except where it carries out of the first byte, and it is kept exactly
+// so, bit-compatible with the reference.  One lane per datagram; the 4 bytes at
+// header offset 8..11 (ttl, proto, crc) are read and written, nothing else.
+struct FwdArgs {
+    uint8_t* base;
+    uint64_t base_len;
+    const pico_csum_desc_dev* desc;
+    uint32_t n;
+    uint8_t* verdict;
+};
+
+__global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint4 d = *reinterpret_cast<const uint4*>(p.desc + i);
+    const uint64_t off = ((uint64_t)d.y << 32) | d.x;
+    uint32_t v = V_MALFORMED;
+    if (off <= p.base_len && d.z <= p.base_len - off && d.z >= 20u) {
+        uint8_t* h = p.base + off;
+        const uint8_t ttl = (uint8_t)(h[8] - 1u);
+        h[8] = ttl;
+        if (ttl < 1u) {
+            v = V_EXPIRED;
+        } else {
+            const uint32_t crc = (uint32_t)h[10] | ((uint32_t)h[11] << 8);
+            const uint32_t inc = (crc + 1u) & 0xFFFFu;
+            h[10] = (uint8_t)inc;
+            h[11] = (uint8_t)(inc >> 8);
+            v = V_ACCEPT;
+        }
+    }
+    if (p.verdict) p.verdict[i] = (uint8_t)v;
+}
+
+
+}  // namespace
+
+extern "C" {
+
+// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6; small: 1-lane
+// rounds for frames of <= 8 chunks (cpl 8 only).
+// mode 3: Ethernet front end; mac48 = the device MAC's 6 bytes (little-endian in a uint64),
+// used when flags carry F_MACF (set by the host layer).
+int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
+                            uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
+                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
+                            uint64_t mac48, void* stream) {
+    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 3 || (small && cpl != 8))
+        return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
+               crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32)};
+    const dim3 grid = grid_for(n, fpw), block(256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    using K = void (*)(FlatArgs);
+    // [mode][nt][cpl 4 | cpl 8 | cpl 8 with the 1-lane class]
+#define SK(m, t) {csum_sorted_kernel<m, t, 4>, csum_sorted_kernel<m, t, 8>, csum_sorted_kernel<m, t, 8, true>}
+    static const K table[4][2][3] = {{SK(0, false), SK(0, true)}, {SK(1, false), SK(1, true)},
+                                     {SK(2, false), SK(2, true)}, {SK(3, false), SK(3, true)}};
+#undef SK
+    const int v = cpl == 4 ? 0 : small ? 2 : 1;
+    hipLaunchKernelGGL(table[mode][nt ? 1 : 0][v], grid, block, 0, s, a);
+    return (int)hipGetLastError();
+}
+
+int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, uint8_t* verdict,
+                                  void* stream) {
+    if (n == 0) return (int)hipSuccess;
+    FwdArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, verdict};
+    const dim3 grid((unsigned)(((uint64_t)n + 255u) / 256u)), block(256);
+    hipLaunchKernelGGL(ipv4_forward_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -165,3 +165,58 @@ def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = T
         buf[t + 3] = 0
     seeds = np.full(n, (net_len | (proto << 16)) if hbh else 0, dtype=np.uint32)
     return buf, net, lengths.copy(), seeds
+
+
+ETH_KINDS = ("ipv4_tcp", "ipv4_udp", "ipv4_icmp", "ipv6_tcp", "ipv6_udp", "ipv6_icmp", "ipv6_hbh_tcp", "arp",
+             "lldp", "ipv4_bad_version")
+
+
+def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")):
+    """A mixed Ethernet burst as a TAP / pico_device RX ring delivers it: n frames, each
+    with a 14-byte Ethernet header, of the kinds in ETH_KINDS (IPv4 / IPv6 datagrams in
+    IMIX sizes, ARP, an unknown ethertype, an IPv4 ethertype carrying version 6), in seeded
+    order with 0-3 byte gaps (every alignment), and destination MACs drawn from {mac,
+    broadcast, 01:00:5e IPv4 multicast, 33:33 IPv6 multicast, a foreign unicast}.  Transport
+    crc fields are zero (TX input).  Returns (buffer, frame offsets uint64, frame bytes
+    uint32, descriptor seeds uint32 (IPv6 net_len | proto << 16 behind a hop-by-hop header,
+    else 0), kind index uint8 into ETH_KINDS)."""
+    rng = np.random.default_rng(seed)
+    kind = rng.integers(0, len(ETH_KINDS), n).astype(np.uint8)
+    frames, seeds = [], np.zeros(n, dtype=np.uint32)
+    lens = imix_lengths(n, seed ^ 0x33)
+    for i in range(n):
+        k = ETH_KINDS[kind[i]]
+        s = seed * 7919 + i
+        if k.startswith("ipv4"):
+            proto = {"ipv4_tcp": 6, "ipv4_udp": 17, "ipv4_icmp": 1, "ipv4_bad_version": 6}[k]
+            b, _, _ = ipv4_batch(np.array([max(int(lens[i]), 48)], np.uint32), seed=s, proto=proto, eth=True)
+            if k == "ipv4_bad_version":
+                b[14] = 0x65
+        elif k.startswith("ipv6"):
+            proto = 6 if "tcp" in k else 17 if "udp" in k else 58
+            b, _, _, sd = ipv6_batch(np.array([max(int(lens[i]) + 20, 68)], np.uint32), seed=s, proto=proto,
+                                     eth=True, hbh="hbh" in k, icmp_type=int(rng.choice([128, 129, 135, 136, 143])))
+            seeds[i] = sd[0]
+        elif k == "arp":
+            b = random_bytes(s, 60)
+            b[12], b[13] = 0x08, 0x06
+        else:
+            b = random_bytes(s, int(rng.integers(60, 300)))
+            b[12], b[13] = 0x88, 0xCC
+        d = int(rng.integers(0, 10))
+        dst = (mac if d < 5 else b"\xff" * 6 if d == 5 else bytes([0x01, 0x00, 0x5e, 1, 2, 3]) if d == 6
+               else bytes([0x33, 0x33, 0, 0, 0, 1]) if d == 7 else bytes([0x02, 0x11, 0x22, 0x33, 0x44, 0x55]))
+        b[0:6] = np.frombuffer(dst, np.uint8)
+        frames.append(b)
+    gaps = rng.integers(0, 4, n)
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        off[i] = pos
+        pos += frames[i].size
+    buf = random_bytes(seed ^ 0xE7, pos + 16)
+    for i in range(n):
+        buf[int(off[i]):int(off[i]) + frames[i].size] = frames[i]
+    flen = np.array([f.size for f in frames], dtype=np.uint32)
+    return buf, off, flen, seeds, kind

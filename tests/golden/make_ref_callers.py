@@ -29,6 +29,11 @@ Output (data only): ref_callers.npz
   mld_buf, mld_net, mld_size, mld_rx, mld_tx: MLDv2 report datagrams (IPv6 header, hop-by-hop
                  router alert, report) and pico_mld_checksum over them as they are (rx) and with
                  the report's crc zeroed (tx)
+and eth_cases.npz: a mixed Ethernet burst (IPv4 / IPv6 / ARP / other ethertypes, MAC filter
+cases) with the oracle_batch_eth expectations (pico_ethernet.c:180-235 dispatch restated in
+oracle/pico_csum_oracle.c), every transport value of an IP frame checked against the
+reference callers above.  The dispatch itself is static in pico_ethernet.c and needs the
+device layer, so that part is restated, not compiled ("parity unpinned" for the dispatch).
 """
 from __future__ import annotations
 
@@ -143,6 +148,95 @@ def mld(lib, n: int = 96):
     return dict(mld_buf=buf, mld_net=starts, mld_size=lens, mld_rx=rx, mld_tx=tx)
 
 
+MAC = bytes.fromhex("02005e0a0b0c")
+
+
+def eth(lib, n: int = 1536):
+    """The Ethernet front end (oracle_batch_eth: pico_ethernet.c:180-235 dispatch, then the
+    IPv4 / IPv6 logic) over a mixed burst (synth.eth_batch): TX expectations on the
+    zero-crc frames; the checksums then stored as the reference TX path does (UDP over IPv4
+    with a real checksum so that RX verifies it); seeded corruptions; RX expectations with
+    and without the destination-MAC filter.  Every transport value of an IP frame is also
+    checked against the reference's own callers."""
+    from oracle import oracle as O
+    buf, off, flen, seeds, kind = synth.eth_batch(n, seed=31, mac=MAC)
+    desc = np.zeros(n, dtype=[("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+    desc["off"], desc["len"], desc["seed"] = off, flen, seeds
+    tx_buf = buf.copy()
+    tn, tl4, tv = O.batch_eth(tx_buf, desc, tx=True)
+    rx_buf = tx_buf.copy()
+    checked = 0
+    for i in range(n):
+        o = int(off[i]) + 14
+        if tv[i] == 1:                                        # IPv4, accepted
+            ihl = int(rx_buf[o]) & 0xF
+            hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
+            tlen = ((int(rx_buf[o + 2]) << 8) | int(rx_buf[o + 3])) - hl
+            proto = int(rx_buf[o + 9])
+            rx_buf[o + 10], rx_buf[o + 11] = tn[i] >> 8, tn[i] & 0xFF
+            if proto in (6, 1):
+                x = o + hl + (16 if proto == 6 else 2)
+                rx_buf[x], rx_buf[x + 1] = tl4[i] >> 8, tl4[i] & 0xFF
+                if proto == 6:
+                    assert call(lib, RC_TCP4, tx_buf, o, int(flen[i]) - 14, hl, tlen, True) == tl4[i]
+                    checked += 1
+            elif proto == 17:
+                c = call(lib, RC_UDP4, rx_buf, o, int(flen[i]) - 14, hl, tlen, True)
+                rx_buf[o + hl + 6], rx_buf[o + hl + 7] = c >> 8, c & 0xFF
+        elif tv[i] == (1 | 128):                              # IPv6, accepted
+            sd = int(seeds[i])
+            net_len, proto = (sd & 0xFFFF, sd >> 16) if sd else (40, int(rx_buf[o + 6]))
+            tlen = ((int(rx_buf[o + 4]) << 8) | int(rx_buf[o + 5])) - (net_len - 40)
+            xo = {6: 16, 17: 6, 58: 2}.get(proto)
+            if xo is not None:
+                which = {6: RC_TCP6, 17: RC_UDP6, 58: RC_ICMP6}[proto]
+                assert call(lib, which, tx_buf, o, int(flen[i]) - 14, net_len, tlen, True) == tl4[i]
+                checked += 1
+                rx_buf[o + net_len + xo], rx_buf[o + net_len + xo + 1] = tl4[i] >> 8, tl4[i] & 0xFF
+    rng = np.random.default_rng(3131)
+    for i in range(n):                                        # corruptions (index-stable)
+        r = rng.random()
+        o, fl = int(off[i]), int(flen[i])
+        if r < 0.7:
+            continue
+        if r < 0.8:
+            rx_buf[o + 14 + int(rng.integers(0, max(1, fl - 14)))] ^= 0x10          # header / payload bit
+        elif r < 0.85:
+            desc["len"][i] = int(rng.integers(0, 40))                               # truncated frame
+        elif r < 0.9:
+            rx_buf[o + 12], rx_buf[o + 13] = 0x81, 0x00                            # VLAN tag: not handled
+        else:
+            rx_buf[o:o + 6] = np.frombuffer(bytes([0x02, 0x99, 0x88, 0x77, 0x66, 0x55]), np.uint8)
+    rn, rl4, rv = O.batch_eth(rx_buf, desc, mac=MAC)
+    rn_nomac, rl4_nomac, rv_nomac = O.batch_eth(rx_buf, desc)
+    for i in range(n):                                        # RX transport values vs the callers
+        o, a = int(off[i]) + 14, int(desc["len"][i]) - 14
+        if rv[i] & 8 or a <= 0 or rl4[i] == 0 and not (rv[i] & 4):
+            continue
+        if rv[i] & 128:
+            sd = int(seeds[i])
+            net_len, proto = (sd & 0xFFFF, sd >> 16) if sd else (40, int(rx_buf[o + 6]))
+            tlen = (((int(rx_buf[o + 4]) << 8) | int(rx_buf[o + 5])) - (net_len - 40)) & 0xFFFF
+            which = {6: RC_TCP6, 17: RC_UDP6, 58: RC_ICMP6}.get(proto)
+            if which is not None:
+                assert call(lib, which, rx_buf, o, a, net_len, tlen, False) == rl4[i], i
+                checked += 1
+        elif rv[i] & 7:
+            ihl = int(rx_buf[o]) & 0xF
+            hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
+            tlen = (((int(rx_buf[o + 2]) << 8) | int(rx_buf[o + 3])) - hl) & 0xFFFF
+            proto = int(rx_buf[o + 9])
+            if proto in (6, 17):
+                assert call(lib, RC_TCP4 if proto == 6 else RC_UDP4, rx_buf, o, a, hl, tlen, False) == rl4[i], i
+                checked += 1
+    print(f"eth: {n} frames, {checked} transport values checked against the reference callers;",
+          "RX verdicts", dict(zip(*[x.tolist() for x in np.unique(rv, return_counts=True)])))
+    return dict(tx_buf=tx_buf, buf=rx_buf, off=off, flen=flen, rx_len=desc["len"].copy(), seed=seeds, kind=kind,
+                mac=np.frombuffer(MAC, np.uint8).copy(), tx_net=tn, tx_l4=tl4, tx_verdict=tv,
+                rx_net=rn, rx_l4=rl4, rx_verdict=rv, rx_net_nomac=rn_nomac, rx_l4_nomac=rl4_nomac,
+                rx_verdict_nomac=rv_nomac)
+
+
 def main() -> None:
     if not os.path.exists(LIB):
         sys.exit(f"{LIB} missing: run `make -C oracle refcallers` first")
@@ -161,6 +255,7 @@ def main() -> None:
     out = dict(v4_rx=v4_rx, v4_tx=v4_tx, v6_rx=v6_rx, v6_tx=v6_tx, **mld(lib))
     np.savez_compressed(os.path.join(OUT, "ref_callers.npz"), **out)
     print("mld:", out["mld_net"].size, "reports")
+    np.savez_compressed(os.path.join(OUT, "eth_cases.npz"), **eth(lib))
 
 
 if __name__ == "__main__":

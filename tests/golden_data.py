@@ -71,3 +71,17 @@ def ref_callers() -> dict:
     """Transport checksums from the reference's own compiled callers (make_ref_callers.py)."""
     z = np.load(os.path.join(GOLDEN, "ref_callers.npz"))
     return {k: z[k] for k in z.files}
+
+
+def eth_cases() -> dict:
+    """Mixed Ethernet burst with the oracle_batch_eth expectations (make_ref_callers.py)."""
+    z = np.load(os.path.join(GOLDEN, "eth_cases.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def eth_desc(c: dict, rx: bool = True) -> np.ndarray:
+    d = np.zeros(c["off"].size, dtype=DESC_DTYPE)
+    d["off"] = c["off"]
+    d["len"] = c["rx_len"] if rx else c["flen"]
+    d["seed"] = c["seed"]
+    return d
