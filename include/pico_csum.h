@@ -200,6 +200,35 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
 int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
                                 uint8_t *d_verdict, void *stream);
 
+/* IPv4 fragment reassembly fused with the transport check of the reassembled datagram
+ * (pico_ipv4_process_frag / pico_fragments_check_complete /
+ * pico_fragments_reassemble, modules/pico_fragments.c:129-139,216-239,304-358,499-568, then
+ * pico_transport_crc_check, stack/pico_socket.c:1916-1968).  One pass reads each fragment's
+ * payload once, writes it into the reassembled datagram and sums it; the reference copies
+ * it (memcpy, :334-345) and sums the copy again.
+ *   d_frag[]   fragments as pico_ipv4_process_in hands them on (desc.off -> the fragment's
+ *              IPv4 header, desc.len = bytes available; header already checked)
+ *   d_groups[] 2 uint32 per datagram: first fragment, count -- the fragments one reassembly
+ *              tree collects (src / dst / id matched by the stack), in arrival order
+ *   d_out_desc[] per datagram: output region in d_out (off a multiple of 4, len = capacity)
+ * Tree order by fragment offset ((frag & 0x1FFF) << 3; a repeated offset keeps the earlier
+ * arrival, as pico_tree_insert rejects the later); complete when the offsets are contiguous
+ * from 0 up to the first fragment without MF.  The output is the first fragment's 20 header
+ * bytes (options are not copied, :332-333) followed by every payload.
+ *   d_out_len[g]       transport length of the reassembled datagram, 0 when not reassembled
+ *   d_out_transport[g] TCP (always) / UDP (crc != 0) checksum with the pseudo header of the
+ *                      copied header (0 = valid; 0 when none is computed)
+ *   d_verdict[g]       ACCEPT, L4_BAD, or MALFORMED = not reassembled: incomplete, a fragment
+ *                      behind the completing one (the reference's copy loop would write past
+ *                      its buffer: reference UB), 20 + len > 65535 (its uint16 allocation size
+ *                      wraps), a fragment header or payload past desc.len or base_len, an empty
+ *                      group or one of more than 512 fragments, an output region too small.
+ * Any of the three output pointers may be NULL. */
+int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
+                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
+                                   uint16_t *d_out_transport, uint8_t *d_verdict, void *stream);
+
 /* ---------------------------------------------------------------- layer 3 */
 
 struct pico_csum_ctx;   /* device, two streams, double-buffered staging */
@@ -212,6 +241,28 @@ void pico_csum_ctx_destroy(struct pico_csum_ctx *ctx);
  * d2h of every result has completed. */
 int pico_checksum_batch_uniform_host(struct pico_csum_ctx *ctx, const void *base, uint64_t stride,
                                      uint32_t len, uint32_t n, uint32_t seed, uint16_t *out);
+/* Host-resident descriptor batches: the TAP / pico_device burst as the stack holds it
+ * (frames anywhere in `base`, base_len bytes, descriptors and results in host memory; pin
+ * `base` and the outputs with pico_csum_host_register for full PCIe rate).  Consecutive
+ * descriptors whose bytes span at most the ctx staging size form a chunk: the span and the
+ * rebased descriptors go H2D, the device batch of the same name runs, and only the per-frame
+ * results come back (with PICO_CSUM_F_WRITE also the span, crc fields stored); chunk c+1's
+ * H2D overlaps chunk c's kernel and D2H on the other stream.  Results, verdicts and error
+ * rules are those of the _dev functions; a frame larger than the staging buffer is -EINVAL.
+ * With F_WRITE, frames of different chunks must not share bytes (true for a frame ring).
+ * Returns when every result is in host memory. */
+int pico_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                             const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
+                             uint16_t *out);
+int pico_ipv4_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                  const struct pico_csum_desc *desc, uint32_t n, uint32_t flags, uint16_t *out_net,
+                                  uint16_t *out_transport, uint8_t *verdict);
+int pico_ipv6_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                  const struct pico_csum_desc *desc, uint32_t n, uint32_t flags,
+                                  uint16_t *out_transport, uint8_t *verdict);
+int pico_eth_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                 const struct pico_csum_desc *desc, uint32_t n, uint32_t flags, const uint8_t *mac,
+                                 uint16_t *out_net, uint16_t *out_transport, uint8_t *verdict);
 int pico_csum_host_register(void *ptr, uint64_t bytes);
 int pico_csum_host_unregister(void *ptr);
 

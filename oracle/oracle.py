@@ -66,6 +66,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_batch_ipv6.argtypes = [_vp, _vp, _u32, _vp, _vp, _u32]
         L.oracle_batch_eth.restype = None
         L.oracle_batch_eth.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]
+        L.oracle_ipv4_reassemble.restype = None
+        L.oracle_ipv4_reassemble.argtypes = [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
         L.oracle_batch_ipv4_forward.restype = None
         L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
@@ -146,6 +148,18 @@ def batch_eth(base: np.ndarray, desc: np.ndarray, mac: bytes | None = None, tx: 
     lib().oracle_batch_eth(_p(base), _p(desc), n, None if m is None else _p(m), _p(on), _p(ol), _p(v),
                            ORACLE_IPV4_TX if tx else 0)
     return on, ol, v
+
+
+def ipv4_reassemble(base: np.ndarray, desc: np.ndarray, groups: np.ndarray, out: np.ndarray, out_desc: np.ndarray):
+    """oracle_ipv4_reassemble: writes into `out` (uint8, writable); returns (out_len, out_l4, verdict)."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    od = np.ascontiguousarray(out_desc, dtype=DESC_DTYPE)
+    grp = np.ascontiguousarray(groups, dtype=np.uint32).reshape(-1)
+    ng = grp.size // 2
+    ol, l4, v = np.zeros(ng, np.uint32), np.zeros(ng, np.uint16), np.zeros(ng, np.uint8)
+    lib().oracle_ipv4_reassemble(_p(base), _p(desc), desc.shape[0], _p(grp), ng, _p(out), _p(od), _p(ol), _p(l4),
+                                 _p(v))
+    return ol, l4, v
 
 
 def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:

@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
+#include <stdlib.h>
 #include <pthread.h>
 #include <time.h>
 
@@ -381,6 +382,103 @@ void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint3
             oracle_batch_ipv6(base, &sub, 1, out_l4 + i, verdict + i, flags);
             verdict[i] |= PICO_CSUM_V_IPV6;
         }
+    }
+}
+
+/*
+ * IPv4 fragment reassembly with the transport check of the reassembled datagram
+ * (SURVEY.md 8f row 4).  Fragments arrive as pico_ipv4_process_in hands them to
+ * pico_ipv4_process_frag (modules/pico_ipv4.c:381-450: f->transport_len = tot - net_len,
+ * f->frag = short_be(hdr->frag)); group g = fragments grp[2g] .. grp[2g] + grp[2g+1] - 1 of
+ * one datagram (src, dst, id matched by the stack, pico_fragments.c:499-568), in arrival
+ * order.  Per group:
+ *   tree order     pico_ipv4_frag_compare (pico_fragments.c:129-139): by offset
+ *                  IP4_FRAG_OFF = (frag & 0x1FFF) << 3; pico_tree_insert rejects a second
+ *                  fragment with the same offset, so the earlier arrival is kept
+ *   completeness   pico_fragments_check_complete (:216-239): offsets contiguous from 0
+ *                  (offset == sum of the previous transport_len), up to the first
+ *                  fragment without PICO_IPV4_MOREFRAG; len = that sum
+ *   gather         pico_fragments_reassemble (:304-358): PICO_SIZE_IP4HDR (20) header
+ *                  bytes of the first fragment, then every fragment's transport bytes
+ *   transport      pico_transport_crc_check (stack/pico_socket.c:1916-1968) with
+ *                  net_hdr->proto of the copied header: TCP always, UDP when its crc != 0;
+ *                  pseudo header from the copied header, transport_len = len
+ * out_len[g] = len (0 when not reassembled), out_l4[g] = the checksum (0 = valid; 0 when
+ * none), verdict[g] = ACCEPT / L4_BAD, or MALFORMED when not reassembled: incomplete, a
+ * fragment behind the completing one (the reference's copy loop, :339-345, would write
+ * past its 20 + len byte buffer), 20 + len > 65535 (its (uint16_t) allocation size wraps),
+ * a fragment whose header or transport lies past desc.len, an empty group or one of more
+ * than 512 fragments (the API's limit), or an output
+ * region (out_desc[g].len) shorter than 20 + len or not 4-byte aligned (the API's contract).
+ */
+void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
+                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
+                            uint8_t *verdict)
+{
+    uint32_t g;
+    for (g = 0; g < ng; g++) {
+        uint32_t first = grp[2 * g], cnt = grp[2 * g + 1], i, k, m = 0, len = 0, bad = 0, e = 0, done = 0;
+        uint32_t na = cnt && cnt <= 512 ? cnt : 1;
+        uint32_t *ord = (uint32_t *)malloc(sizeof(uint32_t) * na);
+        uint32_t *foff = (uint32_t *)malloc(sizeof(uint32_t) * na);
+        uint32_t *tl = (uint32_t *)malloc(sizeof(uint32_t) * na);
+        uint32_t *hlen = (uint32_t *)malloc(sizeof(uint32_t) * na);
+        uint8_t *mf = (uint8_t *)malloc(na);
+        out_len[g] = 0;
+        out_l4[g] = 0;
+        verdict[g] = PICO_CSUM_V_MALFORMED;
+        if (cnt == 0 || cnt > 512 || first > nd || cnt > nd - first)   /* 512: the device API's limit */
+            bad = 1;
+        for (i = 0; i < cnt && !bad; i++) {
+            const struct pico_csum_desc *f = &d[first + i];
+            const uint8_t *h = base + f->off;
+            uint32_t ihl, frag;
+            if (f->len < 20) { bad = 1; break; }
+            ihl = h[0] & 0x0Fu;
+            hlen[i] = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+            tl[i] = (uint16_t)(((h[2] << 8) | h[3]) - hlen[i]);
+            frag = (uint32_t)((h[6] << 8) | h[7]);
+            foff[i] = (frag & 0x1FFFu) << 3;
+            mf[i] = (frag & 0x2000u) != 0;
+            if (hlen[i] + tl[i] > f->len) bad = 1;
+        }
+        /* tree: insertion by offset, a repeated offset keeps the earlier arrival */
+        for (i = 0; i < cnt && !bad; i++) {
+            uint32_t pos = 0, dup = 0;
+            for (k = 0; k < m; k++) {
+                if (foff[ord[k]] == foff[i]) { dup = 1; break; }
+                if (foff[ord[k]] < foff[i]) pos = k + 1;
+            }
+            if (dup) continue;
+            memmove(ord + pos + 1, ord + pos, sizeof(uint32_t) * (m - pos));
+            ord[pos] = i;
+            m++;
+        }
+        for (k = 0; k < m && !bad; k++) {
+            if (foff[ord[k]] != len) break;
+            len += tl[ord[k]];
+            if (!mf[ord[k]]) { e = k; done = 1; break; }
+        }
+        if (!bad && done && e + 1 == m && 20u + len <= 0xFFFFu && od[g].len >= 20u + len && (od[g].off & 3u) == 0) {
+            uint8_t *dst = out + od[g].off;
+            const uint8_t *h0 = base + d[first + ord[0]].off;
+            uint32_t at = 20, s;
+            uint8_t proto = h0[9];
+            memcpy(dst, h0, 20);
+            for (k = 0; k < m; k++) {
+                const uint8_t *src = base + d[first + ord[k]].off + hlen[ord[k]];
+                memcpy(dst + at, src, tl[ord[k]]);
+                at += tl[ord[k]];
+            }
+            out_len[g] = len;
+            verdict[g] = PICO_CSUM_V_ACCEPT;
+            if (proto == 6 || (proto == 17 && len >= 8 && (dst[20 + 6] || dst[20 + 7]))) {
+                s = oracle_ipv4_pseudo_sum(dst + 12, dst + 16, proto, (uint16_t)len);
+                out_l4[g] = oracle_checksum_finalize(oracle_checksum_adder(s, dst + 20, len));
+                if (out_l4[g]) verdict[g] = PICO_CSUM_V_L4_BAD;
+            }
+        }
+        free(ord); free(foff); free(tl); free(hlen); free(mf);
     }
 }
 

@@ -42,6 +42,9 @@ void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint
                        uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
 void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const uint8_t *mac,
                       uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags);
+void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
+                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
+                            uint8_t *verdict);
 void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
                          uint32_t n, uint16_t *out, uint32_t nthreads);

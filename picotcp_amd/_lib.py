@@ -26,9 +26,14 @@ EXPORTED = (
     "pico_ipv6_checksum_batch_dev",
     "pico_eth_checksum_batch_dev",
     "pico_ipv4_forward_batch_dev",
+    "pico_ipv4_reassemble_batch_dev",
     "pico_csum_ctx_create",
     "pico_csum_ctx_destroy",
     "pico_checksum_batch_uniform_host",
+    "pico_checksum_batch_host",
+    "pico_ipv4_checksum_batch_host",
+    "pico_ipv6_checksum_batch_host",
+    "pico_eth_checksum_batch_host",
     "pico_csum_host_register",
     "pico_csum_host_unregister",
     "pico_csum_abi_version",
@@ -82,9 +87,14 @@ def load() -> ctypes.CDLL:
     sig("pico_ipv6_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp)
     sig("pico_eth_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp)
+    sig("pico_ipv4_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
     sig("pico_csum_ctx_destroy", None, vp)
     sig("pico_checksum_batch_uniform_host", ctypes.c_int, vp, vp, u64, u32, u32, u32, vp)
+    sig("pico_checksum_batch_host", ctypes.c_int, vp, vp, u64, vp, u32, i32, u32, vp)
+    sig("pico_ipv4_checksum_batch_host", ctypes.c_int, vp, vp, u64, vp, u32, u32, vp, vp, vp)
+    sig("pico_ipv6_checksum_batch_host", ctypes.c_int, vp, vp, u64, vp, u32, u32, vp, vp)
+    sig("pico_eth_checksum_batch_host", ctypes.c_int, vp, vp, u64, vp, u32, u32, vp, vp, vp, vp)
     sig("pico_csum_host_register", ctypes.c_int, vp, u64)
     sig("pico_csum_host_unregister", ctypes.c_int, vp)
     sig("pico_csum_abi_version", ctypes.c_int)

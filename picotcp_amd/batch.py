@@ -203,6 +203,34 @@ def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: 
     return verdict
 
 
+def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: int, groups: torch.Tensor,
+                          out: torch.Tensor, out_desc: torch.Tensor, stream=None, results=None):
+    """IPv4 reassembly gather + transport check (pico_fragments.c:216-358): groups = uint32
+    (first, count) pairs per datagram (int32 tensor of 2*n), out = uint8 device buffer the
+    datagrams are written into at out_desc[g].off.  Returns (out_len int32[n], out_transport
+    int16[n], verdict uint8[n])."""
+    for t, nm in ((base, "base"), (frag_desc, "frag_desc"), (groups, "groups"), (out, "out"), (out_desc, "out_desc")):
+        _require_device(t, nm)
+    n = groups.numel() // 2
+    if groups.element_size() != 4 or not groups.is_contiguous():
+        raise ValueError("groups must be a contiguous 32-bit tensor of (first, count) pairs")
+    if frag_desc.numel() < 16 * n_frag or out_desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than its count")
+    dev = base.device
+    if results is None:
+        results = (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+                   torch.empty(n, dtype=torch.uint8, device=dev))
+    ol, l4, v = results
+    for t, nm, sz in ((ol, "out_len", 4), (l4, "out_transport", 2), (v, "verdict", 1)):
+        _check_out(t, n, nm, dev, sz)
+    lib = _lib.load()
+    _lib.check("pico_ipv4_reassemble_batch_dev",
+               lib.pico_ipv4_reassemble_batch_dev(_ptr(base), base.numel(), _ptr(frag_desc), n_frag, _ptr(groups), n,
+                                                  _ptr(out), out.numel(), _ptr(out_desc), _ptr(ol), _ptr(l4), _ptr(v),
+                                                  _stream_handle(stream)))
+    return ol, l4, v
+
+
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic,
@@ -217,8 +245,9 @@ def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int 
 
 
 class HostBatch:
-    """Host-resident batches through pico_checksum_batch_uniform_host: H2D, kernel and D2H
-    chunked over two streams (staging_bytes per chunk)."""
+    """Host-resident batches (pico_checksum_batch_uniform_host and the descriptor batches
+    pico_{checksum,ipv4_checksum,ipv6_checksum,eth_checksum}_batch_host): H2D, kernel and
+    D2H chunked over two streams (staging_bytes per chunk)."""
 
     def __init__(self, device: int = 0, staging_bytes: int = 64 << 20):
         self._lib = _lib.load()
@@ -254,6 +283,55 @@ class HostBatch:
                                                               seed & 0xFFFFFFFF,
                                                               ctypes.c_void_p(out.ctypes.data)))
         return out
+
+    @staticmethod
+    def _host(a: np.ndarray, name: str, dtype=None) -> int:
+        if not isinstance(a, np.ndarray) or not a.flags.c_contiguous or (dtype is not None and a.dtype != dtype):
+            raise ValueError(f"{name} must be a contiguous numpy array" + (f" of {dtype}" if dtype else ""))
+        return a.ctypes.data
+
+    def _desc_args(self, base: np.ndarray, desc: np.ndarray):
+        if not (isinstance(base, np.ndarray) and base.dtype == np.uint8 and base.flags.c_contiguous):
+            raise ValueError("base must be a contiguous uint8 numpy array (host memory)")
+        d = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        return d, ctypes.c_void_p(base.ctypes.data), base.size, ctypes.c_void_p(d.ctypes.data), d.size
+
+    def _outs(self, n, *spec):
+        return [np.zeros(n, dtype=dt) for dt in spec]
+
+    def checksum_batch(self, base: np.ndarray, desc: np.ndarray, crc_off: int = -1, flags: int = 0) -> np.ndarray:
+        """pico_checksum_batch_host: raw descriptor batch from host memory (F_WRITE stores in `base`)."""
+        d, b, bl, dp, n = self._desc_args(base, desc)
+        (out,) = self._outs(n, np.uint16)
+        _lib.check("pico_checksum_batch_host",
+                   self._lib.pico_checksum_batch_host(self._ctx, b, bl, dp, n, crc_off, flags,
+                                                      ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def ipv4_checksum_batch(self, base: np.ndarray, desc: np.ndarray, flags: int = 0):
+        d, b, bl, dp, n = self._desc_args(base, desc)
+        on, ol, v = self._outs(n, np.uint16, np.uint16, np.uint8)
+        _lib.check("pico_ipv4_checksum_batch_host",
+                   self._lib.pico_ipv4_checksum_batch_host(self._ctx, b, bl, dp, n, flags, on.ctypes.data,
+                                                           ol.ctypes.data, v.ctypes.data))
+        return on, ol, v
+
+    def ipv6_checksum_batch(self, base: np.ndarray, desc: np.ndarray, flags: int = 0):
+        d, b, bl, dp, n = self._desc_args(base, desc)
+        ol, v = self._outs(n, np.uint16, np.uint8)
+        _lib.check("pico_ipv6_checksum_batch_host",
+                   self._lib.pico_ipv6_checksum_batch_host(self._ctx, b, bl, dp, n, flags, ol.ctypes.data,
+                                                           v.ctypes.data))
+        return ol, v
+
+    def eth_checksum_batch(self, base: np.ndarray, desc: np.ndarray, flags: int = 0, mac: bytes | None = None):
+        d, b, bl, dp, n = self._desc_args(base, desc)
+        on, ol, v = self._outs(n, np.uint16, np.uint16, np.uint8)
+        m = None if mac is None else ctypes.create_string_buffer(bytes(mac), 6)
+        _lib.check("pico_eth_checksum_batch_host",
+                   self._lib.pico_eth_checksum_batch_host(self._ctx, b, bl, dp, n, flags, m, on.ctypes.data,
+                                                          ol.ctypes.data, v.ctypes.data))
+        return on, ol, v
 
     def close(self) -> None:
         if self._ctx:

@@ -42,6 +42,10 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint64_t mac48, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
                                   void *stream);
+int pico_csum_launch_ipv4_reassemble(const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
+                                     const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len,
+                                     const void *out_desc, uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict,
+                                     void *stream);
 int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                           uint16_t *out_net,
                           uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
@@ -502,10 +506,35 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
                          "pico_ipv4_forward_batch_dev");
 }
 
+int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
+                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
+                                   uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
+{
+    int rc;
+    if (n_dgram == 0)
+        return 0;
+    if (!d_base || !d_frag || !d_groups || !d_out || !d_out_desc)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_frag & 15u) != 0 || ((uintptr_t)d_out_desc & 15u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor arrays must be 16-byte aligned");
+    if (((uintptr_t)d_groups & 3u) != 0 || ((uintptr_t)d_out & 3u) != 0)
+        return fail(PICO_CSUM_EINVAL, "d_groups and d_out must be 4-byte aligned");
+    if ((rc = need_device()) != 0)
+        return rc;
+    return launch_status(pico_csum_launch_ipv4_reassemble(d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out,
+                                                          out_len, d_out_desc, d_out_len, d_out_transport, d_verdict,
+                                                          stream),
+                         "pico_ipv4_reassemble_batch_dev");
+}
+
 /* ------------------------------------------------------------------ layer 3 */
 
 /* results buffer of a staging slot: one uint16 per frame, up to this many frames per chunk */
 #define CTX_MAX_FRAMES(staging) ((staging) / 16u + 64u)
+
+/* descriptors per chunk of a host-resident descriptor batch (>= 64 bytes a frame on average) */
+#define CTX_MAX_DESC(staging) ((staging) / 64u + 64u)
 
 struct pico_csum_ctx {
     int device;
@@ -514,6 +543,12 @@ struct pico_csum_ctx {
     uint16_t *d_out[2];
     hipStream_t st[2];
     hipEvent_t done[2];
+    /* descriptor batches (allocated on first use): rebased descriptors (pinned host ->
+     * device) and the per-frame results of a chunk */
+    struct pico_csum_desc *h_desc[2], *d_desc[2];
+    uint16_t *d_net[2], *d_l4[2];
+    uint8_t *d_ver[2];
+    int desc_ready;
 };
 
 struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes)
@@ -554,6 +589,11 @@ void pico_csum_ctx_destroy(struct pico_csum_ctx *c)
         if (c->d_out[i]) hipFree(c->d_out[i]);
         if (c->done[i]) hipEventDestroy(c->done[i]);
         if (c->st[i]) hipStreamDestroy(c->st[i]);
+        if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
+        if (c->d_desc[i]) hipFree(c->d_desc[i]);
+        if (c->d_net[i]) hipFree(c->d_net[i]);
+        if (c->d_l4[i]) hipFree(c->d_l4[i]);
+        if (c->d_ver[i]) hipFree(c->d_ver[i]);
     }
     free(c);
 }
@@ -583,7 +623,6 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
     uint64_t per;
     uint32_t first = 0;
     int b = 0, rc = 0;
-    struct shape s;
     if (!c || !base || !out)
         return fail(PICO_CSUM_EINVAL, "NULL argument");
     if (n == 0)
@@ -604,10 +643,7 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
         /* staging buffer b is free once its previous chunk's D2H is done (same stream: ordered) */
         e = hipMemcpyAsync(c->d_buf[b], src, bytes, hipMemcpyHostToDevice, c->st[b]);
         if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "H2D: %s", hipGetErrorString(e)); break; }
-        s = pick_shape(cnt, len, 1);
-        rc = launch_status(pico_csum_launch_raw(c->d_buf[b], c->staging, NULL, stride, len, cnt, seed, -1, 0,
-                                                c->d_out[b], NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, c->st[b]),
-                           "pico_checksum_batch_uniform_host");
+        rc = pico_checksum_batch_uniform_dev(c->d_buf[b], c->staging, stride, len, cnt, seed, c->d_out[b], c->st[b]);
         if (rc) break;
         e = hipMemcpyAsync(out + first, c->d_out[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]);
         if (e != hipSuccess) { rc = fail(PICO_CSUM_EIO, "D2H: %s", hipGetErrorString(e)); break; }
@@ -617,4 +653,162 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
     if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
         if (!rc) rc = fail(PICO_CSUM_EIO, "stream synchronize failed");
     return rc;
+}
+
+/* ---- host-resident descriptor batches (raw / IPv4 / IPv6 / Ethernet) */
+
+enum { HB_RAW = 0, HB_IPV4 = 1, HB_IPV6 = 2, HB_ETH = 3 };
+
+static int ctx_desc_alloc(struct pico_csum_ctx *c)
+{
+    uint64_t nd = CTX_MAX_DESC(c->staging);
+    int i;
+    if (c->desc_ready)
+        return 0;
+    for (i = 0; i < 2; i++) {
+        if (hipHostMalloc((void **)&c->h_desc[i], nd * sizeof(struct pico_csum_desc), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **)&c->d_desc[i], nd * sizeof(struct pico_csum_desc)) != hipSuccess ||
+            hipMalloc((void **)&c->d_net[i], nd * 2u) != hipSuccess || hipMalloc((void **)&c->d_l4[i], nd * 2u) != hipSuccess ||
+            hipMalloc((void **)&c->d_ver[i], nd) != hipSuccess)
+            return fail(PICO_CSUM_ENOMEM, "ctx descriptor staging (%llu descriptors)", (unsigned long long)nd);
+    }
+    c->desc_ready = 1;
+    return 0;
+}
+
+/* One burst: descriptors [i, j) whose bytes span at most the staging buffer go H2D (the span
+ * and the descriptors, rebased to it) on stream b, through the device batch, and their results
+ * (with F_WRITE also the span, crc fields written) D2H; the next chunk's H2D overlaps this one
+ * on the other stream.  A region outside base_len is handed to the kernel as one (offset past
+ * the staging bound), so it gets the device API's answer for it. */
+static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, uint64_t base_len,
+                           const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
+                           const uint8_t *mac, uint16_t *out, uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict,
+                           const char *what)
+{
+    const uint64_t maxd = CTX_MAX_DESC(c->staging);
+    uint32_t i = 0;
+    int b = 0, rc = 0;
+    if (!c || !base || !desc)
+        return fail(PICO_CSUM_EINVAL, "%s: NULL argument", what);
+    if (n == 0)
+        return 0;
+    if ((rc = ctx_desc_alloc(c)) != 0)
+        return rc;
+    if (hipSetDevice(c->device) != hipSuccess)
+        return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
+    while (i < n && !rc) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        uint32_t j = i, k, cnt;
+        hipError_t e;
+        /* grow the chunk while the span fits the staging buffer */
+        while (j < n && (uint64_t)(j - i) < maxd) {
+            uint64_t o = desc[j].off, oa, end;
+            if (o > base_len || desc[j].len > base_len - o) {   /* out of bounds: no bytes */
+                j++;
+                continue;
+            }
+            oa = o & ~(uint64_t)15;   /* the span starts on a 16-byte line: frames keep their alignment */
+            end = o + desc[j].len;
+            if ((end > hi ? end : hi) - (oa < lo ? oa : lo) > c->staging) {
+                if (j == i)
+                    return fail(PICO_CSUM_EINVAL, "%s: a frame of %u bytes exceeds the staging buffer", what,
+                                desc[j].len);
+                break;
+            }
+            if (oa < lo) lo = oa;
+            if (end > hi) hi = end;
+            j++;
+        }
+        cnt = j - i;
+        if (lo == UINT64_MAX) lo = hi = 0;
+        /* the pinned descriptor slot is reused: its previous H2D must be done */
+        if (hipEventSynchronize(c->done[b]) != hipSuccess)
+            return fail(PICO_CSUM_EIO, "%s: event synchronize failed", what);
+        for (k = 0; k < cnt; k++) {
+            const struct pico_csum_desc *s = &desc[i + k];
+            struct pico_csum_desc *t = &c->h_desc[b][k];
+            int oob = s->off > base_len || s->len > base_len - s->off;
+            t->off = oob ? UINT64_MAX : s->off - lo;
+            t->len = s->len;
+            t->seed = s->seed;
+        }
+        if (hi > lo && (e = hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice,
+                                           c->st[b])) != hipSuccess)
+            return fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
+        if ((e = hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
+                                hipMemcpyHostToDevice, c->st[b])) != hipSuccess)
+            return fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
+        switch (mode) {
+        case HB_RAW:
+            rc = pico_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, crc_off, flags, c->d_l4[b], NULL,
+                                         c->st[b]);
+            break;
+        case HB_IPV4:
+            rc = pico_ipv4_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, c->d_net[b], c->d_l4[b],
+                                              c->d_ver[b], c->st[b]);
+            break;
+        case HB_IPV6:
+            rc = pico_ipv6_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, c->d_l4[b], c->d_ver[b],
+                                              c->st[b]);
+            break;
+        default:
+            rc = pico_eth_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, mac, c->d_net[b],
+                                             c->d_l4[b], c->d_ver[b], c->st[b]);
+            break;
+        }
+        if (rc)
+            break;
+#define D2H(dst, src, bytes)                                                                              \
+        if ((dst) && (e = hipMemcpyAsync((dst), (src), (bytes), hipMemcpyDeviceToHost, c->st[b])) != hipSuccess) \
+            return fail(PICO_CSUM_EIO, "%s: D2H: %s", what, hipGetErrorString(e));
+        D2H(out ? out + i : NULL, c->d_l4[b], (size_t)cnt * 2u)
+        D2H(out_net ? out_net + i : NULL, c->d_net[b], (size_t)cnt * 2u)
+        D2H(out_l4 ? out_l4 + i : NULL, c->d_l4[b], (size_t)cnt * 2u)
+        D2H(verdict ? verdict + i : NULL, c->d_ver[b], (size_t)cnt)
+        if ((flags & PICO_CSUM_F_WRITE) && hi > lo)
+            D2H((uint8_t *)base + lo, c->d_buf[b], hi - lo)
+#undef D2H
+        if (hipEventRecord(c->done[b], c->st[b]) != hipSuccess)
+            return fail(PICO_CSUM_EIO, "%s: event record failed", what);
+        i = j;
+        b ^= 1;
+    }
+    if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
+        if (!rc) rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
+    return rc;
+}
+
+int pico_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                             const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
+                             uint16_t *out)
+{
+    if (!out)
+        return fail(PICO_CSUM_EINVAL, "NULL argument");
+    return desc_batch_host(ctx, HB_RAW, base, base_len, desc, n, crc_off, flags, NULL, out, NULL, NULL, NULL,
+                           "pico_checksum_batch_host");
+}
+
+int pico_ipv4_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                  const struct pico_csum_desc *desc, uint32_t n, uint32_t flags, uint16_t *out_net,
+                                  uint16_t *out_transport, uint8_t *verdict)
+{
+    return desc_batch_host(ctx, HB_IPV4, base, base_len, desc, n, -1, flags, NULL, NULL, out_net, out_transport,
+                           verdict, "pico_ipv4_checksum_batch_host");
+}
+
+int pico_ipv6_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                  const struct pico_csum_desc *desc, uint32_t n, uint32_t flags,
+                                  uint16_t *out_transport, uint8_t *verdict)
+{
+    return desc_batch_host(ctx, HB_IPV6, base, base_len, desc, n, -1, flags, NULL, NULL, NULL, out_transport, verdict,
+                           "pico_ipv6_checksum_batch_host");
+}
+
+int pico_eth_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
+                                 const struct pico_csum_desc *desc, uint32_t n, uint32_t flags, const uint8_t *mac,
+                                 uint16_t *out_net, uint16_t *out_transport, uint8_t *verdict)
+{
+    return desc_batch_host(ctx, HB_ETH, base, base_len, desc, n, -1, flags, mac, NULL, out_net, out_transport,
+                           verdict, "pico_eth_checksum_batch_host");
 }

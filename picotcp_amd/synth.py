@@ -220,3 +220,79 @@ def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")
         buf[int(off[i]):int(off[i]) + frames[i].size] = frames[i]
     flen = np.array([f.size for f in frames], dtype=np.uint32)
     return buf, off, flen, seeds, kind
+
+
+def _ones_sum(data: np.ndarray, seed: int = 0) -> int:
+    """pico_checksum_adder over data (LE 16-bit words, odd trailing byte low), mod 2^32."""
+    n = data.size
+    s = int(data[: n & ~1].view("<u2").astype(np.uint64).sum()) if n >= 2 else 0
+    if n & 1:
+        s += int(data[-1])
+    return (seed + s) & 0xFFFFFFFF
+
+
+def _finalize(s: int) -> int:
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    c = ~s & 0xFFFF
+    return ((c >> 8) | (c << 8)) & 0xFFFF
+
+
+def ipv4_fragments(lengths, seed: int = 21, proto: int = 17, frag_payload: int = 1480, shuffle: bool = True,
+                   valid: bool = True):
+    """IPv4 datagrams of the given TRANSPORT lengths, each split into fragments of
+    `frag_payload` bytes (a multiple of 8; the last one shorter) as a sender's
+    pico_ipv4_fragment / an MTU-1500 path produces them, every fragment an IPv4 frame
+    (14-byte Ethernet gap, 20-byte header: tot = 20 + payload, frag = MF | offset/8, same
+    id / src / dst / proto).  With `valid` the transport carries a correct TCP / UDP
+    checksum over the whole datagram.  Fragments of a datagram are placed in the buffer
+    (and listed) in a seeded arrival order when `shuffle`.
+    Returns (buffer, frag offsets uint64 (-> IPv4 header), frag bytes uint32, groups
+    uint32[n, 2] = (first descriptor, count) per datagram)."""
+    lengths = np.asarray(lengths, dtype=np.uint32)
+    assert frag_payload % 8 == 0 and frag_payload > 0
+    rng = np.random.default_rng(seed)
+    pieces, groups = [], []
+    for g, L in enumerate(lengths.tolist()):
+        t = random_bytes(seed * 1000003 + g, L)
+        src = bytes([10, int(rng.integers(256)), int(rng.integers(256)), 1])
+        dst = bytes([192, 168, int(rng.integers(256)), 2])
+        if proto == 6 and L >= 20:
+            t[12], t[13], t[16], t[17] = 0x50, 0x18, 0, 0
+        if proto == 17 and L >= 8:
+            t[4], t[5], t[6], t[7] = (L >> 8) & 0xFF, L & 0xFF, 0, 0
+        if valid and proto in (6, 17) and L >= (20 if proto == 6 else 8):
+            ph = np.frombuffer(src + dst + bytes([0, proto, (L >> 8) & 0xFF, L & 0xFF]), np.uint8)
+            c = _finalize(_ones_sum(t, _ones_sum(ph)))
+            x = 16 if proto == 6 else 6
+            t[x], t[x + 1] = c >> 8, c & 0xFF
+        ident = int(rng.integers(1, 65536))
+        offs = list(range(0, max(L, 1), frag_payload)) if L else [0]
+        frs = []
+        for o in offs:
+            pl = min(frag_payload, L - o)
+            h = np.zeros(20, np.uint8)
+            h[0], h[2], h[3] = 0x45, ((20 + pl) >> 8) & 0xFF, (20 + pl) & 0xFF
+            h[4], h[5], h[8], h[9] = ident >> 8, ident & 0xFF, 64, proto
+            fr = (o >> 3) | (0x2000 if o + pl < L else 0)
+            h[6], h[7] = fr >> 8, fr & 0xFF
+            h[12:16] = np.frombuffer(src, np.uint8)
+            h[16:20] = np.frombuffer(dst, np.uint8)
+            frs.append(np.concatenate([h, t[o:o + pl]]))
+        if shuffle:
+            frs = [frs[i] for i in rng.permutation(len(frs))]
+        groups.append((len(pieces), len(frs)))
+        pieces.extend(frs)
+    n = len(pieces)
+    place = rng.permutation(n) if shuffle else np.arange(n)
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for j in place.tolist():
+        pos += 14
+        off[j] = pos
+        pos += pieces[j].size
+    buf = random_bytes(seed ^ 0xF4A6, pos + 16)
+    for j in range(n):
+        buf[int(off[j]):int(off[j]) + pieces[j].size] = pieces[j]
+    flen = np.array([p.size for p in pieces], dtype=np.uint32)
+    return buf, off, flen, np.array(groups, dtype=np.uint32).reshape(-1, 2)

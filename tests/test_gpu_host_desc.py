@@ -1,0 +1,97 @@
+"""GPU: host-resident descriptor batches (pico_{checksum,ipv4_checksum,ipv6_checksum,
+eth_checksum}_batch_host) -- a burst in host memory, chunked H2D / kernel / D2H over two
+streams -- against the oracle, with a small staging buffer so every burst spans many chunks;
+out-of-bounds and unsorted descriptors; F_WRITE stores written back to host memory."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from picotcp_amd import _lib, batch, synth
+from tests import golden_data as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hb():
+    h = batch.HostBatch(0, staging_bytes=1 << 20)         # 1 MiB: C2-sized bursts take ~90 chunks
+    yield h
+    h.close()
+
+
+def imix_ipv4(n, seed):
+    lens = synth.imix_lengths(n, seed)
+    buf, net, avail = synth.ipv4_batch(lens, seed=seed, proto=6)
+    return buf, batch.make_desc(net, avail)
+
+
+def test_ipv4_host_rx_tx(hb):
+    buf, d = imix_ipv4(100_000, 3)
+    on, ol, v = hb.ipv4_checksum_batch(buf, d, flags=_lib.F_TX)
+    wn, wl, wv = O.batch_ipv4(buf, d, tx=True)
+    np.testing.assert_array_equal(on, wn)
+    np.testing.assert_array_equal(ol, wl)
+    np.testing.assert_array_equal(v, wv)
+    want = buf.copy()
+    hb.ipv4_checksum_batch(buf, d, flags=_lib.F_TX | _lib.F_WRITE)     # crc fields stored in host memory
+    on, ol, v = hb.ipv4_checksum_batch(buf, d)
+    assert (v == 1).all() and (on == 0).all() and (ol == 0).all()
+    assert np.count_nonzero(buf != want) <= 4 * d.size
+    buf[np.random.default_rng(1).integers(0, buf.size, 500)] ^= 0x20
+    on, ol, v = hb.ipv4_checksum_batch(buf, d)
+    wn, wl, wv = O.batch_ipv4(buf, d)
+    np.testing.assert_array_equal(on, wn)
+    np.testing.assert_array_equal(ol, wl)
+    np.testing.assert_array_equal(v, wv)
+
+
+def test_ipv4_host_unsorted_and_out_of_bounds(hb):
+    buf, d = imix_ipv4(20_000, 5)
+    rng = np.random.default_rng(2)
+    d = d[rng.permutation(d.size)]
+    d["off"][::97] = buf.size + 5                           # past base_len -> MALFORMED, unread
+    d["len"][1::101] = buf.size                             # region past base_len
+    on, ol, v = hb.ipv4_checksum_batch(buf, d)
+    oob = (d["off"] > buf.size) | (d["len"].astype(np.uint64) > buf.size - np.minimum(d["off"], buf.size))
+    assert oob.sum() > 300 and (v[oob] == 8).all() and (on[oob] == 0).all() and (ol[oob] == 0).all()
+    wn, wl, wv = O.batch_ipv4(buf, d[~oob])
+    np.testing.assert_array_equal(on[~oob], wn)
+    np.testing.assert_array_equal(ol[~oob], wl)
+    np.testing.assert_array_equal(v[~oob], wv)
+
+
+def test_ipv6_and_eth_host(hb):
+    c6 = G.ipv6_cases()
+    ol, v = hb.ipv6_checksum_batch(c6["buf"], G.ipv6_desc(c6))
+    np.testing.assert_array_equal(ol, c6["rx_l4"])
+    np.testing.assert_array_equal(v, c6["rx_verdict"])
+    ce = G.eth_cases()
+    on, ol, v = hb.eth_checksum_batch(ce["buf"], G.eth_desc(ce), mac=ce["mac"].tobytes())
+    np.testing.assert_array_equal(on, ce["rx_net"])
+    np.testing.assert_array_equal(ol, ce["rx_l4"])
+    np.testing.assert_array_equal(v, ce["rx_verdict"])
+
+
+def test_raw_host_with_write(hb):
+    n = 30_000
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 3)[:-1]]).astype(np.uint64)
+    buf = synth.random_bytes(77, int(offs[-1]) + int(lens[-1]) + 8)
+    d = batch.make_desc(offs, lens, rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32))
+    want = O.batch_raw(buf, d, crc_off=2)
+    out = hb.checksum_batch(buf, d, crc_off=2, flags=_lib.F_WRITE)
+    np.testing.assert_array_equal(out, want)
+    has = lens >= 4
+    o = offs[has].astype(np.int64)
+    np.testing.assert_array_equal((buf[o + 2].astype(np.uint16) << 8) | buf[o + 3], want[has])
+
+
+def test_frame_larger_than_staging_is_einval(hb):
+    buf = np.zeros(3 << 20, np.uint8)
+    d = batch.make_desc([0], [2 << 20])
+    with pytest.raises(_lib.PicoCsumError) as e:
+        hb.checksum_batch(buf, d)
+    assert e.value.rc == -_lib.EINVAL
