@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c3|c3_64k|c3_frag|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
@@ -9,7 +9,9 @@ A step = one pass of the hot path over one batch resident in HBM:
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
   c2tx: the same datagrams, fused TX (checksums computed and written in place)
   c2v6: 256K IMIX+20 B IPv6/TCP datagrams, fused IPv6 pseudo-header RX verify
+  c2eth: the C2 frames through the Ethernet front end (one launch: ethertype dispatch + RX verify)
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
+  c3_reasm: 4K x 64512 B datagrams reassembled from 1480 B fragments + TCP check in the same pass
   c3: 256K x 9000 B jumbo frames;  c3_64k: 16K x 64 KiB reassembled buffers
   c4: 4M x 1500 B frames sharded over the ranks (strong scaling)
 c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame batches
@@ -18,8 +20,9 @@ barrier and the max-over-ranks timing).
 
 Rank 0 prints ONE JSON line.  `roofline` is the checksum kernel's achieved algorithmic HBM
 bandwidth (HIP events bracketing the K timed launches on the launch stream; elapsed / K =
-average launch duration) against the 8.0 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch from profiles/ (gfx950
-FETCH_SIZE x2 correction, rocprofv3 separate passes) when recorded for this config;
+average launch duration) against the 8.0 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch
+from profiles/pmc_traffic.json (FETCH_SIZE x2, calibrated to 128 B per touched line by tools/fetch_calib.py,
++ WRITE_SIZE; separate rocprofv3 passes recorded earlier, named in `traffic_source`) when recorded for this config;
 `cpu_baseline` times the reference's own pico_checksum (compiled from stack/pico_frame.c,
 oracle/_ref) on the host cores over a bounded sample of the same frames.
 """
@@ -62,6 +65,14 @@ CONFIGS = {
     "c3_frag": dict(kind="ipv4", frames=16384, frame_bytes=64512,
                     workload="C3 reassembled: 16K x 64512 B (PICO_IPV4_FRAG_MAX_SIZE) IPv4/TCP datagrams, fused "
                              "IPv4 header + TCP pseudo-header RX verify"),
+    "c2eth": dict(kind="eth", frames=262144,
+                  workload="C2 through the Ethernet front end (SURVEY 8f row 1): the 256K simple-IMIX IPv4/TCP "
+                           "frames, descriptors at the Ethernet header, ethertype dispatch + destination-MAC filter "
+                           "+ fused IPv4 / TCP RX verify in one launch"),
+    "c3_reasm": dict(kind="frag", frames=4096, frame_bytes=64512,
+                     workload="C3 reassembly (SURVEY 8f row 4): 4K x 64512 B IPv4/TCP datagrams arriving as 1480 B "
+                              "fragments (44 per datagram, 14 B Ethernet gap each), gathered into reassembled "
+                              "buffers with the TCP pseudo-header check of each datagram in the same pass"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -124,6 +135,72 @@ def make_c2v6(n, device, seed, keep_host=True):
     return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
 
 
+MAC = bytes.fromhex("02005e0a0b0c")
+
+
+def make_c2eth(n, device, seed, keep_host=True):
+    """The C2 datagrams as Ethernet frames addressed to MAC (descriptors at the frame start)."""
+    lens = synth.imix_lengths(n, seed)
+    buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
+    e = net.astype(np.int64) - 14
+    for k, b in enumerate(MAC):
+        buf[e + k] = b
+    desc = batch.make_desc(net - np.uint64(14), avail + 14)
+    d_buf = torch.from_numpy(buf).to(device)
+    d_desc = batch.desc_to_device(desc, device)
+    batch.eth_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize(device)
+    return d_buf, d_desc, int(lens.sum()) + 14 * n, (buf, desc) if keep_host else None
+
+
+FRAG = 1480                 # fragment payload (MTU 1500 - 20 B header)
+
+
+def make_frag(n, tl, device, seed):
+    """n IPv4/TCP datagrams of tl transport bytes as in-order 1480 B fragments, each behind a
+    14 B gap, built on the device (vectorized); the TCP checksum made valid with one untimed
+    reassembly pass.  Returns (buffer, fragment descriptors, groups, out, out descriptors,
+    fragment count, payload bytes)."""
+    nf = -(-tl // FRAG)
+    pl = np.full(nf, FRAG, np.int64)
+    pl[-1] = tl - FRAG * (nf - 1)
+    fsz = 14 + 20 + pl                                   # bytes per fragment slot
+    per = int(fsz.sum())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    buf = torch.randint(0, 256, (n * per,), dtype=torch.uint8, device=device, generator=g)
+    rel = np.concatenate([[0], np.cumsum(fsz)[:-1]]) + 14          # header offsets in one datagram
+    net = (np.arange(n, dtype=np.int64)[:, None] * per + rel[None, :]).reshape(-1)
+    hdr = np.zeros((n, nf, 20), np.uint8)
+    tot = 20 + pl
+    hdr[:, :, 0] = 0x45
+    hdr[:, :, 2], hdr[:, :, 3] = (tot >> 8)[None, :], (tot & 0xFF)[None, :]
+    ident = (np.arange(n) * 7 + seed) & 0xFFFF
+    hdr[:, :, 4], hdr[:, :, 5] = (ident >> 8)[:, None], (ident & 0xFF)[:, None]
+    frag = ((np.arange(nf) * FRAG) >> 3) | np.where(np.arange(nf) < nf - 1, 0x2000, 0)
+    hdr[:, :, 6], hdr[:, :, 7] = (frag >> 8)[None, :], (frag & 0xFF)[None, :]
+    hdr[:, :, 8], hdr[:, :, 9] = 64, 6
+    hdr[:, :, 12:16] = [10, 1, 2, 3]
+    hdr[:, :, 16:20] = [192, 168, 4, 5]
+    idx = torch.from_numpy((net[:, None] + np.arange(20)[None, :]).reshape(-1)).to(device)
+    buf[idx] = torch.from_numpy(hdr.reshape(-1)).to(device)
+    crc = torch.from_numpy(np.stack([net[::nf] + 20 + 16, net[::nf] + 20 + 17], 1).reshape(-1)).to(device)
+    buf[crc] = 0                                         # TCP crc of each datagram (first fragment)
+    desc = batch.make_desc(net.astype(np.uint64), np.repeat(tot[None, :], n, 0).reshape(-1))
+    grp = np.stack([np.arange(n) * nf, np.full(n, nf)], 1).astype(np.uint32).reshape(-1)
+    cap = (20 + tl + 15) // 16 * 16
+    od = batch.make_desc(np.arange(n, dtype=np.uint64) * cap, np.full(n, cap))
+    d_desc, d_od = batch.desc_to_device(desc, device), batch.desc_to_device(od, device)
+    d_grp = torch.from_numpy(grp.view(np.int32)).to(device)
+    out = torch.empty(n * cap, dtype=torch.uint8, device=device)
+    _, l4, _ = batch.ipv4_reassemble_batch(buf, d_desc, n * nf, d_grp, out, d_od)
+    c = l4.view(torch.int16).to(torch.int32) & 0xFFFF                # value to store: short_be(c)
+    buf[crc[0::2]] = (c >> 8).to(torch.uint8)
+    buf[crc[1::2]] = (c & 0xFF).to(torch.uint8)
+    torch.cuda.synchronize(device)
+    return buf, d_desc, d_grp, out, d_od, n * nf, n * tl
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -177,15 +254,17 @@ def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
     return out
 
 
-def cpu_baseline_fused(host, ipv6: bool, tx: bool, target_s: float):
-    """The oracle's fused IPv4/IPv6 restatement (oracle/pico_csum_oracle.c, a port of the
-    reference's callers over its pico_checksum) on 1 host core over a bounded sample
+def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float):
+    """The oracle's fused IPv4/IPv6/Ethernet restatement (oracle/pico_csum_oracle.c, a port of
+    the reference's callers over its pico_checksum) on 1 host core over a bounded sample
     of the same datagrams (the reference's own IPv4/TCP modules need the whole stack)."""
     from oracle import oracle as O
     buf, desc = host
     k = min(desc.size, 65536)
     sample, nbytes = desc[:k], int(desc["len"][:k].astype(np.int64).sum())
-    fn = (lambda: O.batch_ipv6(buf, sample, tx=tx)) if ipv6 else (lambda: O.batch_ipv4(buf, sample, tx=tx))
+    ipv6 = kind == "ipv6"
+    fn = {"ipv6": lambda: O.batch_ipv6(buf, sample, tx=tx), "ipv4": lambda: O.batch_ipv4(buf, sample, tx=tx),
+          "eth": lambda: O.batch_eth(buf, sample, mac=MAC, tx=tx)}[kind]
     t0 = time.perf_counter()
     fn()
     reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))
@@ -195,7 +274,57 @@ def cpu_baseline_fused(host, ipv6: bool, tx: bool, target_s: float):
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {k} datagrams of the batch ({nbytes / 2**20:.0f} MiB), oracle fused "
-                      f"{'IPv6' if ipv6 else 'IPv4'} {'TX' if tx else 'RX'} restatement, gcc -O3, 1 thread, {reps} passes"}
+                      f"{ {'ipv6': 'IPv6', 'ipv4': 'IPv4', 'eth': 'Ethernet + IPv4/IPv6'}[kind]} "
+                      f"{'TX' if tx else 'RX'} restatement, gcc -O3, 1 thread, {reps} passes"}
+
+
+def cpu_baseline_frag(st, target_s: float):
+    """The oracle's reassembly restatement (memcpy gather + pico_checksum of the reassembled
+    transport, as pico_fragments_reassemble + pico_transport_crc_check do) on 1 host core
+    over the first 256 datagrams of the batch."""
+    from oracle import oracle as O
+    b, d, gr, o, od, nfr, payload = st
+    n = gr.numel() // 2
+    k = min(n, 256)
+    grp = gr.cpu().numpy().view(np.uint32)[:2 * k]
+    nf_used = int(grp[-2] + grp[-1])
+    desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
+    hi = int(desc["off"][-1]) + int(desc["len"][-1])
+    host = b[:hi].cpu().numpy()
+    odh = od.cpu().numpy().view(batch.DESC_DTYPE)[:k]
+    outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
+    nbytes = payload // n * k
+    t0 = time.perf_counter()
+    O.ipv4_reassemble(host, desc, grp, outh, odh)
+    reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        O.ipv4_reassemble(host, desc, grp, outh, odh)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload), oracle reassembly restatement "
+                      f"(sort, memcpy gather, pico_checksum of the transport), gcc -O3, 1 thread, {reps} passes"}
+
+
+def e2e_rate_desc(host):
+    """Host-resident fused IPv4 path (pico_ipv4_checksum_batch_host): the C2 burst in pinned
+    host memory -> chunked H2D -> fused kernel -> D2H of the per-frame results."""
+    buf, desc = host
+    pinned = torch.from_numpy(buf).pin_memory()
+    hb = batch.HostBatch(torch.cuda.current_device(), staging_bytes=64 << 20)
+    try:
+        hb.ipv4_checksum_batch(pinned.numpy(), desc)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            hb.ipv4_checksum_batch(pinned.numpy(), desc)
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        hb.close()
+    nbytes = int(desc["len"].astype(np.int64).sum())
+    return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "datagrams": int(desc.size),
+            "path": "pico_ipv4_checksum_batch_host: pinned host burst -> H2D (64 MiB chunks, rebased "
+                    "descriptors) -> fused IPv4/TCP RX kernel -> D2H of out_net/out_transport/verdict, 2 streams"}
 
 
 def e2e_rate(n, ln):
@@ -218,15 +347,22 @@ def e2e_rate(n, ln):
 
 
 def load_traffic(config: str):
+    """(HBM bytes per launch, source) from profiles/pmc_traffic.json: rocprofv3 PMC passes of this
+    config recorded on an earlier box (FETCH_SIZE x2 calibrated to 128 B per touched line, plus
+    WRITE_SIZE); not measured by this run -- PMC counters need their own rocprofv3 passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
             rec = json.load(f).get(config)
-        return None if rec is None else rec.get("hbm_bytes_per_launch")
+        if rec is None:
+            return None, None
+        return rec.get("hbm_bytes_per_launch"), (f"profiles/pmc_traffic.json round {rec.get('round')}: rocprofv3 "
+                                                  "--pmc FETCH_SIZE (x2, line-calibrated) + WRITE_SIZE, separate "
+                                                  "passes of this config, recorded earlier (not this run)")
     except Exception:
-        return None
+        return None, None
 
 
 def _free_port() -> int:
@@ -320,6 +456,34 @@ def main():
         frame_bytes = sets[0][2]
         # datagrams + descriptors + (2+2+1) B results (+ the two 2-byte crc fields written in place on TX)
         algo_bytes = frame_bytes + 16 * n + 5 * n + (4 * n if cfg.get("tx") else 0)
+    elif cfg["kind"] == "eth":
+        n = cfg["frames"]
+        ln = 0
+        rot = a.rotate or rotation(n * (IMIX_MEAN + 14))
+        sets = [make_c2eth(n, dev, 500 + 13 * rank + i, keep_host=i == 0) for i in range(rot)]
+        outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
+
+        def step(i):
+            b, d, _, _ = sets[i % rot]
+            batch.eth_checksum_batch(b, d, n, mac=MAC, out=outs[i % rot])
+        frame_bytes = sets[0][2]
+        algo_bytes = frame_bytes + 16 * n + 5 * n            # frames + descriptors + (2+2+1) B results
+    elif cfg["kind"] == "frag":
+        n, ln = cfg["frames"], cfg["frame_bytes"]
+        rot = a.rotate or max(2, rotation(2 * n * ln))
+        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i) for i in range(rot)]
+        res = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+                torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
+
+        def step(i):
+            b, d, gr, o, od, nfr, _ = sets[i % rot]
+            batch.ipv4_reassemble_batch(b, d, nfr, gr, o, od, results=res[i % rot])
+        frame_bytes = sets[0][6]
+        nfr = sets[0][5]
+        # payload read + written, fragment headers (20 B) + descriptors (16 B) read, 2 x 4 B group,
+        # 20 B header written, (4+2+1) B results
+        algo_bytes = 2 * frame_bytes + 36 * nfr + 8 * n + 20 * n + 7 * n
     else:
         n = cfg["frames"]
         ln = 0
@@ -372,6 +536,7 @@ def main():
     value = total_bytes / (ms_per_step / 1e3) / GIB
 
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+    traffic, traffic_src = load_traffic(a.config)
     out = None
     if rank == 0:
         out = {
@@ -383,7 +548,7 @@ def main():
                        "batch_bytes_per_gpu": frame_bytes, "rotating_batches": rot,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(a.config),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_avg_us": round(kern_ms * 1e3, 2), "kernel_avg_us_max_rank": round(kern_max_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": algo_bytes},
         }
@@ -394,9 +559,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(sample, ln, a.cpu_seconds)
         if not a.no_e2e:
             out["e2e_host_to_host"] = e2e_rate(n, ln)
-    elif rank == 0 and world == 1 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline_fused(sets[0][3], cfg["kind"] == "ipv6", bool(cfg.get("tx")),
-                                                 a.cpu_seconds / 2)
+    elif rank == 0 and world == 1 and cfg["kind"] in ("ipv4", "ipv6", "eth"):
+        if not a.no_cpu:
+            out["cpu_baseline"] = cpu_baseline_fused(sets[0][3], cfg["kind"], bool(cfg.get("tx")),
+                                                     a.cpu_seconds / 2)
+        if not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not ln:
+            out["e2e_host_to_host"] = e2e_rate_desc(sets[0][3])
+    elif rank == 0 and world == 1 and cfg["kind"] == "frag" and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_frag(sets[0], a.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -12,6 +12,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpicocsum.so")
+# A/B measurement only (tools/ab_lib.sh): another build of the same library
+if os.environ.get("PICO_CSUM_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["PICO_CSUM_LIB"])
 
 # Public symbols declared by include/pico_csum.h (checked by tests/test_abi.py).
 EXPORTED = (

@@ -157,6 +157,17 @@ def ipv6_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: i
     return out_l4, verdict
 
 
+_MACS: dict = {}
+
+
+def _mac_buf(mac: bytes):
+    """A ctypes copy of a 6-byte MAC, built once per address (launch overhead stays below the kernel's)."""
+    b = _MACS.get(mac)
+    if b is None:
+        b = _MACS[mac] = ctypes.create_string_buffer(mac, 6)
+    return b
+
+
 def eth_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: int = 0, mac: bytes | None = None,
                        stream=None, out=None):
     """Ethernet front end + fused IPv4 / IPv6 checksums in one launch (pico_ethernet.c:180-235):
@@ -177,7 +188,7 @@ def eth_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: in
     for t, nm, sz in ((out_net, "out_net", 2), (out_l4, "out_transport", 2), (verdict, "verdict", 1)):
         _check_out(t, n, nm, dev, sz)
     lib = _lib.load()
-    m = None if mac is None else ctypes.create_string_buffer(bytes(mac), 6)
+    m = None if mac is None else _mac_buf(bytes(mac))
     _lib.check("pico_eth_checksum_batch_dev",
                lib.pico_eth_checksum_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, flags, m, _ptr(out_net),
                                                _ptr(out_l4), _ptr(verdict), _stream_handle(stream)))

@@ -168,7 +168,7 @@ def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = T
 
 
 ETH_KINDS = ("ipv4_tcp", "ipv4_udp", "ipv4_icmp", "ipv6_tcp", "ipv6_udp", "ipv6_icmp", "ipv6_hbh_tcp", "arp",
-             "lldp", "ipv4_bad_version")
+             "lldp", "ipv4_bad_version", "ipv4_opt_tcp", "ipv4_opt_udp")
 
 
 def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")):
@@ -188,8 +188,11 @@ def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")
         k = ETH_KINDS[kind[i]]
         s = seed * 7919 + i
         if k.startswith("ipv4"):
-            proto = {"ipv4_tcp": 6, "ipv4_udp": 17, "ipv4_icmp": 1, "ipv4_bad_version": 6}[k]
-            b, _, _ = ipv4_batch(np.array([max(int(lens[i]), 48)], np.uint32), seed=s, proto=proto, eth=True)
+            proto = {"ipv4_tcp": 6, "ipv4_udp": 17, "ipv4_icmp": 1, "ipv4_bad_version": 6, "ipv4_opt_tcp": 6,
+                     "ipv4_opt_udp": 17}[k]
+            ihl = int(rng.integers(6, 16)) if "opt" in k else 5
+            b, _, _ = ipv4_batch(np.array([max(int(lens[i]), 4 * ihl + 28)], np.uint32), seed=s, proto=proto, eth=True,
+                                 ihl=ihl)
             if k == "ipv4_bad_version":
                 b[14] = 0x65
         elif k.startswith("ipv6"):

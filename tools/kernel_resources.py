@@ -55,3 +55,30 @@ if __name__ == "__main__":
         if sub in k["name"]:
             print(f'{k["name"][:90]:90s} vgpr {k["vgpr"]:>4} vspill {k["vspill"]:>3} sgpr {k["sgpr"]:>3} '
                   f'sspill {k["sspill"]:>3} lds {k["lds"]:>6} scratch {k["scratch"]}')
+
+
+def disasm(kernel_substr: str, so: str = os.path.join(ROOT, "picotcp_amd", "libpicocsum.so")) -> str:
+    """llvm-objdump of the first kernel whose symbol contains kernel_substr."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fatbin")
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", so, fb], check=True)
+        blob = open(fb, "rb").read()
+        starts, i = [], blob.find(magic)
+        while i >= 0:
+            starts.append(i)
+            i = blob.find(magic, i + 1)
+        for k, a in enumerate(starts):
+            b = starts[k + 1] if k + 1 < len(starts) else len(blob)
+            part, co = os.path.join(d, f"b{k}"), os.path.join(d, f"k{k}.co")
+            open(part, "wb").write(blob[a:b])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+            txt = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                                 capture_output=True, text=True).stdout
+            blocks = txt.split("\n\n")
+            for blk in blocks:
+                head = blk.strip().split("\n", 1)[0]
+                if kernel_substr in head and head.endswith(">:"):
+                    return blk
+    return ""

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs: per counter, the median over the checksum kernel's dispatches."""
+"""Summarise rocprofv3 --pmc CSVs (one directory per run under ROOT): per counter, the median over
+the checksum kernel's dispatches (the kernel with the most dispatches in the run)."""
 import csv
 import glob
 import os
@@ -9,8 +10,8 @@ import sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 res = {}
 for f in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv"))):
-    name = os.path.basename(os.path.dirname(f)).rsplit("_", 1)[0]
-    rows = [r for r in csv.DictReader(open(f)) if "csum" in r["Kernel_Name"]]
+    name = os.path.basename(os.path.dirname(f))
+    rows = [r for r in csv.DictReader(open(f)) if "csum" in r["Kernel_Name"] or "reassemble" in r["Kernel_Name"]]
     # the measured kernel: the one with the most dispatches (setup launches differ)
     counts = {}
     for r in rows:

@@ -39,7 +39,7 @@ def main():
     by = {}
     for r in rows:
         nm = r["Kernel_Name"]
-        if "csum" in nm or "forward_kernel" in nm:
+        if "csum" in nm or "forward_kernel" in nm or "reassemble" in nm:
             by.setdefault(nm, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     kern = max(by, key=lambda k: len(by[k]))
     disp = sorted(by[kern])

@@ -72,6 +72,25 @@ def main():
             b, d = sets[i % rot]
             batch.ipv6_checksum_batch(b, d, n)
         algo = int(lens.sum()) + 19 * n
+    elif a.config == "c2eth":
+        # the C2 datagrams through the Ethernet front end (descriptors -> frame start)
+        n = 262144
+        lens = synth.imix_lengths(n, 3)
+        rot = a.rotate
+        sets = []
+        for r in range(rot):
+            buf, net, avail = synth.ipv4_batch(lens, seed=10 + r, proto=6, eth=True)
+            d_buf = torch.from_numpy(buf).to(dev)
+            d_desc = batch.desc_to_device(batch.make_desc(net - np.uint64(14), avail + 14), dev)
+            batch.eth_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+            sets.append((d_buf, d_desc))
+        o3 = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+               torch.empty(n, dtype=torch.uint8, device=dev)) for r in range(rot)]
+
+        def launch(i):
+            b, d = sets[i % rot]
+            batch.eth_checksum_batch(b, d, n, out=o3[i % rot])
+        algo = int(lens.sum()) + 14 * n + 16 * n + 5 * n
     elif a.config in ("c2raw", "c2", "c2tx", "c2txnw"):
         n = 262144
         lens = synth.imix_lengths(n, 3)
