@@ -188,8 +188,10 @@ def make_frag(n, tl, device, seed):
     buf[crc] = 0                                         # TCP crc of each datagram (first fragment)
     desc = batch.make_desc(net.astype(np.uint64), np.repeat(tot[None, :], n, 0).reshape(-1))
     grp = np.stack([np.arange(n) * nf, np.full(n, nf)], 1).astype(np.uint32).reshape(-1)
-    cap = (20 + tl + 15) // 16 * 16
-    od = batch.make_desc(np.arange(n, dtype=np.uint64) * cap, np.full(n, cap))
+    cap = (20 + tl + 15) // 16 * 16 + 16
+    # each reassembled datagram at 12 mod 16, so that its transport (behind the 20 B header) is
+    # 16-byte aligned: the gather then stores whole 16-byte units wherever a fragment's place is
+    od = batch.make_desc(np.arange(n, dtype=np.uint64) * cap + np.uint64(12), np.full(n, cap - 12))
     d_desc, d_od = batch.desc_to_device(desc, device), batch.desc_to_device(od, device)
     d_grp = torch.from_numpy(grp.view(np.int32)).to(device)
     out = torch.empty(n * cap, dtype=torch.uint8, device=device)
@@ -304,6 +306,26 @@ def cpu_baseline_frag(st, target_s: float):
     return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload), oracle reassembly restatement "
                       f"(sort, memcpy gather, pico_checksum of the transport), gcc -O3, 1 thread, {reps} passes"}
+
+
+def copy_ceiling(nbytes: int, dev) -> dict:
+    """The device's own contiguous copy (torch copy_ = a HIP D2D copy kernel) of the payload bytes the
+    reassembly moves (read + write), timed the same way: the practical ceiling of a gather."""
+    rot = max(3, -(-(1 << 30) // nbytes))
+    src = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(rot)]
+    dst = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(rot)]
+    for i in range(10):
+        dst[i % rot].copy_(src[i % rot])
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    k = 50
+    for i in range(k):
+        dst[i % rot].copy_(src[i % rot])
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    us = ev0.elapsed_time(ev1) / k * 1e3
+    return {"copy_us": round(us, 2), "copy_GBs": round(2 * nbytes / us / 1e3, 1),
+            "what": f"torch copy_ of {nbytes} B (read + write), {rot} rotating buffers, HIP events"}
 
 
 def e2e_rate_desc(host):
@@ -565,8 +587,10 @@ def main():
                                                      a.cpu_seconds / 2)
         if not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not ln:
             out["e2e_host_to_host"] = e2e_rate_desc(sets[0][3])
-    elif rank == 0 and world == 1 and cfg["kind"] == "frag" and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline_frag(sets[0], a.cpu_seconds / 2)
+    elif rank == 0 and world == 1 and cfg["kind"] == "frag":
+        if not a.no_cpu:
+            out["cpu_baseline"] = cpu_baseline_frag(sets[0], a.cpu_seconds / 2)
+        out["roofline"]["copy_ceiling"] = copy_ceiling(sets[0][6], dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -210,7 +210,8 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
  *              IPv4 header, desc.len = bytes available; header already checked)
  *   d_groups[] 2 uint32 per datagram: first fragment, count -- the fragments one reassembly
  *              tree collects (src / dst / id matched by the stack), in arrival order
- *   d_out_desc[] per datagram: output region in d_out (off a multiple of 4, len = capacity)
+ *   d_out_desc[] per datagram: output region in d_out (off a multiple of 4, len = capacity;
+ *              off = 12 mod 16 puts the transport on a 16-byte line: whole-line stores)
  * Tree order by fragment offset ((frag & 0x1FFF) << 3; a repeated offset keeps the earlier
  * arrival, as pico_tree_insert rejects the later); complete when the offsets are contiguous
  * from 0 up to the first fragment without MF.  The output is the first fragment's 20 header

@@ -9,16 +9,21 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// One wave per datagram (its fragments are a contiguous descriptor range, arrival order):
-//   1. lane j parses fragment j's header (IHL, total length, MF, offset) into LDS;
+// One workgroup (4 waves) per datagram (its fragments are a contiguous descriptor range, in
+// arrival order):
+//   1. wave 0, lane j parses fragment j's header (IHL, total length, MF, offset) into LDS;
 //   2. tree order: rank by offset among the first arrivals of each offset (pico_tree_insert
 //      rejects a repeated key), LDS broadcast reads, O(count^2 / 64) per lane;
 //   3. completeness: a wave prefix scan of the sorted transport lengths against the
 //      offsets, up to the first fragment without MF (must be the last in tree order);
-//   4. gather: the first fragment's 20 header bytes, then fragment by fragment one dword
-//      per lane per step (unaligned source: two aligned loads + alignbyte; the datagram's
-//      transport starts 4-byte aligned, offsets are multiples of 8, so every dword is a
-//      whole pair of checksum words), v_dot2 sums on the fly, a wave reduction at the end.
+//   4. gather, all 4 waves, fragment-major (wave w takes fragments w, w + 4, ...): a
+//      fragment's payload in 16-byte units, 2 x 64 units per wave per step, every load
+//      issued before any is used: two aligned 16-byte loads through a buffer window over the
+//      payload (out-of-range slots read zeros, no branches) and a shift by the payload's
+//      alignment (wave-uniform per fragment: dword select + alignbyte); stores are 8-byte
+//      (or 4-byte) at the unit's place in the transport, which starts 4-byte aligned,
+//      offsets being multiples of 8; v_dot2 sums on the fly (every unit is a whole number of
+//      checksum words); a workgroup reduction through LDS at the end.
 #include "pico_csum_dev.h"
 
 namespace {
@@ -40,163 +45,229 @@ struct FragArgs {
     uint8_t* verdict;
 };
 
-struct FragWaveLds {
+struct FragLds {
     uint32_t key[FRAG_MAX];   // offset | MF << 16 | header length << 17 | dup << 24
     uint32_t tl[FRAG_MAX];    // transport length
     uint16_t sidx[FRAG_MAX];  // tree position -> fragment
+    uint32_t bm[FRAG_MAX];    // tree position -> bookmark (the fragment's place in the transport)
+    uint64_t src[FRAG_MAX];   // fragment -> payload address (no descriptor re-read in the gather)
+    uint32_t m, len, bad, proto, pseudo;
+    uint32_t acc[4], w1[4];
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*p; }
 
-// The dword at byte address a (any alignment) of the region [lo, hi): two aligned loads and
-// alignbyte; the second load only where the dword reaches into it (never past the region's
-// last 4-byte word, so never into an unmapped page).
-__device__ __forceinline__ uint32_t ld_unaligned(const uint8_t* a, const uint8_t* hi) {
-    const uintptr_t ua = reinterpret_cast<uintptr_t>(a);
-    const uint32_t sh = (uint32_t)(ua & 3u);
-    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(ua & ~(uintptr_t)3);
-    const uint32_t* w1 = (sh != 0 && reinterpret_cast<const uint8_t*>(w0 + 1) < hi) ? w0 + 1 : w0;
-    return __builtin_amdgcn_alignbyte(*w1, *w0, sh);
-}
-
 __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
-    __shared__ FragWaveLds lds_all[4];
-    const uint32_t lane = threadIdx.x & 63u;
-    FragWaveLds& L = lds_all[threadIdx.x >> 6];
-    const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (g >= p.n_dgram) return;
+    __shared__ FragLds L;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x;
+    if (g >= p.n_dgram) return;                       // workgroup-uniform
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
-    bool bad = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first;
 
-    // ---- 1. parse (pico_ipv4_process_in: net_len, transport_len = tot - net_len, frag)
-    if (!bad) {
-        bool b = false;
-        for (uint32_t j = lane; j < cnt; j += 64u) {
-            const pico_csum_desc_dev d = p.frag[first + j];
-            uint32_t key = 0, tl = 0;
-            if (d.len < 20u || d.off > p.base_len || d.len > p.base_len - d.off) {
-                b = true;
-            } else {
-                const uint8_t* h = p.base + d.off;
-                const uint32_t ihl = ld_u8(h) & 0x0Fu;
-                const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-                tl = ((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl;
-                tl &= 0xFFFFu;
-                const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
-                key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u) | (hl << 17);
-                if (hl + tl > d.len) b = true;
+    if (wv == 0) {
+        bool bad = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first;
+        // ---- 1. parse (pico_ipv4_process_in: net_len, transport_len = tot - net_len, frag)
+        if (!bad) {
+            bool b = false;
+            for (uint32_t j = lane; j < cnt; j += 64u) {
+                const pico_csum_desc_dev d = p.frag[first + j];
+                uint32_t key = 0, tl = 0;
+                if (d.len < 20u || d.off > p.base_len || d.len > p.base_len - d.off) {
+                    b = true;
+                } else {
+                    const uint8_t* h = p.base + d.off;
+                    const uint32_t ihl = ld_u8(h) & 0x0Fu;
+                    const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                    tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
+                    const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
+                    key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u) | (hl << 17);
+                    if (hl + tl > d.len) b = true;
+                }
+                L.key[j] = key;
+                L.tl[j] = tl;
+                L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + (key >> 17);
             }
-            L.key[j] = key;
-            L.tl[j] = tl;
-        }
-        bad = __builtin_amdgcn_ballot_w64(b) != 0;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-
-    // ---- 2. tree order: repeated offsets keep the earliest arrival; rank among the kept
-    uint32_t m = 0;
-    if (!bad) {
-        for (uint32_t j = lane; j < cnt; j += 64u) {
-            const uint32_t fj = L.key[j] & 0xFFFFu;
-            bool dup = false;
-            for (uint32_t k = 0; k < j; ++k) dup |= (L.key[k] & 0xFFFFu) == fj;
-            if (dup) L.key[j] |= 1u << 24;
+            bad = __builtin_amdgcn_ballot_w64(b) != 0;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
-        uint32_t kept = 0;
-        for (uint32_t j = lane; j < cnt; j += 64u) {
-            const uint32_t kj = L.key[j];
-            if (kj >> 24) continue;
-            uint32_t r = 0;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const uint32_t kk = L.key[k];
-                r += ((kk >> 24) == 0 && (kk & 0xFFFFu) < (kj & 0xFFFFu)) ? 1u : 0u;
-            }
-            L.sidx[r] = (uint16_t)j;
-            ++kept;
-        }
-        m = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(kept), 63);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
 
-    // ---- 3. completeness (pico_fragments_check_complete): offset == bookmark up to the
-    //         first fragment without MF, which must be the last one in tree order
-    uint32_t len = 0;
-    if (!bad) {
-        uint32_t carry = 0, e = NONE;
-        bool gap = false;
-        for (uint32_t i0 = 0; i0 < m && e == NONE; i0 += 64u) {
-            const uint32_t i = i0 + lane;
-            const bool in = i < m;
-            const uint32_t j = in ? L.sidx[i] : 0u;
-            const uint32_t kj = in ? L.key[j] : 0u, tl = in ? L.tl[j] : 0u;
-            const uint32_t incl = wave_scan_add(tl);
-            const uint32_t P = carry + incl - tl;
-            const uint64_t last = __builtin_amdgcn_ballot_w64(in && !(kj & (1u << 16)));
-            const uint32_t le = last ? (uint32_t)__builtin_ctzll(last) : 64u;     // first MF-clear lane
-            gap |= __builtin_amdgcn_ballot_w64(in && lane <= le && (kj & 0xFFFFu) != P) != 0;
-            if (last) {
-                e = i0 + le;
-                len = (uint32_t)__builtin_amdgcn_readlane((int)(P + tl), (int)le);
+        // ---- 2. tree order: repeated offsets keep the earliest arrival; rank among the kept
+        uint32_t m = 0;
+        if (!bad) {
+            for (uint32_t j = lane; j < cnt; j += 64u) {
+                const uint32_t fj = L.key[j] & 0xFFFFu;
+                bool dup = false;
+                for (uint32_t k = 0; k < j; ++k) dup |= (L.key[k] & 0xFFFFu) == fj;
+                if (dup) L.key[j] |= 1u << 24;
             }
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        }
-        bad = gap || e == NONE || e + 1u != m || 20u + len > 0xFFFFu || od.len < 20u + len ||
-              (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off;
-    }
-
-    // ---- 4. gather + checksum
-    uint32_t acc = 0, w1 = 0;
-    uint32_t proto = 0, pseudo = 0;
-    if (!bad) {
-        uint8_t* dst = p.out + od.off;
-        const pico_csum_desc_dev d0 = p.frag[first + L.sidx[0]];
-        const uint8_t* h0 = p.base + d0.off;
-        // the first fragment's PICO_SIZE_IP4HDR bytes (pico_fragments.c:332-333)
-        const uint32_t hb = lane < 20u ? ld_u8(h0 + lane) : 0u;
-        if (lane < 20u) dst[lane] = (uint8_t)hb;
-        proto = (uint32_t)__shfl((int)hb, 9);
-        // pseudo header (struct pico_ipv4_pseudo_hdr) as LE words: src, dst, proto << 8, bswap16(len)
-        const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
-        pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) + (proto << 8) +
-                 (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
-        uint8_t* t = dst + 20;
-        uint32_t at = 0;                                   // bookmark (== the fragment's offset)
-        for (uint32_t i = 0; i < m; ++i) {
-            const uint32_t j = L.sidx[i];
-            const uint32_t hl = (L.key[j] >> 17) & 0x7Fu, tl = L.tl[j];
-            const pico_csum_desc_dev d = p.frag[first + j];
-            const uint8_t* src = p.base + d.off + hl;
-            const uint8_t* src_end = src + tl;
-            for (uint32_t w = lane; 4u * w < tl; w += 64u) {
-                const uint32_t b0 = 4u * w, nb = min(4u, tl - b0);
-                uint32_t v = ld_unaligned(src + b0, src_end);
-                if (nb < 4u) v &= (1u << (8u * nb)) - 1u;
-                if (nb == 4u) {
-                    *reinterpret_cast<uint32_t*>(t + at + b0) = v;
-                } else {
-                    for (uint32_t q = 0; q < nb; ++q) t[at + b0 + q] = (uint8_t)(v >> (8u * q));
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            uint32_t kept = 0;
+            for (uint32_t j = lane; j < cnt; j += 64u) {
+                const uint32_t kj = L.key[j];
+                if (kj >> 24) continue;
+                uint32_t r = 0;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const uint32_t kk = L.key[k];
+                    r += ((kk >> 24) == 0 && (kk & 0xFFFFu) < (kj & 0xFFFFu)) ? 1u : 0u;
                 }
-                acc = dot2_add(v, acc);                    // at + b0 is even: frame-relative pairs
-                if (at + b0 == 4u) w1 = v;                 // transport bytes 4..7 (UDP crc: 6, 7)
+                L.sidx[r] = (uint16_t)j;
+                ++kept;
             }
-            at += tl;
+            m = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(kept), 63);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+
+        // ---- 3. completeness (pico_fragments_check_complete): offset == bookmark up to the
+        //         first fragment without MF, which must be the last one in tree order
+        uint32_t len = 0;
+        if (!bad) {
+            uint32_t carry = 0, e = NONE;
+            bool gap = false;
+            for (uint32_t i0 = 0; i0 < m && e == NONE; i0 += 64u) {
+                const uint32_t i = i0 + lane;
+                const bool in = i < m;
+                const uint32_t j = in ? L.sidx[i] : 0u;
+                const uint32_t kj = in ? L.key[j] : 0u, tl = in ? L.tl[j] : 0u;
+                const uint32_t incl = wave_scan_add(tl);
+                const uint32_t P = carry + incl - tl;
+                if (in) L.bm[i] = P;
+                const uint64_t last = __builtin_amdgcn_ballot_w64(in && !(kj & (1u << 16)));
+                const uint32_t le = last ? (uint32_t)__builtin_ctzll(last) : 64u;     // first MF-clear lane
+                gap |= __builtin_amdgcn_ballot_w64(in && lane <= le && (kj & 0xFFFFu) != P) != 0;
+                if (last) {
+                    e = i0 + le;
+                    len = (uint32_t)__builtin_amdgcn_readlane((int)(P + tl), (int)le);
+                }
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+            bad = gap || e == NONE || e + 1u != m || 20u + len > 0xFFFFu || od.len < 20u + len ||
+                  (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off;
+        }
+        // the first fragment's PICO_SIZE_IP4HDR bytes (pico_fragments.c:332-333) and the pseudo
+        // header (struct pico_ipv4_pseudo_hdr as LE words: src, dst, proto << 8, bswap16(len))
+        uint32_t proto = 0, pseudo = 0;
+        if (!bad) {
+            uint8_t* dst = p.out + od.off;
+            const pico_csum_desc_dev d0 = p.frag[first + L.sidx[0]];
+            const uint32_t hb = lane < 20u ? ld_u8(p.base + d0.off + lane) : 0u;
+            if (lane < 20u) dst[lane] = (uint8_t)hb;
+            proto = (uint32_t)__shfl((int)hb, 9);
+            const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
+            pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) + (proto << 8) +
+                     (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+        }
+        if (lane == 0) {
+            L.m = m;
+            L.len = len;
+            L.bad = bad ? 1u : 0u;
+            L.proto = proto;
+            L.pseudo = pseudo;
+        }
+    }
+    __syncthreads();
+    const bool bad = L.bad != 0;
+
+    // ---- 4. gather + checksum, all waves, fragment-major (wave w: fragments w, w + 4, ...)
+    uint32_t acc = 0, w1 = 0;
+    if (!bad) {
+        const uint32_t m = L.m;
+        uint8_t* t = p.out + od.off + 20;
+        const bool t8 = ((reinterpret_cast<uintptr_t>(t)) & 7u) == 0;   // workgroup-uniform
+        struct Frag {
+            Window win;
+            uint32_t s, tl, at, nu;
+            bool o16;
+        };
+        auto frag_ctx = [&](uint32_t i) {
+            Frag f;
+            const uint32_t j = L.sidx[i];
+            f.tl = L.tl[j];
+            f.at = L.bm[i];
+            const uint64_t sa = L.src[j];
+            // a buffer window over the payload's 16-byte lines: every slot loads unconditionally,
+            // slots past the payload read zeros (no branch, so no vmcnt(0) between the loads)
+            f.win = make_window(sa & ~15ull, ((uint32_t)(sa & 15u) + f.tl + 15u) & ~15u);
+            f.s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sa & 15u));
+            f.o16 = ((reinterpret_cast<uintptr_t>(t) + f.at) & 15u) == 0;   // wave-uniform
+            f.nu = (f.tl + 15u) >> 4;                                    // 16-byte units
+            return f;
+        };
+        constexpr int U = 2;                   // 64-unit slots per fragment per step
+        auto issue = [&](const Frag& f, uint32_t u0, uint4 (&c0)[U], uint4 (&c1)[U]) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t u = u0 + 64u * k + lane;
+                c0[k] = load_win<true>(f.win, u < f.nu ? 16u * u : WIN_OOB);
+                c1[k] = load_win<true>(f.win, u < f.nu && f.s ? 16u * u + 16u : WIN_OOB);
+            }
+        };
+        auto consume = [&](const Frag& f, uint32_t u0, const uint4 (&c0)[U], const uint4 (&c1)[U]) {
+            const uint32_t q = f.s >> 2, sb = f.s & 3u;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t u = u0 + 64u * k + lane;
+                if (u >= f.nu) continue;
+                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+                uint32_t x[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)                     // bytes [s, s + 16) of the 32 loaded
+                    x[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
+                                                      sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sb);
+                const uint32_t b0 = 16u * u, nb = min(16u, f.tl - b0);
+                uint8_t* o = t + f.at + b0;
+                if (nb < 16u) {                                 // the fragment's last, partial unit
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint32_t lo = 4u * w;
+                        x[w] = nb <= lo ? 0u : nb >= lo + 4u ? x[w] : x[w] & ((1u << (8u * (nb - lo))) - 1u);
+                    }
+                    for (uint32_t qq = 0; qq < nb; ++qq) o[qq] = (uint8_t)(x[qq >> 2] >> (8u * (qq & 3u)));
+                } else if (f.o16) {
+                    *reinterpret_cast<uint4*>(o) = make_uint4(x[0], x[1], x[2], x[3]);
+                } else if (t8) {
+                    reinterpret_cast<uint2*>(o)[0] = make_uint2(x[0], x[1]);
+                    reinterpret_cast<uint2*>(o)[1] = make_uint2(x[2], x[3]);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = x[w];
+                }
+                acc = dot2_add(x[3], dot2_add(x[2], dot2_add(x[1], dot2_add(x[0], acc))));   // even offset
+                if (f.at + b0 == 0u) w1 = x[1];                 // transport bytes 4..7 (UDP crc: 6, 7)
+            }
+        };
+        // one fragment per step (two per step measured 145 -> 178 us on c3_reasm: 83 VGPRs, 6 waves
+        // per SIMD instead of 8)
+        for (uint32_t i = wv; i < m; i += 4u) {
+            const Frag f = frag_ctx(i);
+            for (uint32_t u0 = 0; u0 < f.nu; u0 += 64u * U) {
+                uint4 c0[U], c1[U];
+                issue(f, u0, c0, c1);
+                consume(f, u0, c0, c1);
+            }
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
         w1 = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(w1), 63);
+        if (lane == 0) {
+            L.acc[wv] = acc;
+            L.w1[wv] = w1;
+        }
     }
+    __syncthreads();
 
     // ---- 5. pico_transport_crc_check on the reassembled frame
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         uint32_t l4 = 0, v = V_MALFORMED;
+        const uint32_t len = L.len, proto = L.proto;
         if (!bad) {
+            const uint32_t s = L.acc[0] + L.acc[1] + L.acc[2] + L.acc[3];
+            const uint32_t word1 = L.w1[0] | L.w1[1] | L.w1[2] | L.w1[3];
             v = V_ACCEPT;
-            if (proto == 6u || (proto == 17u && len >= 8u && (w1 >> 16) != 0u)) {
-                l4 = finalize(pseudo + acc);
+            if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
+                l4 = finalize(L.pseudo + s);
                 if (l4) v = V_L4_BAD;
             }
         }
@@ -218,7 +289,7 @@ int pico_csum_launch_ipv4_reassemble(const void* base, uint64_t base_len, const 
     FragArgs a{static_cast<const uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(frag), groups,
                n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
                static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict};
-    const dim3 grid((n_dgram + 3u) / 4u), block(256);
+    const dim3 grid(n_dgram), block(256);
     hipLaunchKernelGGL(ipv4_reassemble_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }

@@ -45,16 +45,17 @@ def layout(lens, align=16, shift=0):
     return G.ipv4_desc(off, (cap - np.uint64(align)).astype(np.uint32)), int(cap.sum()) + shift + 16
 
 
+@pytest.mark.parametrize("shift", [4, 12])
 @pytest.mark.parametrize("proto", [6, 17, 1])
 @pytest.mark.parametrize("payload", [1480, 8, 552, 64000])
-def test_reassembly_vs_oracle(proto, payload):
+def test_reassembly_vs_oracle(proto, payload, shift):
     rng = np.random.default_rng(proto * 100 + payload % 97)
     lens = rng.integers(0, 12000, 40).tolist() + [64512, 65515, 1, 7, 8, 9, 1480, 1481, 2959, 2960]
     if payload == 8:
         lens = [x for x in lens if x <= 4000]           # <= 512 fragments per datagram
     buf, off, flen, grp = synth.ipv4_fragments(lens, seed=proto + payload, proto=proto, frag_payload=payload)
     d = G.ipv4_desc(off, flen)
-    od, size = layout(lens, shift=4)
+    od, size = layout(lens, shift=shift)              # 12: transports on 16-byte lines
     wl, wv = check(buf, d, grp, od, size)
     assert (wl == np.array(lens)).all()
 
