@@ -217,6 +217,10 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
         uint32_t ng = 64u / s.G, f = n / 32768u;
         f -= f % ng;
         s.fpw = f < 2 * ng ? 2 * ng : f > 64 ? 64 : f;
+        /* bursts of <= 4K frames: one frame set per lane group (more, shorter waves), -10 %
+         * at 1K-4K x 1500 B (tools/burst_sweep.py, r02g) */
+        if (n <= 4096u)
+            s.fpw = ng;
     }
     if (!uniform) {
         /* descriptor batches: sorted-rounds kernel (each wave sorts its frames by
@@ -224,12 +228,14 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
          * (<= 128 VGPRs, 4 waves per SIMD); ~4K waves, so a 256K-frame batch is
          * one residency round of 64-frame waves; non-temporal loads in the wide
          * (>= 16-lane) rounds only.  Measured on MI355X: DESIGN.md "Launch shapes". */
-        uint32_t f = n / 4096u;
+        uint32_t f = n / 2048u;
         s.G = 2;
         s.CPL = 8;
         s.U = 1;            /* narrowest round width: 1 = one frame per lane for <= 8-chunk frames */
         s.nt = 1;
-        s.fpw = f < 16 ? 16 : f > 64 ? 64 : f;
+        /* n / 2048 frames per wave in [4, 64]: 1K-4K bursts 4 (-20 % vs 16), 16K 8, 64K 32,
+         * 256K 64 (one residency round of 64-frame waves) -- tools/burst_sweep.py, r02g */
+        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
     }
     if (g_ovr_group) {
         uint32_t auto_u = s.U;
@@ -477,12 +483,12 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
     }
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
     if (s.G != 2) {           /* the Ethernet mode exists in the sorted-rounds kernel only */
-        uint32_t f = n / 4096u;
+        uint32_t f = n / 2048u;
         s.G = 2;
         s.CPL = 8;
         s.U = 1;
         s.nt = 1;
-        s.fpw = f < 16 ? 16 : f > 64 ? 64 : f;
+        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
     }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags | ablate_flags(), NULL, NULL,
                                                  d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
