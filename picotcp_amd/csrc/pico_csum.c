@@ -250,8 +250,8 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
 }
 
 /* Ablation bits for the sorted-rounds kernel (PICO_CSUM_ABLATE, measurement only):
- * 1 = skip the rounds, 2 = skip the head-window loads, 4 = skip the IPv4 TX crc writes.  Passed in flags bits 8+, which
- * the public API rejects. */
+ * 1 = skip the rounds, 2 = skip the head-window loads, 4 = skip the IPv4 TX crc writes.
+ * Passed in flags bits 8+, which the public API rejects. */
 static uint32_t ablate_flags(void)
 {
     const char *e = getenv("PICO_CSUM_ABLATE");
