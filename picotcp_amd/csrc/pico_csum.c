@@ -554,6 +554,12 @@ struct pico_csum_ctx {
     struct pico_csum_desc *h_desc[2], *d_desc[2];
     uint16_t *d_net[2], *d_l4[2];
     uint8_t *d_ver[2];
+    /* pinned result staging: the D2H stays asynchronous (into pageable memory HIP would block
+     * the host loop until it completes, serialising the chunks); copied out when the slot is
+     * next reused or at the end */
+    uint16_t *h_net[2], *h_l4[2];
+    uint8_t *h_ver[2];
+    uint32_t pend_first[2], pend_cnt[2];
     int desc_ready;
 };
 
@@ -600,6 +606,9 @@ void pico_csum_ctx_destroy(struct pico_csum_ctx *c)
         if (c->d_net[i]) hipFree(c->d_net[i]);
         if (c->d_l4[i]) hipFree(c->d_l4[i]);
         if (c->d_ver[i]) hipFree(c->d_ver[i]);
+        if (c->h_net[i]) hipHostFree(c->h_net[i]);
+        if (c->h_l4[i]) hipHostFree(c->h_l4[i]);
+        if (c->h_ver[i]) hipHostFree(c->h_ver[i]);
     }
     free(c);
 }
@@ -675,7 +684,10 @@ static int ctx_desc_alloc(struct pico_csum_ctx *c)
         if (hipHostMalloc((void **)&c->h_desc[i], nd * sizeof(struct pico_csum_desc), hipHostMallocDefault) != hipSuccess ||
             hipMalloc((void **)&c->d_desc[i], nd * sizeof(struct pico_csum_desc)) != hipSuccess ||
             hipMalloc((void **)&c->d_net[i], nd * 2u) != hipSuccess || hipMalloc((void **)&c->d_l4[i], nd * 2u) != hipSuccess ||
-            hipMalloc((void **)&c->d_ver[i], nd) != hipSuccess)
+            hipMalloc((void **)&c->d_ver[i], nd) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_net[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_l4[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_ver[i], nd, hipHostMallocDefault) != hipSuccess)
             return fail(PICO_CSUM_ENOMEM, "ctx descriptor staging (%llu descriptors)", (unsigned long long)nd);
     }
     c->desc_ready = 1;
@@ -692,7 +704,7 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
                            const uint8_t *mac, uint16_t *out, uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict,
                            const char *what)
 {
-    const uint64_t maxd = CTX_MAX_DESC(c->staging);
+    const uint64_t maxd = CTX_MAX_DESC(c ? c->staging : 0);
     uint32_t i = 0;
     int b = 0, rc = 0;
     if (!c || !base || !desc)
@@ -703,6 +715,19 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         return rc;
     if (hipSetDevice(c->device) != hipSuccess)
         return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
+    c->pend_cnt[0] = c->pend_cnt[1] = 0;
+    /* results of slot bb's last chunk, from pinned staging to the caller's arrays */
+#define FLUSH(bb)                                                                                  \
+    do {                                                                                           \
+        uint32_t f0 = c->pend_first[bb], fc = c->pend_cnt[bb];                                     \
+        if (fc) {                                                                                  \
+            if (out) memcpy(out + f0, c->h_l4[bb], (size_t)fc * 2u);                               \
+            if (out_net) memcpy(out_net + f0, c->h_net[bb], (size_t)fc * 2u);                      \
+            if (out_l4) memcpy(out_l4 + f0, c->h_l4[bb], (size_t)fc * 2u);                         \
+            if (verdict) memcpy(verdict + f0, c->h_ver[bb], fc);                                   \
+            c->pend_cnt[bb] = 0;                                                                   \
+        }                                                                                          \
+    } while (0)
     while (i < n && !rc) {
         uint64_t lo = UINT64_MAX, hi = 0;
         uint32_t j = i, k, cnt;
@@ -728,9 +753,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         }
         cnt = j - i;
         if (lo == UINT64_MAX) lo = hi = 0;
-        /* the pinned descriptor slot is reused: its previous H2D must be done */
+        /* the pinned descriptor and result slots are reused: the previous chunk on them must be
+         * done, and its results copied out */
         if (hipEventSynchronize(c->done[b]) != hipSuccess)
             return fail(PICO_CSUM_EIO, "%s: event synchronize failed", what);
+        FLUSH(b);
         for (k = 0; k < cnt; k++) {
             const struct pico_csum_desc *s = &desc[i + k];
             struct pico_csum_desc *t = &c->h_desc[b][k];
@@ -768,10 +795,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
 #define D2H(dst, src, bytes)                                                                              \
         if ((dst) && (e = hipMemcpyAsync((dst), (src), (bytes), hipMemcpyDeviceToHost, c->st[b])) != hipSuccess) \
             return fail(PICO_CSUM_EIO, "%s: D2H: %s", what, hipGetErrorString(e));
-        D2H(out ? out + i : NULL, c->d_l4[b], (size_t)cnt * 2u)
-        D2H(out_net ? out_net + i : NULL, c->d_net[b], (size_t)cnt * 2u)
-        D2H(out_l4 ? out_l4 + i : NULL, c->d_l4[b], (size_t)cnt * 2u)
-        D2H(verdict ? verdict + i : NULL, c->d_ver[b], (size_t)cnt)
+        D2H(out || out_l4 ? c->h_l4[b] : NULL, c->d_l4[b], (size_t)cnt * 2u)
+        D2H(out_net ? c->h_net[b] : NULL, c->d_net[b], (size_t)cnt * 2u)
+        D2H(verdict ? c->h_ver[b] : NULL, c->d_ver[b], (size_t)cnt)
+        c->pend_first[b] = i;
+        c->pend_cnt[b] = cnt;
         if ((flags & PICO_CSUM_F_WRITE) && hi > lo)
             D2H((uint8_t *)base + lo, c->d_buf[b], hi - lo)
 #undef D2H
@@ -782,6 +810,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
     }
     if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
         if (!rc) rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
+    if (!rc) {
+        FLUSH(0);
+        FLUSH(1);
+    }
+#undef FLUSH
     return rc;
 }
 
