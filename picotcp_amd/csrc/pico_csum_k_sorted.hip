@@ -5,6 +5,22 @@
 
 namespace {
 
+#ifdef PICO_CSUM_STAMPS
+// Diagnostic build only (tools/stamps.py; never the product library): per wave, s_memrealtime
+// (100 MHz, comparable across XCDs) at entry, after phase 1, after the rounds and at the end,
+// into a buffer no other code reads.
+__device__ uint64_t* g_stamps;
+__device__ uint32_t g_stamps_n;
+#define STAMP(k)                                                                                   \
+    do {                                                                                           \
+        const uint64_t wv_ = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);        \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                      \
+        if ((threadIdx.x & 63u) == 0 && g_stamps && wv_ < g_stamps_n) g_stamps[4 * wv_ + (k)] = t_; \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------- sorted-rounds kernel
 //
 // Descriptor batches of any size mix, all modes (RAW / fused IPv4 / fused IPv6).
@@ -512,6 +528,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
     const bool any_xo = __builtin_amdgcn_ballot_w64(nch != 0 && (xpos != NONE || optend != 0)) != 0;
 
+    STAMP(1);
     // ---- 2. order the frames by size class (the narrowest round width that covers
     //         them in one pass): ballots and bit counts, no data movement but one
     //         LDS store per frame
@@ -557,6 +574,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
 
+    STAMP(2);
     // ---- 4. lane j finalizes frame j (state reloaded from LDS)
     if (lane < cnt) sorted_finish<MODE>(p, L, lane, f0 + lane, tx);
     __builtin_amdgcn_wave_barrier();
@@ -570,7 +588,9 @@ __global__ __launch_bounds__(256, CPL == 8 || MODE != 0 ? 4 : 5) void csum_sorte
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
+    STAMP(0);
     if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+    STAMP(3);
 }
 
 // ---------------------------------------------------------------- IPv4 forwarding step
@@ -619,6 +639,15 @@ __global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
 }  // namespace
 
 extern "C" {
+
+#ifdef PICO_CSUM_STAMPS
+int pico_csum_diag_set_stamps(void* d_buf, uint32_t waves) {
+    uint64_t* b = static_cast<uint64_t*>(d_buf);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &b, sizeof(b)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_n), &waves, sizeof(waves)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
 
 // Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6; small: 1-lane
 // rounds for frames of <= 8 chunks (cpl 8 only).

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the sorted-rounds kernel from the diagnostic build
+(picotcp_amd/diag/libpicocsum_stamps.so, `make -C picotcp_amd/csrc diag`): every wave stamps
+s_memrealtime (100 MHz) at entry, after phase 1 (descriptors, head windows, parse), after the
+rounds and at the end.  Run on a C2 batch (rotating copies, the stamps of the last launch):
+
+    PICO_CSUM_LIB=picotcp_amd/diag/libpicocsum_stamps.so python tools/stamps.py --config c2
+
+Prints the kernel span and, per phase, percentiles over the waves of its start / duration,
+plus how much of the span the slowest waves' tail takes."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("PICO_CSUM_LIB", os.path.join(ROOT, "picotcp_amd", "diag", "libpicocsum_stamps.so"))
+from picotcp_amd import _lib, batch, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=["c2", "c2tx", "c2v6", "c2raw"])
+    ap.add_argument("--n", type=int, default=262144)
+    ap.add_argument("--rotate", type=int, default=12)
+    a = ap.parse_args()
+    lib = _lib.load()
+    lib.pico_csum_diag_set_stamps.restype = ctypes.c_int
+    lib.pico_csum_diag_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    dev = torch.device("cuda:0")
+    n = a.n
+    lens = synth.imix_lengths(n, 3) + (20 if a.config == "c2v6" else 0)
+    sets = []
+    for r in range(a.rotate):
+        if a.config == "c2v6":
+            buf, net, avail, seeds = synth.ipv6_batch(lens.astype(np.uint32), seed=10 + r, proto=6, eth=True)
+            d = batch.desc_to_device(batch.make_desc(net, avail, seeds), dev)
+            b = torch.from_numpy(buf).to(dev)
+            batch.ipv6_checksum_batch(b, d, n, flags=batch.F_TX | batch.F_WRITE)
+        else:
+            buf, net, avail = synth.ipv4_batch(lens, seed=10 + r, proto=6, eth=True)
+            d = batch.desc_to_device(batch.make_desc(net, avail), dev)
+            b = torch.from_numpy(buf).to(dev)
+            batch.ipv4_checksum_batch(b, d, n, flags=batch.F_TX | batch.F_WRITE)
+        sets.append((b, d))
+    waves = -(-n // 64) + 64
+    st = torch.zeros(4 * waves, dtype=torch.int64, device=dev)
+
+    def launch(i):
+        b, d = sets[i % a.rotate]
+        if a.config == "c2v6":
+            batch.ipv6_checksum_batch(b, d, n)
+        elif a.config == "c2raw":
+            batch.checksum_batch(b, d, n)
+        else:
+            batch.ipv4_checksum_batch(b, d, n, flags=batch.F_TX | batch.F_WRITE if a.config == "c2tx" else 0)
+    for i in range(30):
+        launch(i)
+    torch.cuda.synchronize()
+    assert lib.pico_csum_diag_set_stamps(ctypes.c_void_p(st.data_ptr()), waves) == 0
+    res = []
+    for rep in range(5):
+        st.zero_()
+        torch.cuda.synchronize()
+        launch(100 + rep)
+        torch.cuda.synchronize()
+        t = st.cpu().numpy().reshape(-1, 4)
+        t = t[t[:, 0] > 0]
+        res.append(t)
+    lib.pico_csum_diag_set_stamps(ctypes.c_void_p(0), 0)
+    out = []
+    for t in res:
+        t0 = t[:, 0].min()
+        rel = (t - t0) * 10.0 / 1000.0          # 100 MHz ticks -> us
+        span = rel[:, 3].max()
+        q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 99, 100)]
+        out.append({"waves": int(t.shape[0]), "span_us": round(float(span), 2),
+                    "start_pctl": q(rel[:, 0]), "phase1_end_pctl": q(rel[:, 1]), "rounds_end_pctl": q(rel[:, 2]),
+                    "end_pctl": q(rel[:, 3]), "phase1_dur_pctl": q(rel[:, 1] - rel[:, 0]),
+                    "rounds_dur_pctl": q(rel[:, 2] - rel[:, 1]), "finish_dur_pctl": q(rel[:, 3] - rel[:, 2]),
+                    "waves_done_at_90pct_span": round(float((rel[:, 3] <= 0.9 * span).mean()), 3)})
+    for o in out:
+        print(json.dumps({"config": a.config, **o}))
+
+
+if __name__ == "__main__":
+    main()
