@@ -491,15 +491,51 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         const uint32_t xs = 16u * d + xpos;
         const bool oin = optend != 0u && k0 != 0u;
         const uint32_t sl = odd ? SEL_ODD : SEL_EVEN;
-        // One masked sum per window chunk of the region (the compiler builds the byte masks
-        // with a few 64-bit shifts; whole-chunk sums + two edge corrections measured +16 %
-        // VALU instructions, r02d).
+        // p_all: whole-chunk sums of chunks [d, d + k0), minus the bytes of the first chunk
+        // before rs and of the last chunk from re on.  The two edge chunks come from the LDS
+        // stage (one ds_read each).  Against one masked sum per window chunk: -14 % VALU
+        // instructions per wave, C2 -1.5 % (r02d, profiles/r02d).
+        auto edge_chunk = [&](uint32_t idx) {      // bit-mask blends (a select chain becomes a scratch array)
+            uint4 v = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (uint32_t i = 0; i < HW; ++i) {
-            if (i >= d && i < d + k0) {
-                p_all += masked_chunk_sum<true>(hw[i], 16u * i, min(rs, re), re, sl);
-                if (xin && !staged) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
-                if (oin) p_opt += masked_chunk_sum<true>(hw[i], 16u * i, rs + 20u, 16u * d + optend, sl);
+            for (uint32_t i = 0; i < HW; ++i) {
+                const uint32_t m = idx == i ? 0xFFFFFFFFu : 0u;
+                v.x |= hw[i].x & m; v.y |= hw[i].y & m; v.z |= hw[i].z & m; v.w |= hw[i].w & m;
+            }
+            return v;
+        };
+        auto window_sums = [&](auto perm_tag) {
+            constexpr bool PERM = decltype(perm_tag)::value;
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) {
+                const uint32_t c = add_full<PERM>(hw[i], sl, 0u);
+                p_all += (i >= d && i < d + k0) ? c : 0u;
+            }
+            if (__builtin_amdgcn_ballot_w64(k0 != 0u)) {
+                const uint32_t e0 = k0 ? d : 0u, e1 = k0 ? d + k0 - 1u : 0u;
+                uint4 h0, h1;
+                if (__builtin_amdgcn_ballot_w64(k0 != 0u && !staged) == 0) {
+                    h0 = stage[lane * HW + (e0 ^ (lane & (HW - 1)))];
+                    h1 = stage[lane * HW + (e1 ^ (lane & (HW - 1)))];
+                } else {
+                    h0 = edge_chunk(e0);
+                    h1 = edge_chunk(e1);
+                }
+                if (k0) {
+                    p_all -= masked_chunk_sum<PERM>(h0, 16u * e0, 16u * e0, rs, sl);
+                    p_all -= masked_chunk_sum<PERM>(h1, 16u * e1, re, P, sl);
+                }
+            }
+        };
+        if (__builtin_amdgcn_ballot_w64(k0 != 0u && odd)) window_sums(std::integral_constant<bool, true>{});
+        else window_sums(std::integral_constant<bool, false>{});
+        if (__builtin_amdgcn_ballot_w64(oin || (xin && !staged))) {     // IPv4 options / > 2 GiB batches
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) {
+                if (i >= d && i < d + k0) {
+                    if (xin && !staged) p_x += masked_chunk_sum<true>(hw[i], 16u * i, xs, xs + 2u, sl);
+                    if (oin) p_opt += masked_chunk_sum<true>(hw[i], 16u * i, rs + 20u, 16u * d + optend, sl);
+                }
             }
         }
         // The isolated field is one word of the region's pairing: whatever the start's
