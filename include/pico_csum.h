@@ -224,6 +224,8 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
  *                      its buffer: reference UB), 20 + len > 65535 (its uint16 allocation size
  *                      wraps), a fragment header or payload past desc.len or base_len, an empty
  *                      group or one of more than 512 fragments, an output region too small.
+ * The bytes of an output region are unspecified when its datagram is not reassembled (the
+ * gather starts before completeness is known); no byte outside the region is written.
  * Any of the three output pointers may be NULL. */
 int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
                                    uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,

@@ -11,19 +11,24 @@
 //
 // One workgroup (4 waves) per datagram (its fragments are a contiguous descriptor range, in
 // arrival order):
-//   1. wave 0, lane j parses fragment j's header (IHL, total length, MF, offset) into LDS;
-//   2. tree order: rank by offset among the first arrivals of each offset (pico_tree_insert
-//      rejects a repeated key), LDS broadcast reads, O(count^2 / 64) per lane;
-//   3. completeness: a wave prefix scan of the sorted transport lengths against the
-//      offsets, up to the first fragment without MF (must be the last in tree order);
-//   4. gather, all 4 waves, fragment-major (wave w takes fragments w, w + 4, ...): a
-//      fragment's payload in 16-byte units, 2 x 64 units per wave per step, every load
-//      issued before any is used: two aligned 16-byte loads through a buffer window over the
-//      payload (out-of-range slots read zeros, no branches) and a shift by the payload's
-//      alignment (wave-uniform per fragment: dword select + alignbyte); stores are 8-byte
-//      (or 4-byte) at the unit's place in the transport, which starts 4-byte aligned,
-//      offsets being multiples of 8; v_dot2 sums on the fly (every unit is a whole number of
-//      checksum words); a workgroup reduction through LDS at the end.
+//   1. all 256 threads parse the fragment headers (IHL, total length, MF, offset) into LDS and
+//      mark repeated offsets (pico_tree_insert rejects a repeated key: the earliest arrival
+//      of each offset is kept);
+//   2. the gather starts at once: a kept fragment's place in the transport is its own offset
+//      (completeness, checked beside it, requires offset == bookmark), so no wave waits for the
+//      ordering.  Waves 1-3 gather fragments 1, 2, 3 mod 4 while wave 0 checks completeness
+//      (rank by offset among the kept fragments, LDS broadcast reads; a wave prefix scan of
+//      the sorted transport lengths against the offsets, up to the first fragment without MF,
+//      which must be the last in tree order), copies the first fragment's 20 header bytes,
+//      then gathers fragments 0 mod 4;
+//   3. gather: a fragment's payload in 16-byte units, 2 x 64 units per wave per step, every
+//      load issued before any is used: two aligned 16-byte loads through a buffer window over
+//      the payload (out-of-range slots read zeros, no branches) and a shift by the payload's
+//      alignment (wave-uniform per fragment: dword select + alignbyte); stores are 16-, 8- or
+//      4-byte at the unit's place in the transport (which starts 4-byte aligned, offsets being
+//      multiples of 8), only where the fragment fits the output region; v_dot2 sums on the
+//      fly (every unit is a whole number of checksum words); a workgroup reduction at the end.
+// The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
 namespace {
@@ -49,9 +54,8 @@ struct FragLds {
     uint32_t key[FRAG_MAX];   // offset | MF << 16 | header length << 17 | dup << 24
     uint32_t tl[FRAG_MAX];    // transport length
     uint16_t sidx[FRAG_MAX];  // tree position -> fragment
-    uint32_t bm[FRAG_MAX];    // tree position -> bookmark (the fragment's place in the transport)
     uint64_t src[FRAG_MAX];   // fragment -> payload address (no descriptor re-read in the gather)
-    uint32_t m, len, bad, proto, pseudo;
+    uint32_t len, bad, proto, pseudo, first0;
     uint32_t acc[4], w1[4];
 };
 
@@ -59,194 +63,177 @@ __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*
 
 __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
     __shared__ FragLds L;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t g = blockIdx.x;
     if (g >= p.n_dgram) return;                       // workgroup-uniform
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
+    const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
+                      (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < 20u;
+    if (tid == 0) {
+        L.bad = bad0 ? 1u : 0u;
+        L.first0 = NONE;
+    }
+    __syncthreads();
 
-    if (wv == 0) {
-        bool bad = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first;
-        // ---- 1. parse (pico_ipv4_process_in: net_len, transport_len = tot - net_len, frag)
-        if (!bad) {
-            bool b = false;
-            for (uint32_t j = lane; j < cnt; j += 64u) {
-                const pico_csum_desc_dev d = p.frag[first + j];
-                uint32_t key = 0, tl = 0;
-                if (d.len < 20u || d.off > p.base_len || d.len > p.base_len - d.off) {
-                    b = true;
-                } else {
-                    const uint8_t* h = p.base + d.off;
-                    const uint32_t ihl = ld_u8(h) & 0x0Fu;
-                    const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-                    tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
-                    const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
-                    key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u) | (hl << 17);
-                    if (hl + tl > d.len) b = true;
-                }
-                L.key[j] = key;
-                L.tl[j] = tl;
-                L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + (key >> 17);
+    // ---- 1. parse (pico_ipv4_process_in: net_len, transport_len = tot - net_len, frag)
+    if (!bad0) {
+        for (uint32_t j = tid; j < cnt; j += 256u) {
+            const pico_csum_desc_dev d = p.frag[first + j];
+            uint32_t key = 0, tl = 0;
+            if (d.len < 20u || d.off > p.base_len || d.len > p.base_len - d.off) {
+                L.bad = 1u;
+            } else {
+                const uint8_t* h = p.base + d.off;
+                const uint32_t ihl = ld_u8(h) & 0x0Fu;
+                const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
+                const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
+                key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u) | (hl << 17);
+                if (hl + tl > d.len) L.bad = 1u;
             }
-            bad = __builtin_amdgcn_ballot_w64(b) != 0;
+            L.key[j] = key;
+            L.tl[j] = tl;
+            L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + (key >> 17);
         }
+    }
+    __syncthreads();
+    bool bad = L.bad != 0;                              // workgroup-uniform
+    if (!bad) {                                         // repeated offsets: the earliest arrival stays
+        for (uint32_t j = tid; j < cnt; j += 256u) {
+            const uint32_t fj = L.key[j] & 0xFFFFu;
+            bool dup = false;
+            for (uint32_t k = 0; k < j; ++k) dup |= (L.key[k] & 0xFFFFu) == fj;
+            if (dup) L.key[j] |= 1u << 24;
+            else if (fj == 0u) L.first0 = j;            // the tree's first fragment (offset 0)
+        }
+    }
+    __syncthreads();
+    uint8_t* t = p.out + od.off + 20;
+    const uint32_t cap = od.len - 20u;                  // transport bytes the output region holds
+
+    // ---- 2. wave 0: completeness (pico_fragments_check_complete) and the header
+    if (wv == 0 && !bad) {
+        uint32_t kept = 0;
+        for (uint32_t j = lane; j < cnt; j += 64u) {
+            const uint32_t kj = L.key[j];
+            if (kj >> 24) continue;
+            uint32_t r = 0;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t kk = L.key[k];
+                r += ((kk >> 24) == 0 && (kk & 0xFFFFu) < (kj & 0xFFFFu)) ? 1u : 0u;
+            }
+            L.sidx[r] = (uint16_t)j;
+            ++kept;
+        }
+        const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(kept), 63);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
-
-        // ---- 2. tree order: repeated offsets keep the earliest arrival; rank among the kept
-        uint32_t m = 0;
-        if (!bad) {
-            for (uint32_t j = lane; j < cnt; j += 64u) {
-                const uint32_t fj = L.key[j] & 0xFFFFu;
-                bool dup = false;
-                for (uint32_t k = 0; k < j; ++k) dup |= (L.key[k] & 0xFFFFu) == fj;
-                if (dup) L.key[j] |= 1u << 24;
+        uint32_t carry = 0, e = NONE, len = 0;
+        bool gap = false;
+        for (uint32_t i0 = 0; i0 < m && e == NONE; i0 += 64u) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < m;
+            const uint32_t j = in ? L.sidx[i] : 0u;
+            const uint32_t kj = in ? L.key[j] : 0u, tl = in ? L.tl[j] : 0u;
+            const uint32_t incl = wave_scan_add(tl);
+            const uint32_t P = carry + incl - tl;
+            const uint64_t last = __builtin_amdgcn_ballot_w64(in && !(kj & (1u << 16)));
+            const uint32_t le = last ? (uint32_t)__builtin_ctzll(last) : 64u;     // first MF-clear lane
+            gap |= __builtin_amdgcn_ballot_w64(in && lane <= le && (kj & 0xFFFFu) != P) != 0;
+            if (last) {
+                e = i0 + le;
+                len = (uint32_t)__builtin_amdgcn_readlane((int)(P + tl), (int)le);
             }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            uint32_t kept = 0;
-            for (uint32_t j = lane; j < cnt; j += 64u) {
-                const uint32_t kj = L.key[j];
-                if (kj >> 24) continue;
-                uint32_t r = 0;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const uint32_t kk = L.key[k];
-                    r += ((kk >> 24) == 0 && (kk & 0xFFFFu) < (kj & 0xFFFFu)) ? 1u : 0u;
-                }
-                L.sidx[r] = (uint16_t)j;
-                ++kept;
-            }
-            m = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(kept), 63);
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-
-        // ---- 3. completeness (pico_fragments_check_complete): offset == bookmark up to the
-        //         first fragment without MF, which must be the last one in tree order
-        uint32_t len = 0;
-        if (!bad) {
-            uint32_t carry = 0, e = NONE;
-            bool gap = false;
-            for (uint32_t i0 = 0; i0 < m && e == NONE; i0 += 64u) {
-                const uint32_t i = i0 + lane;
-                const bool in = i < m;
-                const uint32_t j = in ? L.sidx[i] : 0u;
-                const uint32_t kj = in ? L.key[j] : 0u, tl = in ? L.tl[j] : 0u;
-                const uint32_t incl = wave_scan_add(tl);
-                const uint32_t P = carry + incl - tl;
-                if (in) L.bm[i] = P;
-                const uint64_t last = __builtin_amdgcn_ballot_w64(in && !(kj & (1u << 16)));
-                const uint32_t le = last ? (uint32_t)__builtin_ctzll(last) : 64u;     // first MF-clear lane
-                gap |= __builtin_amdgcn_ballot_w64(in && lane <= le && (kj & 0xFFFFu) != P) != 0;
-                if (last) {
-                    e = i0 + le;
-                    len = (uint32_t)__builtin_amdgcn_readlane((int)(P + tl), (int)le);
-                }
-                carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            }
-            bad = gap || e == NONE || e + 1u != m || 20u + len > 0xFFFFu || od.len < 20u + len ||
-                  (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off;
-        }
+        const bool b = gap || e == NONE || e + 1u != m || 20u + len > 0xFFFFu || len > cap;
         // the first fragment's PICO_SIZE_IP4HDR bytes (pico_fragments.c:332-333) and the pseudo
         // header (struct pico_ipv4_pseudo_hdr as LE words: src, dst, proto << 8, bswap16(len))
         uint32_t proto = 0, pseudo = 0;
-        if (!bad) {
-            uint8_t* dst = p.out + od.off;
-            const pico_csum_desc_dev d0 = p.frag[first + L.sidx[0]];
-            const uint32_t hb = lane < 20u ? ld_u8(p.base + d0.off + lane) : 0u;
-            if (lane < 20u) dst[lane] = (uint8_t)hb;
+        if (!b) {
+            const uint8_t* h0 = reinterpret_cast<const uint8_t*>(L.src[L.first0]) - ((L.key[L.first0] >> 17) & 0x7Fu);
+            const uint32_t hb = lane < 20u ? ld_u8(h0 + lane) : 0u;
+            if (lane < 20u) t[(int)lane - 20] = (uint8_t)hb;
             proto = (uint32_t)__shfl((int)hb, 9);
             const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
             pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) + (proto << 8) +
                      (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
         }
         if (lane == 0) {
-            L.m = m;
-            L.len = len;
-            L.bad = bad ? 1u : 0u;
+            L.len = b ? 0u : len;
             L.proto = proto;
             L.pseudo = pseudo;
+            if (b) L.bad = 1u;
         }
     }
-    __syncthreads();
-    const bool bad = L.bad != 0;
 
-    // ---- 4. gather + checksum, all waves, fragment-major (wave w: fragments w, w + 4, ...)
+    // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order),
+    //         each kept fragment at its own offset
     uint32_t acc = 0, w1 = 0;
     if (!bad) {
-        const uint32_t m = L.m;
-        uint8_t* t = p.out + od.off + 20;
         const bool t8 = ((reinterpret_cast<uintptr_t>(t)) & 7u) == 0;   // workgroup-uniform
         struct Frag {
             Window win;
             uint32_t s, tl, at, nu;
             bool o16;
         };
-        auto frag_ctx = [&](uint32_t i) {
+        constexpr int U = 2;                   // 64-unit slots per fragment per step
+        for (uint32_t j = wv; j < cnt; j += 4u) {
+            const uint32_t kj = L.key[j];
             Frag f;
-            const uint32_t j = L.sidx[i];
             f.tl = L.tl[j];
-            f.at = L.bm[i];
+            f.at = kj & 0xFFFFu;
+            // a repeated offset is not gathered; nor a fragment the output region cannot hold
+            // (its datagram is then not reassembled: past its end, or larger than the region)
+            if ((kj >> 24) != 0 || f.at + f.tl > cap) continue;            // wave-uniform
             const uint64_t sa = L.src[j];
             // a buffer window over the payload's 16-byte lines: every slot loads unconditionally,
             // slots past the payload read zeros (no branch, so no vmcnt(0) between the loads)
             f.win = make_window(sa & ~15ull, ((uint32_t)(sa & 15u) + f.tl + 15u) & ~15u);
             f.s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sa & 15u));
-            f.o16 = ((reinterpret_cast<uintptr_t>(t) + f.at) & 15u) == 0;   // wave-uniform
-            f.nu = (f.tl + 15u) >> 4;                                    // 16-byte units
-            return f;
-        };
-        constexpr int U = 2;                   // 64-unit slots per fragment per step
-        auto issue = [&](const Frag& f, uint32_t u0, uint4 (&c0)[U], uint4 (&c1)[U]) {
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const uint32_t u = u0 + 64u * k + lane;
-                c0[k] = load_win<true>(f.win, u < f.nu ? 16u * u : WIN_OOB);
-                c1[k] = load_win<true>(f.win, u < f.nu && f.s ? 16u * u + 16u : WIN_OOB);
-            }
-        };
-        auto consume = [&](const Frag& f, uint32_t u0, const uint4 (&c0)[U], const uint4 (&c1)[U]) {
+            f.o16 = ((reinterpret_cast<uintptr_t>(t) + f.at) & 15u) == 0;
+            f.nu = (f.tl + 15u) >> 4;
             const uint32_t q = f.s >> 2, sb = f.s & 3u;
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const uint32_t u = u0 + 64u * k + lane;
-                if (u >= f.nu) continue;
-                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-                uint32_t x[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w)                     // bytes [s, s + 16) of the 32 loaded
-                    x[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
-                                                      sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sb);
-                const uint32_t b0 = 16u * u, nb = min(16u, f.tl - b0);
-                uint8_t* o = t + f.at + b0;
-                if (nb < 16u) {                                 // the fragment's last, partial unit
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        const uint32_t lo = 4u * w;
-                        x[w] = nb <= lo ? 0u : nb >= lo + 4u ? x[w] : x[w] & ((1u << (8u * (nb - lo))) - 1u);
-                    }
-                    for (uint32_t qq = 0; qq < nb; ++qq) o[qq] = (uint8_t)(x[qq >> 2] >> (8u * (qq & 3u)));
-                } else if (f.o16) {
-                    *reinterpret_cast<uint4*>(o) = make_uint4(x[0], x[1], x[2], x[3]);
-                } else if (t8) {
-                    reinterpret_cast<uint2*>(o)[0] = make_uint2(x[0], x[1]);
-                    reinterpret_cast<uint2*>(o)[1] = make_uint2(x[2], x[3]);
-                } else {
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = x[w];
-                }
-                acc = dot2_add(x[3], dot2_add(x[2], dot2_add(x[1], dot2_add(x[0], acc))));   // even offset
-                if (f.at + b0 == 0u) w1 = x[1];                 // transport bytes 4..7 (UDP crc: 6, 7)
-            }
-        };
-        // one fragment per step (two per step measured 145 -> 178 us on c3_reasm: 83 VGPRs, 6 waves
-        // per SIMD instead of 8)
-        for (uint32_t i = wv; i < m; i += 4u) {
-            const Frag f = frag_ctx(i);
             for (uint32_t u0 = 0; u0 < f.nu; u0 += 64u * U) {
                 uint4 c0[U], c1[U];
-                issue(f, u0, c0, c1);
-                consume(f, u0, c0, c1);
+#pragma unroll
+                for (int k = 0; k < U; ++k) {               // every load of the step first
+                    const uint32_t u = u0 + 64u * k + lane;
+                    c0[k] = load_win<true>(f.win, u < f.nu ? 16u * u : WIN_OOB);
+                    c1[k] = load_win<true>(f.win, u < f.nu && f.s ? 16u * u + 16u : WIN_OOB);
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const uint32_t u = u0 + 64u * k + lane;
+                    if (u >= f.nu) continue;
+                    const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+                    uint32_t x[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)             // bytes [s, s + 16) of the 32 loaded
+                        x[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
+                                                          sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sb);
+                    const uint32_t b0 = 16u * u, nb = min(16u, f.tl - b0);
+                    uint8_t* o = t + f.at + b0;
+                    if (nb < 16u) {                         // the fragment's last, partial unit
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) {
+                            const uint32_t lo = 4u * w;
+                            x[w] = nb <= lo ? 0u : nb >= lo + 4u ? x[w] : x[w] & ((1u << (8u * (nb - lo))) - 1u);
+                        }
+                        for (uint32_t qq = 0; qq < nb; ++qq) o[qq] = (uint8_t)(x[qq >> 2] >> (8u * (qq & 3u)));
+                    } else if (f.o16) {
+                        *reinterpret_cast<uint4*>(o) = make_uint4(x[0], x[1], x[2], x[3]);
+                    } else if (t8) {
+                        reinterpret_cast<uint2*>(o)[0] = make_uint2(x[0], x[1]);
+                        reinterpret_cast<uint2*>(o)[1] = make_uint2(x[2], x[3]);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = x[w];
+                    }
+                    acc = dot2_add(x[3], dot2_add(x[2], dot2_add(x[1], dot2_add(x[0], acc))));   // even offset
+                    if (f.at + b0 == 0u) w1 = x[1];         // transport bytes 4..7 (UDP crc: 6, 7)
+                }
             }
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
@@ -257,9 +244,10 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
         }
     }
     __syncthreads();
+    bad = L.bad != 0;
 
-    // ---- 5. pico_transport_crc_check on the reassembled frame
-    if (threadIdx.x == 0) {
+    // ---- 4. pico_transport_crc_check on the reassembled frame
+    if (tid == 0) {
         uint32_t l4 = 0, v = V_MALFORMED;
         const uint32_t len = L.len, proto = L.proto;
         if (!bad) {
