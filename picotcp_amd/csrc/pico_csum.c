@@ -162,10 +162,11 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
     if (group == 1 && unroll > 8)
         return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
-    if (group == 2 && (!(unroll == 0 || unroll == 1 || unroll == 4) || !(cpl == 4 || cpl == 8) ||
-                       (unroll == 1 && cpl != 8)))
+    if (group == 2 && (!(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4) || !(cpl == 4 || cpl == 8) ||
+                       ((unroll == 1 || unroll == 2) && cpl != 8)))
         return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8; unroll = narrowest round width "
-                                        "0 (auto), 1 (cpl 8 only) or 4");
+                                        "0 (auto), 1 (cpl 8 only), 2 (as 1, plus the span stream for dense "
+                                        "waves) or 4");
     if (group == 3 && (unroll != 0 || cpl != 8 || fpw != 16))
         return fail(PICO_CSUM_EINVAL, "per-wave adaptive kernel: unroll 0, cpl 8, fpw 16");
     if (group > 3 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
@@ -248,6 +249,9 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
     }
     return s;
 }
+
+/* sorted-rounds kernel: U -> the launcher's variant (1: 1-lane class, 2: + span stream) */
+#define SMALL_ARG(u) ((u) == 1 ? 1u : (u) == 2 ? 2u : 0u)
 
 /* Ablation bits for the sorted-rounds kernel (PICO_CSUM_ABLATE, measurement only):
  * 1 = skip the rounds, 2 = skip the head-window loads, 4 = skip the IPv4 TX crc writes.
@@ -341,7 +345,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
                                                      d_out, d_bad,
-                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, s.U == 1, 0, stream),
+                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U), 0, stream),
                              "pico_checksum_batch_dev");
     if (s.G == 1)
         return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
@@ -403,7 +407,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
                                                      NULL,
-                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
+                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U),
                                                      0, stream),
                              "pico_ipv4_checksum_batch_dev");
     if (s.G == 1)
@@ -440,7 +444,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
                                                      NULL, NULL,
-                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1, 0, stream),
+                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U), 0, stream),
                              "pico_ipv6_checksum_batch_dev");
     if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
         s.G = 1;
@@ -491,7 +495,7 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
         s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
     }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags | ablate_flags(), NULL, NULL,
-                                                 d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, s.U == 1,
+                                                 d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U),
                                                  mac48, stream),
                          "pico_eth_checksum_batch_dev");
 }

@@ -258,6 +258,17 @@ __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
     return v;
 }
 
+// Inclusive prefix maximum over the 64 lanes (the same DPP steps; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
 // Sum of the bytes of chunk v (chunk start at relative position ch) that lie in
 // [x0, x1) (relative to the same origin), frame-relative pairing via sel.
 // Branch-free: the 16-byte validity mask is built as two 64-bit masks.

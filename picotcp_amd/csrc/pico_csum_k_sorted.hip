@@ -3,6 +3,10 @@
 // Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
 #include "pico_csum_dev.h"
 
+#ifndef SORTED_MODE
+#define SORTED_MODE 0
+#endif
+
 namespace {
 
 #ifdef PICO_CSUM_STAMPS
@@ -145,6 +149,135 @@ __device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L
     }
 }
 
+// ---------------------------------------------------------------- span stream (dense waves)
+//
+// Most descriptor batches are bursts laid out back to back (a TAP / pico_device ring, the
+// C2 layout: datagrams behind 14-byte Ethernet headers).  For such a wave -- frames in
+// ascending, non-overlapping order, each >= 16 bytes, spanning little more than their own
+// bytes -- the rounds are replaced by ONE coalesced stream over the wave's span: step t
+// reads chunks 64t .. 64t+63 (1 KiB, lane l = chunk 64t + l; 8 steps in flight), so every
+// line is fetched once and whole, instead of lane groups touching many frames' partial
+// lines round after round (the rounds' traffic is 1.14-1.25x the bytes).  Per step:
+//   * owner: the frame whose first byte lies in the chunk, or the last one before it
+//     (a prefix max over a per-batch LDS scatter of frame starts);
+//   * the chunk's bytes inside the owner frame, with its pairing (v_perm for an odd
+//     start); a chunk also holding the previous frame's tail (frames start anywhere) adds
+//     that share to the previous frame through LDS (rare);
+//   * per-frame totals by a segmented sum: a wave prefix sum P, and lane j (= frame j)
+//     adds P[last chunk lane of j] - P[first - 1] -- plain uint32 arithmetic, exactly the
+//     reference's wrapping accumulator;
+//   * fused modes: chunks within a frame's first HW chunks are also written to its LDS
+//     head-window row, so the header is parsed from LDS as before.
+// The frame's region (transport) sum is then the total minus the bytes before the region
+// (Ethernet / IPv6 headers) and after it (padding), taken from the head window.
+struct StreamLds {
+    uint8_t owner[512];    // batch scatter: owner[c - first chunk of the batch] = frame + 1 starting in chunk c
+    uint2 ftab[64];        // frame j: {start, end}, bytes from the wave's first 16-byte line
+    uint32_t acc2[64];     // shares of chunks that hold a frame's tail and the next frame's head
+};
+template <bool STREAM>
+struct StreamSmem {
+    StreamLds s;
+};
+template <>
+struct StreamSmem<false> {
+    uint32_t s;
+};
+
+// Dense: every frame of the wave in bounds, >= 16 bytes (a chunk then holds at most two
+// frames) and < 64 KiB, each starting at or after the previous one's end, an even IPv6
+// network-header length in the seed (MODE 2 / 3: the transport pairing is the frame's), and
+// a span <= 1.25 x the frames' bytes + 4 KiB.  Wave-uniform.
+template <int MODE>
+__device__ __forceinline__ bool wave_dense(const FlatArgs& p, uint32_t lane, uint32_t cnt, bool oob, uint64_t off,
+                                           uint32_t len, uint32_t seed) {
+    const int prev = (int)(lane ? lane - 1u : 0u);
+    const uint64_t poff = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), prev) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)off, prev);
+    const uint32_t plen = (uint32_t)__shfl((int)len, prev);
+    bool ok = lane >= cnt || (!oob && len >= 16u && len < 65536u && (lane == 0 || off >= poff + plen));
+    if (MODE == 2 || MODE == 3) ok = ok && (lane >= cnt || (seed & 1u) == 0u);
+    if (__builtin_amdgcn_ballot_w64(!ok)) return false;
+    const uint64_t a = reinterpret_cast<uintptr_t>(p.base) + off;
+    const uint64_t first = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a)) & ~(uint64_t)15;
+    const uint64_t end = a + len;
+    const uint64_t last = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end >> 32), (int)cnt - 1) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)cnt - 1);
+    const uint32_t bytes = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(lane < cnt ? len : 0u), 63);
+    const uint64_t span = last - first;
+    return span < (1u << 24) && span <= (uint64_t)bytes + (bytes >> 2) + 4096u;
+}
+
+// The stream over a dense wave's span; returns lane j's frame total (pairing from the
+// frame's start), fills the head-window rows (fused modes).
+template <int MODE>
+__device__ __forceinline__ uint32_t span_stream(const FlatArgs& p, StreamLds& T, uint4* stage, uint32_t lane,
+                                                uint32_t cnt, uint64_t off, uint32_t len) {
+    const uint64_t a = reinterpret_cast<uintptr_t>(p.base) + off;
+    const uint64_t B = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a)) & ~(uint64_t)15;
+    const uint32_t s = lane < cnt ? (uint32_t)(a - B) : 0u, e = s + (lane < cnt ? len : 0u);
+    const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)cnt - 1);
+    if (lane < cnt) T.ftab[lane] = make_uint2(s, e);
+    T.acc2[lane] = 0u;
+    reinterpret_cast<uint64_t*>(T.owner)[lane] = 0ull;
+    const uint32_t fc = s >> 4;                                   // the chunk of the frame's first byte
+    const uint32_t nxt = (uint32_t)__shfl((int)s, (int)min(lane + 1u, 63u));
+    const uint32_t nc = lane + 1u < cnt ? nxt >> 4 : (e + 15u) >> 4;   // chunks [fc, nc) are this frame's own
+    const uint32_t nsteps = (E + 1023u) >> 10;
+    const Window w = make_window(B, (E + 15u) & ~15u);
+    uint32_t acc = 0u, carry = 0u;
+    asm volatile("" ::: "memory");
+    for (uint32_t tb = 0; tb < nsteps; tb += 8u) {
+        const uint32_t cb = tb << 6;                              // the batch's first chunk
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) v[k] = load_win<false>(w, (cb + 64u * k + lane) << 4);
+        if (lane < cnt && fc >= cb && fc < cb + 512u) T.owner[fc - cb] = (uint8_t)(lane + 1u);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) {
+            const uint32_t ci = cb + 64u * k + lane, c16 = ci << 4;
+            uint32_t o = T.owner[64u * k + lane];
+            T.owner[64u * k + lane] = 0;
+            o = max(wave_scan_max(o), carry);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+            const uint32_t f = o - 1u;                             // >= 0: chunk 0 holds frame 0's start
+            const uint2 fe = T.ftab[f];
+            uint32_t val = masked_chunk_sum<true>(v[k], c16, fe.x, fe.y, (fe.x & 1u) ? SEL_ODD : SEL_EVEN);
+            if constexpr (MODE != 0) {
+                const uint32_t wi = ci - (fe.x >> 4);
+                if (wi < HW) stage[f * HW + (wi ^ (f & (HW - 1u)))] = v[k];
+            }
+            if (__builtin_amdgcn_ballot_w64(f > 0u && c16 < fe.x)) {     // the previous frame's tail too?
+                if (f > 0u && c16 < fe.x) {
+                    const uint2 pe = T.ftab[f - 1u];
+                    if (pe.y > c16) {
+                        atomicAdd(&T.acc2[f - 1u], masked_chunk_sum<true>(v[k], c16, pe.x, pe.y,
+                                                                          (pe.x & 1u) ? SEL_ODD : SEL_EVEN));
+                        if constexpr (MODE != 0) {
+                            const uint32_t wi = ci - (pe.x >> 4);
+                            if (wi < HW) stage[(f - 1u) * HW + (wi ^ ((f - 1u) & (HW - 1u)))] = v[k];
+                        }
+                    }
+                }
+            }
+            const uint32_t P = wave_scan_add(val);
+            const uint32_t bc = cb + 64u * k;
+            const bool in = lane < cnt && fc < bc + 64u && nc > bc;
+            const uint32_t lo = fc > bc ? fc - bc : 0u, hi = in ? min(nc - bc, 64u) : 1u;
+            const uint32_t Ph = (uint32_t)__shfl((int)P, (int)hi - 1);
+            const uint32_t Pl = (uint32_t)__shfl((int)P, lo ? (int)lo - 1 : 0);
+            if (in) acc += Ph - (lo ? Pl : 0u);
+        }
+        asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    return acc + T.acc2[lane];
+}
+
 // MODE: 0 RAW (p.crc_off / p.flags / p.out / p.bad), 1 fused IPv4, 2 fused IPv6,
 // 3 Ethernet front end (per frame: destination filter, ethertype -> IPv4 / IPv6 / ARP / drop;
 // pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in Ipv4Args-compatible fields of FlatArgs.
@@ -257,9 +390,9 @@ __device__ __forceinline__ void window_words(const uint4 (&hw)[HW], uint32_t pos
 // CPL 8 keeps 8 KiB of loads in flight per wave within 128 VGPRs (4 waves per
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
-template <int MODE, bool NT, int CPL, bool SMALL>
-__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, uint32_t lane,
-                                             uint64_t f0) {
+template <int MODE, bool NT, int CPL, bool SMALL, bool STREAM>
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, StreamSmem<STREAM>& SS,
+                                             uint32_t lane, uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2, ETH = MODE == 3;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = MODE != 0 && (p.flags & 2u) != 0;
@@ -276,6 +409,15 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
     uint64_t a0off = off - r;
     uint32_t odd = r & 1u;
+    const uint32_t r_desc = r;                   // the descriptor's start in its head window
+
+    // dense waves: the span stream (phase 1 then parses from the rows it filled; no rounds)
+    bool dense = false;
+    uint32_t total = 0;
+    if constexpr (STREAM) {
+        dense = wave_dense<MODE>(p, lane, cnt, oob, off, len, seed);
+        if (dense) total = span_stream<MODE>(p, SS.s, stage, lane, cnt, off, len);
+    }
 
     uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, l2v = 0;
@@ -296,7 +438,12 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         // rounds start behind the window (or are skipped).
         constexpr uint32_t HDR = IPV6 ? 40u : IPV4 ? 20u : 14u;
         nlh = len >= HDR && !(p.flags & 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;   // 0x200: ablation
-        {
+        if (STREAM && dense) {
+#pragma unroll
+            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * HW + (i ^ (lane & (HW - 1)))];
+            staged = true;
+            asm volatile("" ::: "memory");
+        } else {
             // Buffer loads through a window over the batch (from base's 16-byte line to
             // base_len rounded up -- the bytes load_chunk may touch -- at most 2 GiB, from
             // 1 GiB below the wave's first frame): all HW slots issue back to back and
@@ -474,7 +621,61 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     }
     const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
     uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
-    if constexpr (MODE != 0) {
+    if constexpr (STREAM && MODE == 0) {
+        if (dense) {
+            p_all = total;
+            if (xpos != NONE) {                  // the crc field's word (crc_off even: frame pairing)
+                const uint8_t* q = p.base + a0off + xpos;
+                p_x = (uint32_t)q[0] | ((uint32_t)q[1] << 8);
+            }
+            nch = 0;
+        }
+    }
+    if constexpr (STREAM && MODE != 0) {
+        if (dense) {
+            // window coordinates (origin a0h): the descriptor's bytes [r_desc, r_desc + len), the
+            // region [rs, rs + span); region = total - the bytes before it - the bytes after it
+            // (even offsets apart: one pairing throughout)
+            const uint32_t d = (uint32_t)((a0off - a0h) >> 4);
+            const uint32_t rs = 16u * d + r, sl = odd ? SEL_ODD : SEL_EVEN;
+            const uint32_t e0 = r_desc + len;
+            auto range_sum = [&](uint32_t x0, uint32_t x1) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < HW; ++i)
+                    if (x1 > x0 && 16u * i < x1 && 16u * i + 16u > x0) acc += masked_chunk_sum<true>(hw[i], 16u * i, x0, x1, sl);
+                if (x1 > x0 && x1 > 16u * HW)
+                    for (uint32_t k = max(HW, x0 >> 4); 16u * k < x1; ++k)
+                        acc += masked_chunk_sum<true>(load_chunk(p.base + a0h, k), 16u * k, x0, x1, sl);
+                return acc;
+            };
+            const bool cut = parsed && (rs > r_desc || rs + span < e0);
+            uint32_t c = 0;
+            if (__builtin_amdgcn_ballot_w64(cut)) {
+                if (cut) c = range_sum(r_desc, rs) + range_sum(rs + span, e0);
+            }
+            p_all = total - c;
+            if (xpos != NONE) {
+                const uint32_t xs = 16u * d + xpos;
+                if (xs + 2u <= 16u * HW) {
+                    const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
+                    const uint32_t sw = (lane & (HW - 1)) << 4;
+                    p_x = (uint32_t)row[xs ^ sw] | ((uint32_t)row[(xs + 1u) ^ sw] << 8);
+                } else {
+                    const uint8_t* q = p.base + a0h + xs;
+                    p_x = (uint32_t)q[0] | ((uint32_t)q[1] << 8);
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(optend != 0u)) {      // IPv4 options (always inside the window)
+                if (optend != 0u) p_opt = range_sum(rs + 20u, 16u * d + optend);
+            }
+            asm volatile("" ::: "memory");
+            xpos = NONE;
+            optend = 0;
+            nch = 0;
+        }
+    }
+    if (MODE != 0 && !(STREAM && dense)) {
         // sums over the head window: the region's chunks [0, k0) = window chunks
         // [d, d + k0) (d: where the region's chunk grid starts in the window -- IPv6:
         // behind the header); the rounds take region chunks [k0, nch).  A field
@@ -618,17 +819,19 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
-template <int MODE, bool NT, int CPL, bool SMALL = false>
-__global__ __launch_bounds__(256, CPL == 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+template <int MODE, bool NT, int CPL, bool SMALL = false, bool STREAM = false>
+__global__ __launch_bounds__(256, CPL >= 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveSmem<MODE != 0> lds_all[4];
+    __shared__ StreamSmem<STREAM> lds_stream[4];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
     STAMP(0);
-    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL, STREAM>(p, S.s, S.stage, lds_stream[threadIdx.x >> 6], lane, f0);
     STAMP(3);
 }
 
+#if SORTED_MODE == 0
 // ---------------------------------------------------------------- IPv4 forwarding step
 //
 // pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) on a batch of datagrams that are
@@ -672,43 +875,75 @@ __global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
 }
 
 
+#endif
+
 }  // namespace
+
+#define SORTED_CAT2(a, b) a##b
+#define SORTED_CAT(a, b) SORTED_CAT2(a, b)
 
 extern "C" {
 
 #ifdef PICO_CSUM_STAMPS
-int pico_csum_diag_set_stamps(void* d_buf, uint32_t waves) {
+int SORTED_CAT(pico_csum_diag_stamps_mode, SORTED_MODE)(void* d_buf, uint32_t waves);
+int SORTED_CAT(pico_csum_diag_stamps_mode, SORTED_MODE)(void* d_buf, uint32_t waves) {
     uint64_t* b = static_cast<uint64_t*>(d_buf);
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &b, sizeof(b)) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_n), &waves, sizeof(waves)) != hipSuccess) return -1;
     return 0;
 }
+#if SORTED_MODE == 0
+int pico_csum_diag_stamps_mode1(void*, uint32_t);
+int pico_csum_diag_stamps_mode2(void*, uint32_t);
+int pico_csum_diag_stamps_mode3(void*, uint32_t);
+int pico_csum_diag_set_stamps(void* d_buf, uint32_t waves) {
+    return pico_csum_diag_stamps_mode0(d_buf, waves) | pico_csum_diag_stamps_mode1(d_buf, waves) |
+           pico_csum_diag_stamps_mode2(d_buf, waves) | pico_csum_diag_stamps_mode3(d_buf, waves);
+}
+#endif
 #endif
 
-// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6; small: 1-lane
-// rounds for frames of <= 8 chunks (cpl 8 only).
-// mode 3: Ethernet front end; mac48 = the device MAC's 6 bytes (little-endian in a uint64),
-// used when flags carry F_MACF (set by the host layer).
+// One kernel table per mode: this TU is compiled once per SORTED_MODE (parallel build).
+#define SORTED_LAUNCH SORTED_CAT(pico_csum_sorted_launch_mode, SORTED_MODE)
+int SORTED_LAUNCH(const void* args, uint32_t nt, int v, void* stream);
+int SORTED_LAUNCH(const void* args, uint32_t nt, int v, void* stream) {
+    const FlatArgs& a = *static_cast<const FlatArgs*>(args);
+    using K = void (*)(FlatArgs);
+    constexpr int M = SORTED_MODE;
+    // [nt][cpl 4 | cpl 8 | cpl 8 + 1-lane | cpl 8 + 1-lane + span stream]
+#define SK(t) {csum_sorted_kernel<M, t, 4>, csum_sorted_kernel<M, t, 8>, csum_sorted_kernel<M, t, 8, true>,       \
+               csum_sorted_kernel<M, t, 8, true, true>}
+    static const K table[2][4] = {SK(false), SK(true)};
+#undef SK
+    hipLaunchKernelGGL(table[nt ? 1 : 0][v], grid_for(a.n, a.fpw), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
+}
+
+#if SORTED_MODE == 0
+int pico_csum_sorted_launch_mode1(const void* args, uint32_t nt, int v, void* stream);
+int pico_csum_sorted_launch_mode2(const void* args, uint32_t nt, int v, void* stream);
+int pico_csum_sorted_launch_mode3(const void* args, uint32_t nt, int v, void* stream);
+
+// Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6, 3 Ethernet front end;
+// small (cpl 8 only): 0 none, 1 the 1-lane class, 2 the 1-lane class + the span stream for dense waves.
+// mac48 = the device MAC's 6 bytes (little-endian in a uint64), used when flags carry F_MACF
+// (set by the host layer).
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
                             uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
                             uint64_t mac48, void* stream) {
-    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 3 || (small && cpl != 8))
+    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 3 || small > 2 || (small && cpl != 8))
         return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32)};
-    const dim3 grid = grid_for(n, fpw), block(256);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    using K = void (*)(FlatArgs);
-    // [mode][nt][cpl 4 | cpl 8 | cpl 8 with the 1-lane class]
-#define SK(m, t) {csum_sorted_kernel<m, t, 4>, csum_sorted_kernel<m, t, 8>, csum_sorted_kernel<m, t, 8, true>}
-    static const K table[4][2][3] = {{SK(0, false), SK(0, true)}, {SK(1, false), SK(1, true)},
-                                     {SK(2, false), SK(2, true)}, {SK(3, false), SK(3, true)}};
-#undef SK
-    const int v = cpl == 4 ? 0 : small ? 2 : 1;
-    hipLaunchKernelGGL(table[mode][nt ? 1 : 0][v], grid, block, 0, s, a);
-    return (int)hipGetLastError();
+    const int v = cpl == 4 ? 0 : (int)small + 1;
+    switch (mode) {
+        case 0: return pico_csum_sorted_launch_mode0(&a, nt, v, stream);
+        case 1: return pico_csum_sorted_launch_mode1(&a, nt, v, stream);
+        case 2: return pico_csum_sorted_launch_mode2(&a, nt, v, stream);
+        default: return pico_csum_sorted_launch_mode3(&a, nt, v, stream);
+    }
 }
 
 int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, uint8_t* verdict,
@@ -719,5 +954,6 @@ int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* des
     hipLaunchKernelGGL(ipv4_forward_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
+#endif  // SORTED_MODE == 0
 
 }  // extern "C"

@@ -109,7 +109,11 @@ def test_launch_override_validation():
     assert lib.pico_csum_set_launch_override(1, 4, 9, 7, 1, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(1, 4, 0, 7, 1, 0) == 0
     assert lib.pico_csum_set_launch_override(2, 8, 0, 37, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 8, 2, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 8, 3, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 8, 2, 16, 2, 0) == 0
+    assert lib.pico_csum_set_launch_override(2, 16, 2, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 4, 2, 16, 2, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(4, 16, 1, 16, 2, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(2, 4, 1, 16, 2, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(2, 8, 1, 16, 2, 0) == 0
     assert lib.pico_csum_set_launch_override(2, 8, 4, 16, 2, 0) == 0

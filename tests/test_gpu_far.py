@@ -43,7 +43,7 @@ def test_far_apart_over_2gib(ipv6):
     d_desc = batch.desc_to_device(far, DEV)
     for tx in (False, True):
         fl = batch.F_TX if tx else 0
-        for shape in (None, (2, 8, 64, 1, 2), (2, 8, 64, 0, 2)):
+        for shape in (None, (2, 8, 64, 1, 2), (2, 8, 64, 0, 2), (2, 8, 64, 2, 2)):
             if shape is None:
                 batch.set_launch_override(0)
             else:

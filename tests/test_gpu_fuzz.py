@@ -31,7 +31,7 @@ def to_dev(a):
 
 
 # launch shapes exercised for descriptor batches: auto (adaptive), flat, lane groups
-DESC_SHAPES = [None, (3, 8, 16, 0, 1), (2, 8, 64, 4, 2), (2, 8, 5, 4, 1), (2, 8, 64, 1, 2), (2, 8, 5, 1, 1), (2, 4, 33, 0, 1), (1, 1, 1, 0, 1), (1, 4, 64, 0, 2), (1, 2, 7, 2, 1), (4, 8, 16, 1, 1), (64, 2, 4, 1, 2),
+DESC_SHAPES = [None, (3, 8, 16, 0, 1), (2, 8, 64, 2, 2), (2, 8, 6, 2, 1), (2, 8, 64, 4, 2), (2, 8, 5, 4, 1), (2, 8, 64, 1, 2), (2, 8, 5, 1, 1), (2, 4, 33, 0, 1), (1, 1, 1, 0, 1), (1, 4, 64, 0, 2), (1, 2, 7, 2, 1), (4, 8, 16, 1, 1), (64, 2, 4, 1, 2),
                (16, 8, 12, 1, 1)]
 
 
@@ -102,7 +102,7 @@ def test_fuzz_ipv4(trial, tx):
     desc["seed"] = 0
     wn, wl, wv = O.batch_ipv4(buf, desc, tx=tx)
     d_desc = batch.desc_to_device(desc, DEV)
-    for shape in (None, (2, 8, 64, 4, 2), (2, 8, 3, 4, 1), (2, 8, 64, 1, 2), (2, 8, 3, 1, 1), (1, 1, 5, 0, 1), (1, 8, 64, 0, 2), (4, 8, 16, 1, 1),
+    for shape in (None, (2, 8, 64, 2, 2), (2, 8, 3, 2, 1), (2, 8, 64, 4, 2), (2, 8, 3, 4, 1), (2, 8, 64, 1, 2), (2, 8, 3, 1, 1), (1, 1, 5, 0, 1), (1, 8, 64, 0, 2), (4, 8, 16, 1, 1),
                   (32, 2, 64, 1, 1)):
         if shape is None:
             batch.set_launch_override(0)
@@ -122,7 +122,7 @@ def test_fuzz_ipv6(trial, tx):
     buf, desc = random_datagrams(rng, n, ipv6=True)
     wl, wv = O.batch_ipv6(buf, desc, tx=tx)
     d_desc = batch.desc_to_device(desc, DEV)
-    for shape in (None, (2, 8, 64, 4, 2), (2, 8, 7, 4, 1), (2, 8, 64, 1, 2), (2, 8, 7, 1, 1), (1, 1, 3, 0, 1), (1, 8, 64, 0, 2)):
+    for shape in (None, (2, 8, 64, 2, 2), (2, 8, 7, 2, 1), (2, 8, 64, 4, 2), (2, 8, 7, 4, 1), (2, 8, 64, 1, 2), (2, 8, 7, 1, 1), (1, 1, 3, 0, 1), (1, 8, 64, 0, 2)):
         if shape is None:
             batch.set_launch_override(0)
         else:

@@ -20,7 +20,7 @@ DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)] + [(2, 4), (2, 8)]
 # override per descriptor kernel for the kernel-parametrized tests
 KERNELS = {"auto": None, "adaptive": (3, 8, 16, 0, 1), "flat": (1, 4, 8, 1, 1), "sorted": (2, 8, 64, 4, 2),
            "sorted_fpw7": (2, 8, 7, 4, 1), "sorted_c4": (2, 4, 13, 0, 1), "sorted_small": (2, 8, 64, 1, 2),
-           "sorted_small_fpw5": (2, 8, 5, 1, 1)}
+           "sorted_small_fpw5": (2, 8, 5, 1, 1), "sorted_stream": (2, 8, 64, 2, 2), "sorted_stream_fpw9": (2, 8, 9, 2, 1)}
 
 
 def fpws(g):
