@@ -153,41 +153,44 @@ __device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L
 //
 // Most descriptor batches are bursts laid out back to back (a TAP / pico_device ring, the
 // C2 layout: datagrams behind 14-byte Ethernet headers).  For such a wave -- frames in
-// ascending, non-overlapping order, each >= 16 bytes, spanning little more than their own
-// bytes -- the rounds are replaced by ONE coalesced stream over the wave's span: step t
-// reads chunks 64t .. 64t+63 (1 KiB, lane l = chunk 64t + l; 8 steps in flight), so every
-// line is fetched once and whole, instead of lane groups touching many frames' partial
-// lines round after round (the rounds' traffic is 1.14-1.25x the bytes).  Per step:
-//   * owner: the frame whose first byte lies in the chunk, or the last one before it
-//     (a prefix max over a per-batch LDS scatter of frame starts);
-//   * the chunk's bytes inside the owner frame, with its pairing (v_perm for an odd
-//     start); a chunk also holding the previous frame's tail (frames start anywhere) adds
-//     that share to the previous frame through LDS (rare);
-//   * per-frame totals by a segmented sum: a wave prefix sum P, and lane j (= frame j)
-//     adds P[last chunk lane of j] - P[first - 1] -- plain uint32 arithmetic, exactly the
-//     reference's wrapping accumulator;
-//   * fused modes: chunks within a frame's first HW chunks are also written to its LDS
-//     head-window row, so the header is parsed from LDS as before.
-// The frame's region (transport) sum is then the total minus the bytes before the region
-// (Ethernet / IPv6 headers) and after it (padding), taken from the head window.
+// ascending order, each >= 16 bytes and < 64 KiB, gaps < 16 bytes -- the rounds are replaced
+// by ONE coalesced stream over the wave's span: step t reads chunks 64t .. 64t+63 (1 KiB, lane
+// l = chunk 64t + l; 8 steps in flight), so every line is fetched once and whole.  Per step,
+// no masks: each chunk gives two unmasked sums in the batch's own (absolute) pairing,
+// a = E + 256 O (v_dot2) and b = E + O (v_sad_u8); a frame owns the whole chunks from the one
+// holding its first byte up to the next frame's, and lane j (= frame j) adds its owned
+// chunks' a and b through two wave prefix sums (differences: exact, the reference's
+// wrapping uint32 arithmetic).  Once per frame: the bytes before its start in the first chunk
+// and past its end in the last (or its tail in the next frame's first chunk) are corrected
+// from those two chunks (kept in LDS), and an odd start swaps the pairing:
+// O = (a - b) / 255, E = b - O, sum = O + 256 E (exact: a frame < 64 KiB never wraps a).
+// Fused modes: a chunk inside a frame's first HW chunks is also written to its LDS
+// head-window row (the owner frame: a ballot of the chunks holding a frame's first byte +
+// mbcnt), so the header is parsed from LDS as before; the region (transport) sum is the total
+// minus the bytes before the region (Ethernet / IPv6 headers) and after it (padding).
+template <bool RAWM>
 struct StreamLds {
-    uint8_t owner[512];    // batch scatter: owner[c - first chunk of the batch] = frame + 1 starting in chunk c
-    uint2 ftab[64];        // frame j: {start, end}, bytes from the wave's first 16-byte line
-    uint32_t acc2[64];     // shares of chunks that hold a frame's tail and the next frame's head
-};
-template <bool STREAM>
-struct StreamSmem {
-    StreamLds s;
+    uint16_t mk[512];      // batch markers, chunk c: low byte = frame + 1 whose first byte, high = last byte is in c
+    uint4 tbuf[64];        // frame j's last chunk
+    uint4 hbuf[64];        // frame j's first chunk (RAW; the fused modes have it in the head-window row)
 };
 template <>
-struct StreamSmem<false> {
+struct StreamLds<false> {
+    uint16_t mk[512];
+    uint4 tbuf[64];
+};
+template <bool STREAM, bool RAWM>
+struct StreamSmem {
+    StreamLds<RAWM> s;
+};
+template <bool RAWM>
+struct StreamSmem<false, RAWM> {
     uint32_t s;
 };
 
-// Dense: every frame of the wave in bounds, >= 16 bytes (a chunk then holds at most two
-// frames) and < 64 KiB, each starting at or after the previous one's end, an even IPv6
-// network-header length in the seed (MODE 2 / 3: the transport pairing is the frame's), and
-// a span <= 1.25 x the frames' bytes + 4 KiB.  Wave-uniform.
+// Dense: every frame of the wave in bounds, >= 16 bytes and < 64 KiB, each starting at or after
+// the previous one's end and less than 16 bytes behind it, and an even IPv6 network-header
+// length in the seed (MODE 2 / 3: the transport pairing is the frame's).  Wave-uniform.
 template <int MODE>
 __device__ __forceinline__ bool wave_dense(const FlatArgs& p, uint32_t lane, uint32_t cnt, bool oob, uint64_t off,
                                            uint32_t len, uint32_t seed) {
@@ -195,87 +198,132 @@ __device__ __forceinline__ bool wave_dense(const FlatArgs& p, uint32_t lane, uin
     const uint64_t poff = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), prev) << 32) |
                           (uint32_t)__shfl((int)(uint32_t)off, prev);
     const uint32_t plen = (uint32_t)__shfl((int)len, prev);
-    bool ok = lane >= cnt || (!oob && len >= 16u && len < 65536u && (lane == 0 || off >= poff + plen));
+    bool ok = lane >= cnt || (!oob && len >= 16u && len < 65536u &&
+                              (lane == 0 || (off >= poff + plen && off < poff + plen + 16u)));
     if (MODE == 2 || MODE == 3) ok = ok && (lane >= cnt || (seed & 1u) == 0u);
-    if (__builtin_amdgcn_ballot_w64(!ok)) return false;
-    const uint64_t a = reinterpret_cast<uintptr_t>(p.base) + off;
-    const uint64_t first = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a)) & ~(uint64_t)15;
-    const uint64_t end = a + len;
-    const uint64_t last = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end >> 32), (int)cnt - 1) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)cnt - 1);
-    const uint32_t bytes = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(lane < cnt ? len : 0u), 63);
-    const uint64_t span = last - first;
-    return span < (1u << 24) && span <= (uint64_t)bytes + (bytes >> 2) + 4096u;
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
+// Masked sums of chunk v's bytes in [x0, x1) (positions from the batch's 16-byte line, absolute
+// pairing): a = E + 256 O, b = E + O.
+__device__ __forceinline__ void masked_ab(const uint4 v, uint32_t ch, uint32_t x0, uint32_t x1, uint32_t& a,
+                                          uint32_t& b) {
+    const uint32_t lo = x0 <= ch ? 0u : min(x0 - ch, 16u);
+    const uint32_t hi = x1 <= ch ? 0u : min(x1 - ch, 16u);
+    const uint64_t ALL = ~0ull;
+    uint64_t m0 = lo >= 8u ? 0ull : (ALL << (8u * lo));
+    m0 &= hi >= 8u ? ALL : ~(ALL << (8u * hi));
+    uint64_t m1 = lo >= 16u ? 0ull : (lo <= 8u ? ALL : (ALL << (8u * (lo - 8u))));
+    m1 &= hi >= 16u ? ALL : (hi <= 8u ? 0ull : ~(ALL << (8u * (hi - 8u))));
+    const uint32_t x = v.x & (uint32_t)m0, y = v.y & (uint32_t)(m0 >> 32);
+    const uint32_t z = v.z & (uint32_t)m1, w = v.w & (uint32_t)(m1 >> 32);
+    a = dot2_add(w, dot2_add(z, dot2_add(y, dot2_add(x, 0u))));
+    b = __builtin_amdgcn_sad_u8(w, 0u, __builtin_amdgcn_sad_u8(z, 0u, __builtin_amdgcn_sad_u8(y, 0u, __builtin_amdgcn_sad_u8(x, 0u, 0u))));
 }
 
 // The stream over a dense wave's span; returns lane j's frame total (pairing from the
 // frame's start), fills the head-window rows (fused modes).
 template <int MODE>
-__device__ __forceinline__ uint32_t span_stream(const FlatArgs& p, StreamLds& T, uint4* stage, uint32_t lane,
-                                                uint32_t cnt, uint64_t off, uint32_t len) {
-    const uint64_t a = reinterpret_cast<uintptr_t>(p.base) + off;
-    const uint64_t B = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a)) & ~(uint64_t)15;
-    const uint32_t s = lane < cnt ? (uint32_t)(a - B) : 0u, e = s + (lane < cnt ? len : 0u);
+__device__ __forceinline__ uint32_t span_stream(const FlatArgs& p, StreamLds<MODE == 0>& T, uint4* stage,
+                                                uint32_t lane, uint32_t cnt, uint64_t off, uint32_t len) {
+    const uint64_t a0 = reinterpret_cast<uintptr_t>(p.base) + off;
+    const uint64_t B = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a0 >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a0)) & ~(uint64_t)15;
+    const bool fr = lane < cnt;
+    const uint32_t s = fr ? (uint32_t)(a0 - B) : 0u, e = fr ? s + len : 16u;
     const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)cnt - 1);
-    if (lane < cnt) T.ftab[lane] = make_uint2(s, e);
-    T.acc2[lane] = 0u;
-    reinterpret_cast<uint64_t*>(T.owner)[lane] = 0ull;
-    const uint32_t fc = s >> 4;                                   // the chunk of the frame's first byte
-    const uint32_t nxt = (uint32_t)__shfl((int)s, (int)min(lane + 1u, 63u));
-    const uint32_t nc = lane + 1u < cnt ? nxt >> 4 : (e + 15u) >> 4;   // chunks [fc, nc) are this frame's own
+    const uint32_t fc = s >> 4, tc = (e - 1u) >> 4;                  // first / last chunk
+    const uint32_t nfc = (uint32_t)__shfl((int)fc, (int)min(lane + 1u, 63u));
+    const uint32_t oe = lane + 1u < cnt ? nfc : tc + 1u;               // owned chunks [fc, oe)
+    reinterpret_cast<uint4*>(T.mk)[lane] = make_uint4(0, 0, 0, 0);
+    uint8_t* mk8 = reinterpret_cast<uint8_t*>(T.mk);
     const uint32_t nsteps = (E + 1023u) >> 10;
     const Window w = make_window(B, (E + 15u) & ~15u);
-    uint32_t acc = 0u, carry = 0u;
+    uint32_t accA = 0u, accB = 0u, carry = 0u;
     asm volatile("" ::: "memory");
-    for (uint32_t tb = 0; tb < nsteps; tb += 8u) {
-        const uint32_t cb = tb << 6;                              // the batch's first chunk
-        uint4 v[8];
+    // one batch = 8 steps (8 KiB) of loads in flight (loads past the span read zeros without a
+    // memory access)
+    auto load_batch = [&](uint4 (&v)[8], uint32_t tb) {
 #pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) v[k] = load_win<false>(w, (cb + 64u * k + lane) << 4);
-        if (lane < cnt && fc >= cb && fc < cb + 512u) T.owner[fc - cb] = (uint8_t)(lane + 1u);
+        for (uint32_t k = 0; k < 8u; ++k) v[k] = load_win<false>(w, ((tb << 6) + 64u * k + lane) << 4);
+    };
+    auto sum_batch = [&](const uint4 (&v)[8], uint32_t tb) {
+        const uint32_t cb = tb << 6;                              // the batch's first chunk
+        if (fr && fc >= cb && fc < cb + 512u) mk8[2u * (fc - cb)] = (uint8_t)(lane + 1u);
+        if (fr && tc >= cb && tc < cb + 512u) mk8[2u * (tc - cb) + 1u] = (uint8_t)(lane + 1u);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (uint32_t k = 0; k < 8u; ++k) {
-            const uint32_t ci = cb + 64u * k + lane, c16 = ci << 4;
-            uint32_t o = T.owner[64u * k + lane];
-            T.owner[64u * k + lane] = 0;
-            o = max(wave_scan_max(o), carry);
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
-            const uint32_t f = o - 1u;                             // >= 0: chunk 0 holds frame 0's start
-            const uint2 fe = T.ftab[f];
-            uint32_t val = masked_chunk_sum<true>(v[k], c16, fe.x, fe.y, (fe.x & 1u) ? SEL_ODD : SEL_EVEN);
+            const uint32_t ci = cb + 64u * k + lane;
+            const uint32_t m = T.mk[64u * k + lane];
+            T.mk[64u * k + lane] = 0;
+            const uint32_t hd = m & 0xFFu, tl = m >> 8;
+            const uint64_t M = __builtin_amdgcn_ballot_w64(hd != 0u);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+            const uint32_t f = min(carry + below + (hd ? 1u : 0u), 64u) - 1u;   // the owner (last frame started)
+            carry += (uint32_t)__builtin_popcountll(M);
+            const uint4 x = v[k];
+            const uint32_t a = dot2_add(x.w, dot2_add(x.z, dot2_add(x.y, dot2_add(x.x, 0u))));
+            const uint32_t b = __builtin_amdgcn_sad_u8(x.w, 0u, __builtin_amdgcn_sad_u8(x.z, 0u,
+                               __builtin_amdgcn_sad_u8(x.y, 0u, __builtin_amdgcn_sad_u8(x.x, 0u, 0u))));
             if constexpr (MODE != 0) {
-                const uint32_t wi = ci - (fe.x >> 4);
-                if (wi < HW) stage[f * HW + (wi ^ (f & (HW - 1u)))] = v[k];
+                const uint32_t t = tl ? tl - 1u : f;
+                const uint32_t ffc = (uint32_t)__shfl((int)fc, (int)f), ftc = (uint32_t)__shfl((int)tc, (int)f);
+                const uint32_t tfc = (uint32_t)__shfl((int)fc, (int)t);
+                const uint32_t wi = ci - ffc, wt = ci - tfc;
+                if (wi < HW && ci <= ftc) stage[f * HW + (wi ^ (f & (HW - 1u)))] = x;
+                if (tl && t != f && wt < HW) stage[t * HW + (wt ^ (t & (HW - 1u)))] = x;
+            } else {
+                if (hd) T.hbuf[hd - 1u] = x;
             }
-            if (__builtin_amdgcn_ballot_w64(f > 0u && c16 < fe.x)) {     // the previous frame's tail too?
-                if (f > 0u && c16 < fe.x) {
-                    const uint2 pe = T.ftab[f - 1u];
-                    if (pe.y > c16) {
-                        atomicAdd(&T.acc2[f - 1u], masked_chunk_sum<true>(v[k], c16, pe.x, pe.y,
-                                                                          (pe.x & 1u) ? SEL_ODD : SEL_EVEN));
-                        if constexpr (MODE != 0) {
-                            const uint32_t wi = ci - (pe.x >> 4);
-                            if (wi < HW) stage[(f - 1u) * HW + (wi ^ ((f - 1u) & (HW - 1u)))] = v[k];
-                        }
-                    }
-                }
-            }
-            const uint32_t P = wave_scan_add(val);
+            if (tl) T.tbuf[tl - 1u] = x;
+            const uint32_t PA = wave_scan_add(a), PB = wave_scan_add(b);
             const uint32_t bc = cb + 64u * k;
-            const bool in = lane < cnt && fc < bc + 64u && nc > bc;
-            const uint32_t lo = fc > bc ? fc - bc : 0u, hi = in ? min(nc - bc, 64u) : 1u;
-            const uint32_t Ph = (uint32_t)__shfl((int)P, (int)hi - 1);
-            const uint32_t Pl = (uint32_t)__shfl((int)P, lo ? (int)lo - 1 : 0);
-            if (in) acc += Ph - (lo ? Pl : 0u);
+            const bool in = fr && fc < bc + 64u && oe > bc;
+            const uint32_t lo = fc > bc ? fc - bc : 0u, hi = in ? min(oe - bc, 64u) : 1u;
+            const int ih = (int)hi - 1, il = lo ? (int)lo - 1 : 0;
+            const uint32_t PAh = (uint32_t)__shfl((int)PA, ih), PAl = (uint32_t)__shfl((int)PA, il);
+            const uint32_t PBh = (uint32_t)__shfl((int)PB, ih), PBl = (uint32_t)__shfl((int)PB, il);
+            if (in) {
+                accA += PAh - (lo ? PAl : 0u);
+                accB += PBh - (lo ? PBl : 0u);
+            }
         }
         asm volatile("" ::: "memory");
+    };
+    // (two batches in flight -- the next one's loads issued before the current one is summed --
+    // measured slower: C2 35.4 vs 32.6 us, the 1500-byte batch unchanged; profiles/r02u)
+    for (uint32_t tb = 0; tb < nsteps; tb += 8u) {
+        uint4 v[8];
+        load_batch(v, tb);
+        sum_batch(v, tb);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    return acc + T.acc2[lane];
+    // the first chunk's bytes before the frame; the last chunk's bytes past it (owned) or the
+    // frame's tail in the next frame's first chunk (not owned)
+    uint4 H;
+    if constexpr (MODE != 0) H = stage[lane * HW + (lane & (HW - 1u))];
+    else H = T.hbuf[lane];
+    const uint4 L = T.tbuf[lane];
+    uint32_t ca, cbs;
+    masked_ab(H, 16u * fc, 16u * fc, s, ca, cbs);
+    accA -= ca;
+    accB -= cbs;
+    if (tc < oe) {
+        masked_ab(L, 16u * tc, e, 16u * tc + 16u, ca, cbs);
+        accA -= ca;
+        accB -= cbs;
+    } else {
+        masked_ab(L, 16u * tc, 16u * tc, e, ca, cbs);
+        accA += ca;
+        accB += cbs;
+    }
+    if (s & 1u) {                                                 // odd start: the swapped pairing
+        const uint32_t o = (uint32_t)(((uint64_t)(accA - accB) * 0x80808081ull) >> 39);
+        return o + 256u * (accB - o);
+    }
+    return accA;
 }
 
 // MODE: 0 RAW (p.crc_off / p.flags / p.out / p.bad), 1 fused IPv4, 2 fused IPv6,
@@ -391,7 +439,7 @@ __device__ __forceinline__ void window_words(const uint4 (&hw)[HW], uint32_t pos
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
 template <int MODE, bool NT, int CPL, bool SMALL, bool STREAM>
-__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, StreamSmem<STREAM>& SS,
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, StreamSmem<STREAM, MODE == 0>& SS,
                                              uint32_t lane, uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2, ETH = MODE == 3;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
@@ -822,7 +870,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 template <int MODE, bool NT, int CPL, bool SMALL = false, bool STREAM = false>
 __global__ __launch_bounds__(256, CPL >= 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveSmem<MODE != 0> lds_all[4];
-    __shared__ StreamSmem<STREAM> lds_stream[4];
+    __shared__ StreamSmem<STREAM, MODE == 0> lds_stream[4];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
