@@ -73,6 +73,14 @@ struct pico_csum_desc {
 /* flags */
 #define PICO_CSUM_F_WRITE 0x1u  /* store short_be(ret) into the frame's crc field (in place, device memory) */
 #define PICO_CSUM_F_TX    0x2u  /* IPV4 batch: compute (TX) mode -- crc fields read as zero */
+/* IPv6 / Ethernet batches, RX: dispatch the IPv6 TCP / UDP transport check exactly as
+ * pico_transport_crc_check does (pico_socket.c:1919-1923): on `proto` read through a
+ * struct pico_ipv4_hdr cast of the network header -- for IPv6 that is byte 9, the source
+ * address's second byte: 6 -> pico_tcp_checksum (TCP pseudo header), 17 -> the UDP check
+ * when transport bytes 6-7 are non-zero (UDP pseudo header), anything else -> no check.
+ * Without the flag the check follows the transport protocol (next header), the evident
+ * intent.  ICMPv6 is unaffected (pico_icmp6_process_in checks it itself). */
+#define PICO_CSUM_F_REF_DISPATCH 0x4u
 
 /* IPV4 batch verdict byte */
 #define PICO_CSUM_V_ACCEPT    1u  /* frame passes every check the reference makes */

@@ -257,12 +257,19 @@ static int icmp6_checked_type(uint8_t t)
  *   TCP needs 20, UDP 8, ICMPv6 4 transport bytes.  Other protocols: none.
  * MALFORMED: avail < 40, net_len < 40 or past avail, transport past avail, or a
  *   field the reference reads lying past avail.
+ * ORACLE_REF_DISPATCH (RX): TCP / UDP frames are checked as pico_transport_crc_check
+ *   (stack/pico_socket.c:1919-1958) literally does: `switch (net_hdr->proto)` through a
+ *   struct pico_ipv4_hdr cast -- for IPv6 the header's byte 9 (source address byte 1):
+ *   6 -> pico_tcp_checksum -> pico_tcp_checksum_ipv6 (pico_tcp.c:492-505, TCP in the pseudo
+ *   header), 17 -> when t[6..7] != 0, pico_udp_checksum_ipv6 (UDP in the pseudo header),
+ *   else no check.  The transport must hold t[6..7] whenever they are read.
  */
 void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
                        uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
 {
     uint32_t i;
     int tx = (flags & ORACLE_IPV4_TX) != 0;
+    int refd = !tx && (flags & ORACLE_REF_DISPATCH) != 0;
     for (i = 0; i < n; i++) {
         const uint8_t *h = base + d[i].off;
         const uint8_t *t;
@@ -289,7 +296,17 @@ void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint
             continue;
         t = h + net_len;
         s = oracle_ipv6_pseudo_sum(h + 8, h + 24, proto, tl);
-        if (!tx) {
+        if (refd && (proto == 6 || proto == 17)) {
+            uint8_t b9 = h[9];
+            if (proto == 17 || b9 == 17) {
+                if (net_len + 8u > avail) continue;
+            }
+            if (b9 == 6 || (b9 == 17 && (t[6] || t[7]))) {
+                s = oracle_ipv6_pseudo_sum(h + 8, h + 24, b9, tl);
+                l4 = oracle_checksum_finalize(oracle_checksum_adder(s, t, tl));
+                if (l4) v |= PICO_CSUM_V_L4_BAD;
+            }
+        } else if (!tx) {
             if (proto == 6) {
                 l4 = oracle_checksum_finalize(oracle_checksum_adder(s, t, tl));
                 if (l4) v |= PICO_CSUM_V_L4_BAD;

@@ -23,6 +23,7 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_IPV6    128u
 
 #define ORACLE_IPV4_TX 1u
+#define ORACLE_REF_DISPATCH 4u   /* IPv6 RX: pico_transport_crc_check's byte-9 dispatch (PICO_CSUM_F_REF_DISPATCH) */
 
 typedef uint16_t (*oracle_checksum_fn)(void *buf, uint32_t len);
 

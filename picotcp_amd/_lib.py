@@ -46,6 +46,7 @@ EXPORTED = (
 
 F_WRITE = 0x1
 F_TX = 0x2
+F_REF_DISPATCH = 0x4   # IPv6 RX: pico_transport_crc_check's byte-9 dispatch (include/pico_csum.h)
 V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
 V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
 EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12

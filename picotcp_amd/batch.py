@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_IPV6, V_L4_BAD,  # noqa: F401
+from ._lib import (F_REF_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_IPV6, V_L4_BAD,  # noqa: F401
                    V_MALFORMED, V_NET_BAD)
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])

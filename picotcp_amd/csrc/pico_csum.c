@@ -432,15 +432,25 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "NULL buffer");
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
-    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX))
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_REF_DISPATCH))
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
+    if ((flags & PICO_CSUM_F_REF_DISPATCH) && (flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_REF_DISPATCH is an RX option");
     if ((rc = need_device()) != 0)
         return rc;
     s = pick_shape(n, DESC_TYPICAL_LEN, 0);
     if (s.G == 3)
         return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
+    if (s.G != 2 && (flags & PICO_CSUM_F_REF_DISPATCH)) {   /* the sorted-rounds kernel implements it */
+        uint32_t f = n / 2048u;
+        s.G = 2;
+        s.CPL = 8;
+        s.U = 1;
+        s.nt = 1;
+        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
+    }
     if (s.G == 2)
         return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
                                                      NULL, NULL,
@@ -474,10 +484,12 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
         return fail(PICO_CSUM_EINVAL, "NULL buffer");
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
-    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX))
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_REF_DISPATCH))
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
+    if ((flags & PICO_CSUM_F_REF_DISPATCH) && (flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_REF_DISPATCH is an RX option");
     if ((rc = need_device()) != 0)
         return rc;
     if (mac) {

@@ -241,6 +241,7 @@ struct Ipv4Args {
 constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u, V_EXPIRED = 16u;
 constexpr uint32_t V_DROP_L2 = 32u, V_ARP = 64u, V_IPV6 = 128u;   // Ethernet mode (include/pico_csum.h)
 constexpr uint32_t F_MACF = 0x10000u;   // kernel flag (set by the host layer): filter destination MACs
+constexpr uint32_t F_REFD = 0x4u;       // PICO_CSUM_F_REF_DISPATCH (IPv6 RX)
 
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));

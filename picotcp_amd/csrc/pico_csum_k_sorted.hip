@@ -361,7 +361,13 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
         } else if (fam6) {
             if (parsed) {
                 if (l4_needed) {
-                    if (!tx) {
+                    if (!tx && (p.flags & F_REFD) && (proto == 6u || proto == 17u)) {
+                        // pico_socket.c:1919-1958 with net_hdr->proto = byte 9 of the IPv6 header
+                        if (ipcrc == 6u || (ipcrc == 17u && acc_x != 0u)) {
+                            l4 = finalize(pseudo - (proto << 8) + (ipcrc << 8) + acc_all);
+                            if (l4 != 0) verdict |= V_L4_BAD;
+                        }
+                    } else if (!tx) {
                         if (proto == 6u || (proto == 17u && acc_x != 0u) || proto == 58u) {
                             l4 = finalize(pseudo + acc_all);
                             const uint32_t type = acc_x & 0xFFu;   // ICMPv6 type (x field = [0, 2))
@@ -635,9 +641,12 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                     verdict = 0;
                     ext = tl;
                     if (!tx) {
-                        if (proto == 6u) {
+                        // F_REF_DISPATCH: pico_transport_crc_check's proto is byte 9 (kept in ipcrc)
+                        ipcrc = (H[2] >> 8) & 0xFFu;
+                        const bool ref17 = (p.flags & F_REFD) && ipcrc == 17u;
+                        if (proto == 6u && !ref17) {
                             l4_needed = true;
-                        } else if (proto == 17u) {
+                        } else if (proto == 17u || proto == 6u) {   // the UDP crc field is read
                             if (net_len + 8u > avail) { parsed = false; verdict = V_MALFORMED; }
                             else { l4_needed = true; xrel = 6u; ext = max(tl, 8u); }
                         } else if (proto == 58u) {
