@@ -42,6 +42,9 @@ __device__ uint32_t g_stamps_n;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
 constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1
+#ifndef PICO_HW_NT
+#define PICO_HW_NT 0         // non-temporal head-window loads: A/B builds only (5 % slower, profiles/r02nt)
+#endif
 
 struct SortedWaveLds {
     uint32_t acc_all[64];
@@ -533,7 +536,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                 const uint32_t g = FPL * k + gi;
                 const uint32_t gv0 = (uint32_t)__shfl((int)v0, (int)g);
                 const uint32_t gn = (uint32_t)__shfl((int)nin, (int)g);
-                t[k] = load_win<false>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
+                t[k] = load_win<PICO_HW_NT != 0>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
             }
 #pragma unroll
             for (uint32_t k = 0; k < HW; ++k) {
