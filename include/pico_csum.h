@@ -176,6 +176,8 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
  *   when its crc != 0; ICMPv6 (pico_icmp6_checksum pico_icmp6.c:38-55) is always
  *   computed, V_L4_BAD only for the ND / MLD types the reference checks
  *   (pico_ipv6_nd.c:595, pico_mld.c:415).
+ * RX with F_REF_DISPATCH: TCP / UDP checked by header byte 9 as the reference's
+ *   pico_transport_crc_check literally does (see the flag).
  * TX (F_TX): crc field read as zero (pico_tcp.c:980, pico_ipv6.c:1337,1345);
  *   F_WRITE stores it.  d_out_transport: the checksum (0 = valid on RX). */
 int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
@@ -193,7 +195,8 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
  *   (off + 14, len - 14) if the version nibble is 4; 0x86DD -> the IPv6 batch semantics if
  *   it is 6, verdict | V_IPV6; anything else V_DROP_L2.  Frames shorter than 15 bytes are
  *   MALFORMED.  d_out_net is 0 for every non-IPv4 frame.  TX (F_TX, no MAC filter) computes
- *   and, with F_WRITE, stores the IPv4 / IPv6 checksums of the frames the stack built. */
+ *   and, with F_WRITE, stores the IPv4 / IPv6 checksums of the frames the stack built.
+ *   F_REF_DISPATCH (RX) applies to the IPv6 frames as in pico_ipv6_checksum_batch_dev. */
 int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
                                 uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
                                 uint8_t *d_verdict, void *stream);
