@@ -879,10 +879,13 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
+#ifndef PICO_SORTED_WPB
+#define PICO_SORTED_WPB 4    // waves per workgroup (A/B builds: 8)
+#endif
 template <int MODE, bool NT, int CPL, bool SMALL = false, bool STREAM = false>
-__global__ __launch_bounds__(256, CPL >= 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
-    __shared__ SortedWaveSmem<MODE != 0> lds_all[4];
-    __shared__ StreamSmem<STREAM, MODE == 0> lds_stream[4];
+__global__ __launch_bounds__(64 * PICO_SORTED_WPB, CPL >= 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<MODE != 0> lds_all[PICO_SORTED_WPB];
+    __shared__ StreamSmem<STREAM, MODE == 0> lds_stream[PICO_SORTED_WPB];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
@@ -975,7 +978,9 @@ int SORTED_LAUNCH(const void* args, uint32_t nt, int v, void* stream) {
                csum_sorted_kernel<M, t, 8, true, true>}
     static const K table[2][4] = {SK(false), SK(true)};
 #undef SK
-    hipLaunchKernelGGL(table[nt ? 1 : 0][v], grid_for(a.n, a.fpw), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+    const uint64_t waves = ((uint64_t)a.n + a.fpw - 1) / a.fpw;
+    hipLaunchKernelGGL(table[nt ? 1 : 0][v], dim3((unsigned)((waves + PICO_SORTED_WPB - 1) / PICO_SORTED_WPB)),
+                       dim3(64 * PICO_SORTED_WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
 
