@@ -18,7 +18,11 @@ c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame
 are independent shards; no collective touches the data path -- RCCL only carries the
 barrier and the max-over-ranks timing).
 
-Rank 0 prints ONE JSON line.  `roofline` is the checksum kernel's achieved algorithmic HBM
+Rank 0 prints ONE JSON line.  `verified` checks the outputs of the timed region against the CPU
+oracle (every frame of the uniform configs, every datagram of the fused ones); any mismatch
+makes the run exit non-zero.  `value` = the bytes of all ranks / the max over ranks of each
+rank's timed region (from a common start barrier to its own device synchronize; the closing
+barrier is outside it).  `roofline` is the checksum kernel's achieved algorithmic HBM
 bandwidth (HIP events bracketing the K timed launches on the launch stream; elapsed / K =
 average launch duration) against the 8.0 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per launch
 from profiles/pmc_traffic.json (FETCH_SIZE x2, calibrated to 128 B per touched line by tools/fetch_calib.py,
@@ -92,6 +96,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=4.0, help="target CPU-baseline wall per leg")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--no-verify", action="store_true", help="skip the parity check of the timed outputs")
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch the K timed steps one by one from Python instead of replaying them as one "
@@ -309,6 +314,72 @@ def cpu_baseline_frag(st, target_s: float):
     return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload), oracle reassembly restatement "
                       f"(sort, memcpy gather, pico_checksum of the transport), gcc -O3, 1 thread, {reps} passes"}
+
+
+def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
+    """Parity evidence carried by the bench line itself: the outputs the timed region produced
+    for rotation slot 0 against the CPU oracle (oracle/pico_csum_oracle.c, the checker; never
+    the measured path).  uniform: every frame of the batch (the restatement on `threads`
+    pthreads); fused IPv4 / IPv6 / Ethernet: every datagram, on the device buffer as the timed
+    steps left it (TX: the values and the crc fields written in place); reassembly: the first
+    256 datagrams (lengths, checksums, verdicts and the reassembled bytes)."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    if kind == "uniform":
+        b, ln, n = slot
+        hb = b.cpu().numpy()
+        _, want = O.uniform_mt(hb, ln, ln, n, threads, kind="port")
+        got = out.cpu().numpy().view(np.uint16)
+        frames, bad = n, int((got != want).sum())
+        what = f"every frame, oracle_checksum on {threads} threads"
+    elif kind == "frag":
+        b, d, gr, o, od, nfr, payload = slot
+        n = gr.numel() // 2
+        k = min(n, 256)
+        grp = gr.cpu().numpy().view(np.uint32)[:2 * k]
+        nf_used = int(grp[-2] + grp[-1])
+        desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
+        hi = int(desc["off"][-1]) + int(desc["len"][-1])
+        odh = od.cpu().numpy().view(batch.DESC_DTYPE)[:k]
+        outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
+        wl, wl4, wv = O.ipv4_reassemble(b[:hi].cpu().numpy(), desc, grp, outh, odh)
+        gl, gl4, gv = (x.cpu().numpy()[:k] for x in out)
+        gout = o[:outh.size].cpu().numpy()
+        bad = int(((gl.view(np.uint32) != wl) | (gl4.view(np.uint16) != wl4) | (gv != wv)).sum())
+        for g in range(k):
+            if wl[g]:
+                a = int(odh["off"][g])
+                bad += int(not np.array_equal(gout[a:a + 20 + int(wl[g])], outh[a:a + 20 + int(wl[g])]))
+        frames = k
+        what = "first 256 datagrams: lengths, checksums, verdicts and reassembled bytes vs oracle_ipv4_reassemble"
+    else:
+        b, d = slot[0], slot[1]
+        hbuf, hdesc = host
+        tx = bool(cfg.get("tx"))
+        now = b.cpu().numpy()
+        src = hbuf if tx else now                   # TX: the pre-write bytes are the input
+        if kind == "ipv4":
+            want = O.batch_ipv4(src, hdesc, tx=tx)
+        elif kind == "eth":
+            want = O.batch_eth(src, hdesc, mac=MAC, tx=tx)
+        else:
+            want = O.batch_ipv6(src, hdesc, tx=tx)
+        got = [x.cpu().numpy() for x in out]
+        if kind == "ipv6":
+            got = [got[0].view(np.uint16), got[1]]
+        else:
+            got = [got[0].view(np.uint16), got[1].view(np.uint16), got[2]]
+        miss = np.zeros(hdesc.size, bool)
+        for g_, w_ in zip(got, want):
+            miss |= g_ != w_
+        frames, bad = int(hdesc.size), int(miss.sum())
+        if tx:                                      # the in-place writes: oracle RX on them accepts
+            rx = O.batch_ipv4(now, hdesc) if kind == "ipv4" else None
+            if rx is not None:
+                bad += int(((want[2] == 1) & (rx[2] != 1)).sum())
+        what = f"every datagram vs the oracle's fused {kind} {'TX' if tx else 'RX'} restatement" + \
+            (" (+ RX of the written bytes)" if tx and kind == "ipv4" else "")
+    return {"frames": frames, "mismatches": bad, "checker": what, "seconds": round(time.perf_counter() - t0, 2)}
 
 
 def copy_ceiling(nbytes: int, dev) -> dict:
@@ -561,12 +632,12 @@ def main():
             step(i)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0                  # this rank's region: its closing barrier is not in it
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
     if world > 1:
         dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / a.steps
 
-    # ... and whole-job time = max over ranks
+    # ... and whole-job time = max over ranks (each rank's wall from the common start barrier)
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -582,6 +653,23 @@ def main():
 
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
     traffic, traffic_src = load_traffic(a.config)
+
+    # ---- parity of what the timed region produced (every rank checks its own slot 0)
+    ver = None
+    if not a.no_verify:
+        threads = cpu_threads()[0]
+        if cfg["kind"] == "uniform":
+            ver = verify("uniform", cfg, (bufs[0], ln, n), outs[0], None, threads)
+        elif cfg["kind"] == "frag":
+            ver = verify("frag", cfg, sets[0], res[0], None, threads)
+        else:
+            ver = verify(cfg["kind"], cfg, sets[0], outs[0], sets[0][3], threads)
+        vt = torch.tensor([ver["frames"], ver["mismatches"]], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(vt)
+        ver["frames"], ver["mismatches"] = int(vt[0]), int(vt[1])
+        if world > 1:
+            ver["ranks"] = world
     out = None
     if rank == 0:
         out = {
@@ -599,6 +687,8 @@ def main():
                          "kernel_avg_us": round(kern_ms * 1e3, 2), "kernel_avg_us_max_rank": round(kern_max_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": algo_bytes},
         }
+        if ver is not None:
+            out["verified"] = ver
     if rank == 0 and world == 1 and cfg["kind"] == "uniform":
         if not a.no_cpu:
             sample_frames = min(n, 262144)
@@ -621,6 +711,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if ver is not None and ver["mismatches"]:
+        sys.exit(f"bench.py: {ver['mismatches']} of {ver['frames']} outputs differ from the oracle")
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PICO_CSUM_ABI_VERSION 1
+#define PICO_CSUM_ABI_VERSION 2   /* 2: V_FRAG, the reference's IPv6 dispatch by default */
 
 /* picoTCP pico_err values used here (include/pico_protocol.h:27,31,38 + ENODEV) */
 #define PICO_CSUM_EIO     5
@@ -72,22 +72,36 @@ struct pico_csum_desc {
 
 /* flags */
 #define PICO_CSUM_F_WRITE 0x1u  /* store short_be(ret) into the frame's crc field (in place, device memory) */
-#define PICO_CSUM_F_TX    0x2u  /* IPV4 batch: compute (TX) mode -- crc fields read as zero */
-/* IPv6 / Ethernet batches, RX: dispatch the IPv6 TCP / UDP transport check exactly as
- * pico_transport_crc_check does (pico_socket.c:1919-1923): on `proto` read through a
- * struct pico_ipv4_hdr cast of the network header -- for IPv6 that is byte 9, the source
- * address's second byte: 6 -> pico_tcp_checksum (TCP pseudo header), 17 -> the UDP check
- * when transport bytes 6-7 are non-zero (UDP pseudo header), anything else -> no check.
- * Without the flag the check follows the transport protocol (next header), the evident
- * intent.  ICMPv6 is unaffected (pico_icmp6_process_in checks it itself). */
-#define PICO_CSUM_F_REF_DISPATCH 0x4u
+#define PICO_CSUM_F_TX    0x2u  /* fused batches: compute (TX) mode -- crc fields read as zero */
+/* IPv6 / Ethernet batches, RX.  By default the IPv6 TCP / UDP transport check is dispatched
+ * exactly as the reference's pico_transport_crc_check does it (stack/pico_socket.c:1919-1923):
+ * on `proto` read through a struct pico_ipv4_hdr cast of the network header -- for IPv6 that is
+ * byte 9, the source address's second byte: 6 -> pico_tcp_checksum (TCP pseudo header), 17 ->
+ * the UDP check when transport bytes 6-7 are non-zero (UDP pseudo header), anything else -> no
+ * check.  With this flag the check follows the transport's own protocol instead (TCP always,
+ * UDP when its crc != 0: the evident intent, not the reference's behaviour).  ICMPv6 is the
+ * same either way (pico_icmp6_process_in checks it itself). */
+#define PICO_CSUM_F_NXTHDR_DISPATCH 0x4u
 
-/* IPV4 batch verdict byte */
-#define PICO_CSUM_V_ACCEPT    1u  /* frame passes every check the reference makes */
-#define PICO_CSUM_V_NET_BAD   2u  /* pico_ipv4_crc_check would discard (pico_ipv4.c:249-253) */
-#define PICO_CSUM_V_L4_BAD    4u  /* pico_transport_crc_check would discard (pico_socket.c:1929,1953) */
-#define PICO_CSUM_V_MALFORMED 8u  /* infeasible length (pico_ipv4.c:402-405) or a region past the buffer */
-#define PICO_CSUM_V_EXPIRED  16u  /* forwarding: TTL reached 0 (pico_ipv4.c:1549-1552) */
+/* Verdict byte of the fused batches: the reference's FIRST outcome for the frame, in its own
+ * order (one value, plus V_IPV6 on the Ethernet batch's IPv6 frames). */
+#define PICO_CSUM_V_ACCEPT    1u  /* delivered to the transport and every checksum the reference
+                                     checks passes: hand the frame on (a stack built with CRC=0
+                                     need not check it again) */
+#define PICO_CSUM_V_NET_BAD   2u  /* pico_ipv4_crc_check discards it (pico_ipv4.c:420-422, :243-257) */
+#define PICO_CSUM_V_L4_BAD    4u  /* pico_transport_crc_check discards it (pico_socket.c:1929,1953) */
+#define PICO_CSUM_V_MALFORMED 8u  /* discarded before any transport: infeasible length
+                                     (pico_ipv4.c:405-408); after a good header checksum an invalid
+                                     source (:425-428), the evil bit (:431-435), IHL < 5 (:438-443);
+                                     an IPv6 extension-header chain pico_ipv6_extension_headers
+                                     discards (pico_ipv6.c:659-809); a header or field that lies
+                                     past the buffer (where the reference would read past it) */
+#define PICO_CSUM_V_FRAG     16u  /* a fragment: IPv4 MF or offset (pico_ipv4.c:446-455), IPv6 a
+                                     fragment header (pico_ipv6.c:791-795) -- header verified, NO
+                                     transport check (the reference checks the reassembled
+                                     datagram): route it to the reassembly batch.  TX: the
+                                     header checksum only (the transport's covers the datagram). */
+#define PICO_CSUM_V_EXPIRED  16u  /* forwarding batch only (same bit): TTL reached 0 (pico_ipv4.c:1549-1552) */
 #define PICO_CSUM_V_DROP_L2  32u  /* Ethernet batch: discarded by the link layer -- foreign destination MAC
                                      (pico_ethernet.c:221-231), unknown ethertype (:201-202) or an IP
                                      version that does not match it (:143-150, :162-176) */
@@ -148,10 +162,11 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
 
 /* Fused IPv4 header + transport batch, one IPv4 datagram per descriptor
  * (desc.off -> IPv4 header, desc.len = bytes available).
- * RX (flags without F_TX): the checks of pico_ipv4_process_in
- *   (pico_ipv4.c:381-420) + pico_ipv4_crc_check (:243-257) +
- *   pico_transport_crc_check (pico_socket.c:1916-1968): TCP always, UDP when
- *   its crc field != 0, pseudo header from the IP header.
+ * RX (flags without F_TX): pico_ipv4_process_in (pico_ipv4.c:381-456) up to its hand-off --
+ *   lengths, pico_ipv4_crc_check (:243-257), the source check, the evil bit, IHL < 5, the
+ *   fragment hand-off -- then pico_transport_crc_check (pico_socket.c:1916-1968): TCP always,
+ *   UDP when its crc field != 0, pseudo header from the IP header.  The link-directed
+ *   broadcast sources of pico_ipv4_is_broadcast (the stack's link table) are left to the stack.
  *   d_out_net = pico_checksum(hdr, net_len), d_out_transport = the TCP/UDP
  *   checksum (0 = valid; 0 when none is computed), d_verdict = PICO_CSUM_V_*.
  * TX (F_TX): crc fields read as zero; d_out_* are the values to store
@@ -164,20 +179,20 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint16_t *d_out_transport, uint8_t *d_verdict, void *stream);
 
 /* Fused IPv6 transport batch (TCP / UDP / ICMPv6 over IPv6),
- * one datagram per descriptor: desc.off -> IPv6 header, desc.len = bytes
- * available, desc.seed = f->net_len | (transport proto << 16) as
- * pico_ipv6_extension_headers (pico_ipv6.c:707-800) leaves them -- the
- * extension-header chain is control logic and stays in the stack; seed 0 = no
- * extension headers (net_len 40, proto = hdr->nxthdr).  transport_len =
- * (uint16)(payload_len - (net_len - 40)) (pico_ipv6.c:790); pseudo header =
- * struct pico_ipv6_pseudo_hdr (pico_ipv6.h:46-53) from the IPv6 header.
+ * one datagram per descriptor: desc.off -> IPv6 header, desc.len = bytes available,
+ * desc.seed = 0, or f->net_len | (transport proto << 16) when the stack already walked the
+ * extension headers.  RX with seed 0: the kernel walks them itself, as
+ * pico_ipv6_extension_headers does (pico_ipv6.c:659-809: the sequence check, hop-by-hop /
+ * routing / fragment / destination-option processing): a chain the reference discards is
+ * V_MALFORMED, a transport behind a fragment header V_FRAG.  TX with seed 0: net_len 40,
+ * proto = hdr->nxthdr.  transport_len = (uint16)(payload_len - (net_len - 40))
+ * (pico_ipv6.c:790); pseudo header = struct pico_ipv6_pseudo_hdr (pico_ipv6.h:46-53) from
+ * the IPv6 header.
  * RX: pico_transport_crc_check (pico_socket.c:1916-1968; pico_tcp_checksum_ipv6
- *   pico_tcp.c:449-475, pico_udp_checksum_ipv6 pico_udp.c:63-92): TCP always, UDP
- *   when its crc != 0; ICMPv6 (pico_icmp6_checksum pico_icmp6.c:38-55) is always
- *   computed, V_L4_BAD only for the ND / MLD types the reference checks
- *   (pico_ipv6_nd.c:595, pico_mld.c:415).
- * RX with F_REF_DISPATCH: TCP / UDP checked by header byte 9 as the reference's
- *   pico_transport_crc_check literally does (see the flag).
+ *   pico_tcp.c:449-475, pico_udp_checksum_ipv6 pico_udp.c:63-92) dispatched on header byte 9
+ *   as the reference does (see PICO_CSUM_F_NXTHDR_DISPATCH for the alternative); ICMPv6
+ *   (pico_icmp6_checksum pico_icmp6.c:38-55) is always computed, V_L4_BAD only for the ND /
+ *   MLD types the reference checks (pico_ipv6_nd.c:595, pico_mld.c:415).
  * TX (F_TX): crc field read as zero (pico_tcp.c:980, pico_ipv6.c:1337,1345);
  *   F_WRITE stores it.  d_out_transport: the checksum (0 = valid on RX). */
 int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
@@ -196,7 +211,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
  *   it is 6, verdict | V_IPV6; anything else V_DROP_L2.  Frames shorter than 15 bytes are
  *   MALFORMED.  d_out_net is 0 for every non-IPv4 frame.  TX (F_TX, no MAC filter) computes
  *   and, with F_WRITE, stores the IPv4 / IPv6 checksums of the frames the stack built.
- *   F_REF_DISPATCH (RX) applies to the IPv6 frames as in pico_ipv6_checksum_batch_dev. */
+ *   F_NXTHDR_DISPATCH (RX) applies to the IPv6 frames as in pico_ipv6_checksum_batch_dev. */
 int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
                                 uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
                                 uint8_t *d_verdict, void *stream);
@@ -285,17 +300,16 @@ int pico_csum_host_unregister(void *ptr);
 int pico_csum_abi_version(void);
 const char *pico_csum_last_error(void);   /* thread-local, "" when none */
 
-/* Launch-shape override for tests and bench sweeps (all 0 = automatic choice).
- * group = lanes per frame (4..64, power of 2); cpl = 16-byte chunks per lane
- * per pass (1,2,4,8); unroll = frames in flight per group (1,2,4; RAW batches
- * only, cpl*unroll <= 8); fpw = frames per wave (multiple of 64/group, <= 64);
- * nt = 0 auto / 1 plain / 2 non-temporal loads (RAW batches); pipeline = 0 auto /
- * 1 off / 2 on / 3 on with global instead of buffer-window loads (uniform batches
- * whose frames fit one pass: double-buffered frame sets).  group = 1 selects the
- * flat work-list kernel, group = 2 the sorted-rounds kernel (descriptor batches
- * only; there unroll = the narrowest round width: 0 auto, 1 = one frame per lane
- * for frames of <= 8 chunks (cpl 8), 4), group = 3 the per-wave adaptive kernel.
- * Applies to launches from the calling thread only (thread-local). */
+/* Launch-shape override for tests and bench sweeps (all 0 = automatic choice); applies to
+ * launches from the calling thread only (thread-local).
+ *   group 2: descriptor batches (the sorted-rounds kernel) with fpw frames per wave (1..64);
+ *            the other arguments are ignored.
+ *   group 4..64 (power of 2): uniform rings -- lanes per frame; cpl = 16-byte chunks per lane
+ *            per pass (1,2,4,8); unroll = frames in flight per group (1,2,4; cpl*unroll <= 8);
+ *            fpw = frames per wave (multiple of 64/group, <= 64); nt = 0 auto / 1 plain /
+ *            2 non-temporal loads; pipeline = 0 auto / 1 off / 2 on / 3 on with global instead
+ *            of buffer-window loads (frames that fit one pass: double-buffered frame sets).
+ * A group for the other batch kind makes the batch call return -EINVAL. */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);
 

@@ -23,7 +23,7 @@ REF_OS_SO = os.path.join(HERE, "_ref", "libpicoref_Os.so")
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
 ORACLE_IPV4_TX = 1
-ORACLE_REF_DISPATCH = 4   # IPv6 RX: pico_transport_crc_check's byte-9 dispatch
+ORACLE_NXTHDR_DISPATCH = 4   # IPv6 RX: TCP / UDP by next header (default: the reference's byte-9 dispatch)
 
 _vp = ctypes.c_void_p
 _u16, _u32, _u64, _i32 = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
@@ -65,6 +65,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_ipv6_pseudo_sum.argtypes = [_vp, _vp, ctypes.c_uint8, _u32]
         L.oracle_batch_ipv6.restype = None
         L.oracle_batch_ipv6.argtypes = [_vp, _vp, _u32, _vp, _vp, _u32]
+        L.oracle_ipv6_walk.restype = ctypes.c_int
+        L.oracle_ipv6_walk.argtypes = [_vp, _u32, _vp, _vp]
         L.oracle_batch_eth.restype = None
         L.oracle_batch_eth.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]
         L.oracle_ipv4_reassemble.restype = None
@@ -132,24 +134,35 @@ def batch_ipv4(base: np.ndarray, desc: np.ndarray, tx: bool = False):
     return on, ol, v
 
 
-def batch_ipv6(base: np.ndarray, desc: np.ndarray, tx: bool = False, ref_dispatch: bool = False):
+def batch_ipv6(base: np.ndarray, desc: np.ndarray, tx: bool = False, nxthdr_dispatch: bool = False):
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
     n = desc.shape[0]
     ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint8)
     lib().oracle_batch_ipv6(_p(base), _p(desc), n, _p(ol), _p(v),
-                            (ORACLE_IPV4_TX if tx else 0) | (ORACLE_REF_DISPATCH if ref_dispatch else 0))
+                            (ORACLE_IPV4_TX if tx else 0) | (ORACLE_NXTHDR_DISPATCH if nxthdr_dispatch else 0))
     return ol, v
 
 
+WALK_DROP, WALK_PROTO, WALK_FRAG, WALK_BAD = 0, 1, 2, -1
+
+
+def ipv6_walk(dgram) -> tuple:
+    """oracle_ipv6_walk on one IPv6 datagram: (kind, net_len, proto)."""
+    a = _buf(dgram)
+    nl, pr = ctypes.c_uint32(0), ctypes.c_uint8(0)
+    k = lib().oracle_ipv6_walk(_p(a), a.size, ctypes.byref(nl), ctypes.byref(pr))
+    return k, nl.value, pr.value
+
+
 def batch_eth(base: np.ndarray, desc: np.ndarray, mac: bytes | None = None, tx: bool = False,
-              ref_dispatch: bool = False):
+              nxthdr_dispatch: bool = False):
     """Ethernet dispatch + fused IPv4 / IPv6 (oracle_batch_eth); mac None = no destination filter."""
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
     n = desc.shape[0]
     on, ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8)
     m = None if mac is None else _buf(mac)
     lib().oracle_batch_eth(_p(base), _p(desc), n, None if m is None else _p(m), _p(on), _p(ol), _p(v),
-                           (ORACLE_IPV4_TX if tx else 0) | (ORACLE_REF_DISPATCH if ref_dispatch else 0))
+                           (ORACLE_IPV4_TX if tx else 0) | (ORACLE_NXTHDR_DISPATCH if nxthdr_dispatch else 0))
     return on, ol, v
 
 

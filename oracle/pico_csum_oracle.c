@@ -122,24 +122,39 @@ void oracle_batch_uniform(const uint8_t *base, uint64_t stride, uint32_t len, ui
  * the IPv4 header (f->net_hdr); desc.len = bytes available from net_hdr to the
  * end of the frame buffer (f->buffer_len - (f->net_hdr - f->buffer)).
  *
- * RX (flags & ORACLE_IPV4_TX == 0):
- *   lengths + feasibility bound   pico_ipv4_process_in  modules/pico_ipv4.c:381-405
- *   header check                  pico_ipv4_crc_check   modules/pico_ipv4.c:243-257
- *   transport check               pico_transport_crc_check stack/pico_socket.c:1916-1968
- *     TCP: pico_tcp_checksum_ipv4 modules/pico_tcp.c:422-446 (pseudo from IP hdr, f->sock NULL)
- *     UDP: only when the stored crc != 0 (pico_socket.c:1941), pico_udp.c:36-60
- *   out_net = pico_checksum(hdr, net_len)                        (0 when valid)
- *   out_l4  = transport checksum with the IPv4 pseudo header       (0 when valid;
- *             0 when the reference computes none)
- *   verdict = PICO_CSUM_V_ACCEPT, or the OR of the failure bits.
- *   Frames where the reference would read past desc.len (header or
- *   transport beyond the buffer: reference UB) are PICO_CSUM_V_MALFORMED.
+ * RX (flags & ORACLE_IPV4_TX == 0): pico_ipv4_process_in (modules/pico_ipv4.c:381-456) up to
+ * the hand-off, then pico_transport_crc_check (stack/pico_socket.c:1916-1968).  The verdict is
+ * the reference's FIRST discard reason, in its order:
+ *   1. lengths: net_len = 20 + 4 (IHL - 5) (options only when IHL > 5, :394-396),
+ *      transport_len = (uint16)(tot - net_len) (:399); transport_len > max_allowed =
+ *      (uint16)(avail - 20) is discarded (:386, :405-408)                       -> MALFORMED
+ *      (also MALFORMED: the header or the transport past desc.len, where the reference would
+ *      read past its buffer)
+ *   2. pico_ipv4_crc_check over net_len bytes (:420-422, :243-257)               -> NET_BAD
+ *   3. pico_ipv4_is_valid_src (:425-428, :210-229): 255.255.255.255, a multicast source
+ *      (first byte 0xE0-0xFE, :187-194), a loopback source (127/8) from a non-"loop" device
+ *                                                                                 -> MALFORMED
+ *      (the link-directed broadcasts of pico_ipv4_is_broadcast, :1620-1633, are the stack's
+ *      link table: not decidable from the frame, left to the stack)
+ *   4. the evil bit (frag & 0x8000, RFC 3514, :431-435)                           -> MALFORMED
+ *   5. IHL < 5 (:438-443)                                                         -> MALFORMED
+ *   6. MF or a fragment offset (frag & 0x3FFF, :446-455): handed to pico_ipv4_process_frag,
+ *      no transport check on the fragment                                         -> FRAG
+ *   7. transport check: TCP always (pico_tcp_checksum_ipv4, modules/pico_tcp.c:422-446, pseudo
+ *      header from the IP header, f->sock NULL); UDP only when its stored crc != 0
+ *      (pico_socket.c:1941, pico_udp.c:36-60; a UDP transport shorter than 8 bytes would be
+ *      read past: MALFORMED)                                                      -> L4_BAD
+ *   otherwise ACCEPT.
+ *   out_net = pico_checksum(hdr, net_len) (0 when valid) whenever the lengths pass;
+ *   out_l4  = the transport checksum (0 when valid; 0 when the reference computes none).
  * TX (ORACLE_IPV4_TX): the header is complete; crc fields read as zero
  *   (hdr->crc = 0 at pico_ipv4.c:237, pico_tcp.c:980, pico_icmp4.c:38); out_*
  *   are the values the reference stores with short_be() (pico_ipv4.c:238,
  *   pico_tcp.c:981, pico_icmp4.c:39).  UDP over IPv4 sends crc 0
  *   (pico_udp.c:123); other protocols get none.  TCP needs a 20-byte and ICMP
- *   an 8-byte header inside transport_len, else MALFORMED.
+ *   an 8-byte header inside transport_len, else MALFORMED.  A fragment (MF or an offset) gets
+ *   its own header checksum only (pico_ipv4_frame_push :1079 per fragment; the transport
+ *   checksum covers the whole datagram and was set before fragmentation, :1470-1500) -> FRAG.
  */
 void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
                        uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
@@ -151,7 +166,7 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
         const uint8_t *t;
         uint32_t avail = d[i].len;
         uint32_t option_len = 0, net_len, s;
-        uint16_t tot, transport_len, max_allowed;
+        uint16_t tot, transport_len, max_allowed, frag;
         uint16_t net_cs, l4_cs = 0;
         uint8_t proto, v = 0;
 
@@ -163,11 +178,12 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
         net_len = 20u + option_len;
         proto = h[9];
         tot = (uint16_t)((h[2] << 8) | h[3]);
-        transport_len = (uint16_t)(tot - 20u - option_len);    /* uint16 wrap as :395 */
+        frag = (uint16_t)((h[6] << 8) | h[7]);                 /* f->frag = short_be(hdr->frag), :402 */
+        transport_len = (uint16_t)(tot - 20u - option_len);    /* uint16 wrap as :399 */
         max_allowed = (uint16_t)(avail - 20u);                 /* :386 */
         if (net_len > avail)
             continue;
-        if (!tx && transport_len > max_allowed)                /* :402-405 discard */
+        if (!tx && transport_len > max_allowed)                /* :405-408 discard */
             continue;
         if (net_len + (uint32_t)transport_len > avail)         /* reference would overread */
             continue;
@@ -176,26 +192,38 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
         s = oracle_checksum_adder(0, h, net_len);
         if (tx) s -= (uint32_t)(h[10] | (h[11] << 8));
         net_cs = oracle_checksum_finalize(s);
-        if (!tx && net_cs != 0)
-            v |= PICO_CSUM_V_NET_BAD;
+        out_net[i] = net_cs;
 
         if (!tx) {
-            if (proto == 6 || proto == 17) {
+            if (net_cs != 0)
+                v = PICO_CSUM_V_NET_BAD;                                        /* :420-422 */
+            else if ((h[12] == 0xFF && h[13] == 0xFF && h[14] == 0xFF && h[15] == 0xFF) ||
+                     (h[12] != 0xFF && (h[12] & 0xE0) == 0xE0) || h[12] == 0x7F)
+                v = PICO_CSUM_V_MALFORMED;                                      /* :425-428 */
+            else if (frag & 0x8000u)
+                v = PICO_CSUM_V_MALFORMED;                                      /* :431-435 */
+            else if ((h[0] & 0x0F) < 5)
+                v = PICO_CSUM_V_MALFORMED;                                      /* :438-443 */
+            else if (frag & 0x3FFFu)
+                v = PICO_CSUM_V_FRAG;                                           /* :446-455 */
+            else if (proto == 6 || proto == 17) {
                 int check = 1;
                 if (proto == 17) {
-                    if (net_len + 8u > avail) { v |= PICO_CSUM_V_MALFORMED; check = 0; }
+                    if (net_len + 8u > avail) { v = PICO_CSUM_V_MALFORMED; check = 0; }
                     else if (t[6] == 0 && t[7] == 0) check = 0;
                 }
                 if (check) {
                     s = oracle_ipv4_pseudo_sum(h + 12, h + 16, proto, transport_len);
                     l4_cs = oracle_checksum_finalize(oracle_checksum_adder(s, t, transport_len));
                     if (l4_cs != 0)
-                        v |= PICO_CSUM_V_L4_BAD;
+                        v = PICO_CSUM_V_L4_BAD;
                 }
             }
+        } else if (frag & 0x3FFFu) {
+            v = PICO_CSUM_V_FRAG;
         } else {
             if (proto == 6) {
-                if (transport_len < 20) { v |= PICO_CSUM_V_MALFORMED; }
+                if (transport_len < 20) { v = PICO_CSUM_V_MALFORMED; }
                 else {
                     s = oracle_ipv4_pseudo_sum(h + 12, h + 16, proto, transport_len);
                     s = oracle_checksum_adder(s, t, transport_len);
@@ -203,7 +231,7 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
                     l4_cs = oracle_checksum_finalize(s);
                 }
             } else if (proto == 1) {
-                if (transport_len < 8) { v |= PICO_CSUM_V_MALFORMED; }
+                if (transport_len < 8) { v = PICO_CSUM_V_MALFORMED; }
                 else {
                     s = oracle_checksum_adder(0, t, transport_len);
                     s -= (uint32_t)(t[2] | (t[3] << 8));
@@ -211,7 +239,6 @@ void oracle_batch_ipv4(const uint8_t *base, const struct pico_csum_desc *d, uint
                 }
             }
         }
-        out_net[i] = net_cs;
         out_l4[i] = l4_cs;
         verdict[i] = (uint8_t)(v == 0 ? PICO_CSUM_V_ACCEPT : v);
     }
@@ -241,35 +268,225 @@ static int icmp6_checked_type(uint8_t t)
     return (t >= 133 && t <= 137) || (t >= 130 && t <= 132) || t == 143;
 }
 
+/* The walk reads byte k of the datagram only when k < avail; a read past it is where the
+ * reference would read past its buffer (reported as ORACLE_WALK_BAD). */
+#define WALK_BYTE(k, dst)                          \
+    do {                                           \
+        if ((uint32_t)(k) >= avail)                \
+            return ORACLE_WALK_BAD;                \
+        (dst) = h[(uint32_t)(k)];                  \
+    } while (0)
+
+/* pico_ipv6_process_hopbyhop (modules/pico_ipv6.c:525-582) on the header at byte e:
+ * 1 / 0 = must_align, -1 = discard, ORACLE_WALK_BAD (-1 is taken) -> -2.  option = e + 2,
+ * len = (uint8)HBH_LEN (pico_ipv6.h:30); Pad1 advances 1 byte, PadN / router alert / an
+ * unknown option with action "skip" advance (uint8)(opt[1] + 2) -- 0 when opt[1] = 254, and
+ * the reference's loop then never ends; a router alert with data length 2 (MLD) clears
+ * must_align; any other action (0x40 / 0x80 / 0xC0) discards. */
+static int walk_hopbyhop(const uint8_t *h, uint32_t avail, uint32_t e)
+{
+    uint8_t b1, len, type, olen, optlen;
+    uint32_t opt = e + 2;
+    int must_align = 1;
+    if (e + 1 >= avail) return -2;
+    b1 = h[e + 1];
+    len = (uint8_t)(((b1 + 1) << 3) - 2);
+    while (len) {
+        if (opt >= avail) return -2;
+        type = h[opt];
+        if (type == 0) {                        /* PICO_IPV6_EXTHDR_OPT_PAD1 */
+            opt++;
+            len--;
+            continue;
+        }
+        if (opt + 1 >= avail) return -2;
+        olen = h[opt + 1];
+        optlen = (uint8_t)(olen + 2);
+        if (type == 5) {                        /* PICO_IPV6_EXTHDR_OPT_ROUTER_ALERT */
+            if (olen == 2) must_align = 0;
+        } else if (type != 1 && (type & 0xC0) != 0) {
+            return -1;                          /* discard (+ a parameter problem for 0x80 / 0xC0) */
+        }
+        if (optlen == 0) return -2;             /* the reference loops forever */
+        opt += optlen;
+        len = (uint8_t)(len - optlen);
+    }
+    return must_align;
+}
+
+/* pico_ipv6_process_destopt (modules/pico_ipv6.c:610-657): 0 = pass, -1 = discard, -2 = past
+ * the frame / endless.  Every option -- Pad1 included -- advances (uint8)(opt[1] + 2). */
+static int walk_destopt(const uint8_t *h, uint32_t avail, uint32_t e)
+{
+    uint8_t b1, len, type, optlen;
+    uint32_t opt = e + 2;
+    if (e + 1 >= avail) return -2;
+    b1 = h[e + 1];
+    len = (uint8_t)(((b1 + 1) << 3) - 2);
+    while (len) {
+        if (opt + 1 >= avail) return -2;
+        type = h[opt];
+        optlen = (uint8_t)(h[opt + 1] + 2);
+        if (type != 0 && type != 1 && type != 201 && (type & 0xC0) != 0)
+            return -1;
+        if (optlen == 0) return -2;
+        opt += optlen;
+        len = (uint8_t)(len - optlen);
+    }
+    return 0;
+}
+
+/*
+ * pico_ipv6_extension_headers (modules/pico_ipv6.c:707-809) with the sequence check before it
+ * (pico_ipv6_check_headers_sequence, :659-694), on the IPv6 datagram at h (avail bytes).
+ *   sequence check: from the fixed header's next header, walk DESTOPT / ROUTING / HOPBYHOP /
+ *     ESP / AUTH by (uint8)IPV6_OPTLEN(len) -- wraps to 0 for len >= 31 --, FRAG by 8, stop at
+ *     NONE / TCP / UDP / ICMPv6; any other value discards (parameter problem, :685-688)
+ *   walk: f->net_len (uint16) from 40; HOPBYHOP only right behind the fixed header (:727-734);
+ *     ROUTING with segments left and a type other than 2 discards (:585-606); FRAG sets
+ *     f->frag (and with M set a payload length not a multiple of 8 discards, :750-761);
+ *     DESTOPT sets must_align; ESP / AUTH / NONE end the walk with no transport (discarded by
+ *     pico_ipv6_process_in, :855-859); at TCP / UDP / ICMPv6, must_align with a payload length
+ *     not a multiple of 8 discards (:696-705, :783-788), else the transport is reached: behind
+ *     a fragment header the datagram goes to pico_ipv6_process_frag (:791-795), otherwise it
+ *     is delivered with that protocol and net_len.
+ * Endless loops of the reference (a zero-length step that keeps revisiting one header), a
+ * chain whose f->net_len passes 0xFFFF (the uint16 wraps and the walk starts over near the
+ * fixed header) and reads past avail return ORACLE_WALK_BAD.
+ */
+int oracle_ipv6_walk(const uint8_t *h, uint32_t avail, uint32_t *net_len_out, uint8_t *proto_out)
+{
+    uint32_t plen, ptr, iter, cur_nexthdr;
+    uint16_t net_len;
+    uint8_t nx, b;
+    int must_align = 0, frag = 0;
+
+    if (avail < 40) return ORACLE_WALK_BAD;
+    plen = (uint32_t)((h[4] << 8) | h[5]);
+    /* sequence check: each step moves >= 8 bytes, or 0 (a wrapped length) and then the next
+     * step reads the same header again: at most 2 steps per 8 bytes before a read passes avail */
+    ptr = 40;
+    nx = h[6];
+    for (iter = 0;; iter++) {
+        uint8_t optlen;
+        if (iter > 2u * (avail / 8u) + 8u) return ORACLE_WALK_BAD;
+        if (nx == 0 || nx == 43 || nx == 60 || nx == 50 || nx == 51) {
+            WALK_BYTE(ptr + 1, b);
+            optlen = (uint8_t)((b + 1) << 3);
+        } else if (nx == 44) {
+            optlen = 8;
+        } else if (nx == 59 || nx == 6 || nx == 17 || nx == 58) {
+            break;
+        } else {
+            return ORACLE_WALK_DROP;
+        }
+        WALK_BYTE(ptr, nx);
+        ptr += optlen;
+    }
+    /* the walk: each step moves f->net_len by >= 8 (uint16 arithmetic) */
+    net_len = 40;
+    ptr = 40;
+    cur_nexthdr = 6;
+    nx = h[6];
+    for (iter = 0;; iter++) {
+        uint32_t e = net_len;
+        uint16_t cur_optlen = 0;
+        int r;
+        if (iter > avail / 8u + 8u) return ORACLE_WALK_BAD;   /* never: each step moves >= 8 bytes */
+        switch (nx) {
+        case 0:                                               /* HOPBYHOP */
+            if (cur_nexthdr != 6) return ORACLE_WALK_DROP;
+            WALK_BYTE(e + 1, b);
+            cur_optlen = (uint16_t)((b + 1) << 3);
+            if (net_len + cur_optlen > 0xFFFFu) return ORACLE_WALK_BAD;   /* uint16 net_len wraps */
+            net_len = (uint16_t)(net_len + cur_optlen);
+            r = walk_hopbyhop(h, avail, e);
+            if (r == -2) return ORACLE_WALK_BAD;
+            if (r < 0) return ORACLE_WALK_DROP;
+            must_align = r;
+            break;
+        case 43: {                                            /* ROUTING */
+            uint8_t type, segleft;
+            WALK_BYTE(e + 1, b);
+            cur_optlen = (uint16_t)((b + 1) << 3);
+            if (net_len + cur_optlen > 0xFFFFu) return ORACLE_WALK_BAD;
+            net_len = (uint16_t)(net_len + cur_optlen);
+            WALK_BYTE(e + 3, segleft);
+            if (segleft != 0) {
+                WALK_BYTE(e + 2, type);
+                if (type != 2) return ORACLE_WALK_DROP;
+            }
+            break;
+        }
+        case 44: {                                            /* FRAG */
+            uint8_t om0, om1;
+            cur_optlen = 8;
+            if (net_len + 8u > 0xFFFFu) return ORACLE_WALK_BAD;
+            net_len = (uint16_t)(net_len + 8u);
+            WALK_BYTE(e + 2, om0);
+            WALK_BYTE(e + 3, om1);
+            (void)om0;                                        /* f->frag = om0 << 8 | om1: M = bit 0 */
+            frag = 1;
+            if ((om1 & 1u) && (plen % 8u) != 0) return ORACLE_WALK_DROP;
+            break;
+        }
+        case 60:                                              /* DESTOPT */
+            WALK_BYTE(e + 1, b);
+            cur_optlen = (uint16_t)((b + 1) << 3);
+            if (net_len + cur_optlen > 0xFFFFu) return ORACLE_WALK_BAD;
+            net_len = (uint16_t)(net_len + cur_optlen);
+            must_align = 1;
+            r = walk_destopt(h, avail, e);
+            if (r == -2) return ORACLE_WALK_BAD;
+            if (r < 0) return ORACLE_WALK_DROP;
+            break;
+        case 6: case 17: case 58:
+            if (must_align && (plen % 8u) != 0) return ORACLE_WALK_DROP;
+            *net_len_out = net_len;
+            *proto_out = nx;
+            return frag ? ORACLE_WALK_FRAG : ORACLE_WALK_PROTO;
+        default:                                              /* ESP, AUTH, NONE, invalid */
+            return ORACLE_WALK_DROP;
+        }
+        WALK_BYTE(e, nx);                                     /* exthdr->nxthdr, :805 */
+        cur_nexthdr = ptr;
+        ptr += cur_optlen;
+    }
+}
+
 /*
  * Fused IPv6 transport restatement, one datagram per descriptor.  desc.off ->
  * IPv6 header; desc.len = bytes available; desc.seed = f->net_len | proto << 16
- * as pico_ipv6_extension_headers (modules/pico_ipv6.c:707-800) leaves them
- * (seed 0: net_len 40, proto = hdr->nxthdr).
+ * when the stack already walked the extension headers (pico_ipv6_extension_headers,
+ * modules/pico_ipv6.c:707-809), or 0.
+ * RX, seed 0: the walk (oracle_ipv6_walk) decides: a discard (or a read past the frame) is
+ *   MALFORMED; a transport behind a fragment header is FRAG (pico_ipv6_process_frag,
+ *   :791-795, no transport check); otherwise net_len and proto are the walk's.
+ * TX, seed 0: net_len 40, proto = hdr->nxthdr (the stack builds the header it sends).
  *   transport_len = (uint16)(payload_len - (net_len - 40))     pico_ipv6.c:790
- * RX: pico_transport_crc_check (stack/pico_socket.c:1916-1968): TCP always (any
- *   length), UDP when the stored crc (t[6..7], inside the buffer) != 0; ICMPv6:
- *   pico_icmp6_checksum, a verdict only for the ND / MLD types the reference
- *   checks (type byte t[0] inside the buffer).  Other protocols: none.
+ * RX: pico_transport_crc_check (stack/pico_socket.c:1916-1968) as the reference runs it: the
+ *   `switch (net_hdr->proto)` (:1923) reads the header through a struct pico_ipv4_hdr cast --
+ *   for IPv6 that is byte 9 (the source address's second byte): 6 -> pico_tcp_checksum ->
+ *   pico_tcp_checksum_ipv6 (pico_tcp.c:492-505, TCP in the pseudo header), 17 -> when the
+ *   transport's bytes 6-7 are != 0, pico_udp_checksum_ipv6 (pico_udp.c:63-92, UDP in the pseudo
+ *   header), else no check -- for a TCP or UDP datagram (pico_transport_process_in is the TCP /
+ *   UDP module's).  With ORACLE_NXTHDR_DISPATCH instead by the transport protocol: TCP always,
+ *   UDP when its crc != 0.  ICMPv6 (pico_icmp6_process_in): pico_icmp6_checksum always, a
+ *   verdict only for the ND / MLD types the reference checks (pico_ipv6_nd.c:595,
+ *   pico_mld.c:415).  Other protocols: none.
  *   out = the checksum (0 = valid), 0 when none is computed.
  * TX: crc field read as zero (TCP pico_tcp.c:980, ICMPv6 pico_ipv6.c:1337, UDP
  *   crc already 0 from pico_udp_push :123 when pico_ipv6.c:1345 computes it);
  *   TCP needs 20, UDP 8, ICMPv6 4 transport bytes.  Other protocols: none.
  * MALFORMED: avail < 40, net_len < 40 or past avail, transport past avail, or a
- *   field the reference reads lying past avail.
- * ORACLE_REF_DISPATCH (RX): TCP / UDP frames are checked as pico_transport_crc_check
- *   (stack/pico_socket.c:1919-1958) literally does: `switch (net_hdr->proto)` through a
- *   struct pico_ipv4_hdr cast -- for IPv6 the header's byte 9 (source address byte 1):
- *   6 -> pico_tcp_checksum -> pico_tcp_checksum_ipv6 (pico_tcp.c:492-505, TCP in the pseudo
- *   header), 17 -> when t[6..7] != 0, pico_udp_checksum_ipv6 (UDP in the pseudo header),
- *   else no check.  The transport must hold t[6..7] whenever they are read.
+ *   field the reference reads lying past avail (a UDP header: 8 bytes).
  */
 void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint32_t n,
                        uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
 {
     uint32_t i;
     int tx = (flags & ORACLE_IPV4_TX) != 0;
-    int refd = !tx && (flags & ORACLE_REF_DISPATCH) != 0;
+    int refd = !tx && (flags & ORACLE_NXTHDR_DISPATCH) == 0;
     for (i = 0; i < n; i++) {
         const uint8_t *h = base + d[i].off;
         const uint8_t *t;
@@ -287,6 +504,15 @@ void oracle_batch_ipv6(const uint8_t *base, const struct pico_csum_desc *d, uint
         if (d[i].seed == 0) {
             net_len = 40;
             proto = h[6];
+            if (!tx) {
+                int w = oracle_ipv6_walk(h, avail, &net_len, &proto);
+                if (w == ORACLE_WALK_FRAG) {
+                    verdict[i] = PICO_CSUM_V_FRAG;
+                    continue;
+                }
+                if (w != ORACLE_WALK_PROTO)
+                    continue;
+            }
         }
         plen = (uint32_t)((h[4] << 8) | h[5]);
         if (net_len < 40 || net_len > avail)

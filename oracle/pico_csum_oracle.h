@@ -17,13 +17,23 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_NET_BAD   2u
 #define PICO_CSUM_V_L4_BAD    4u
 #define PICO_CSUM_V_MALFORMED 8u
-#define PICO_CSUM_V_EXPIRED  16u
+#define PICO_CSUM_V_EXPIRED  16u   /* forwarding batch */
+#define PICO_CSUM_V_FRAG     16u   /* RX / TX batches: a fragment (same bit, other batches) */
 #define PICO_CSUM_V_DROP_L2  32u
 #define PICO_CSUM_V_ARP      64u
 #define PICO_CSUM_V_IPV6    128u
 
 #define ORACLE_IPV4_TX 1u
-#define ORACLE_REF_DISPATCH 4u   /* IPv6 RX: pico_transport_crc_check's byte-9 dispatch (PICO_CSUM_F_REF_DISPATCH) */
+/* IPv6 RX: check TCP / UDP by the transport's own protocol (PICO_CSUM_F_NXTHDR_DISPATCH);
+ * without it, pico_transport_crc_check's byte-9 dispatch (the reference's behaviour) */
+#define ORACLE_NXTHDR_DISPATCH 4u
+
+/* pico_ipv6_extension_headers outcome (oracle_ipv6_walk) */
+#define ORACLE_WALK_DROP  0   /* the reference discards the datagram */
+#define ORACLE_WALK_PROTO 1   /* transport reached: *net_len, *proto */
+#define ORACLE_WALK_FRAG  2   /* transport reached behind a fragment header: handed to reassembly */
+#define ORACLE_WALK_BAD  -1   /* the reference would read past the frame, or never terminates */
+int oracle_ipv6_walk(const uint8_t *h, uint32_t avail, uint32_t *net_len, uint8_t *proto);
 
 typedef uint16_t (*oracle_checksum_fn)(void *buf, uint32_t len);
 

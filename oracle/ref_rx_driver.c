@@ -1,0 +1,226 @@
+/*
+ * ref_rx_driver.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Runs the reference's own RX decisions on single datagrams, so the fused RX verdicts of the
+ * oracle and of the HIP kernels are pinned to the reference itself (VERDICT r02 "next" 1 and 3):
+ * oracle/_ref/libref_rx.so = the reference stack compiled from /root/reference (stack/*.c and
+ * the IPv4 / IPv6 / ICMP / TCP / UDP / fragment / MLD / IGMP / multicast / null-device modules)
+ * with pico_ipv4.c, pico_ipv6.c and pico_socket.c reached through ref_rx_wrap.c.  The link uses
+ * --wrap so that this file OBSERVES the hand-offs of pico_ipv4_process_in /
+ * pico_ipv6_extension_headers without changing any reference code:
+ *   __wrap_pico_ipv4_process_frag / __wrap_pico_ipv6_process_frag   -> "handed to reassembly"
+ *   __wrap_pico_transport_receive                                    -> "delivered to proto"
+ * (a delivered frame is kept for the transport check, rr_transport_crc_check, or discarded).
+ *
+ * rr_ipv4_rx(datagram, avail): a frame with net_hdr at the buffer start and buffer_len = avail
+ *   (allocated larger, zero-filled behind avail) goes through pico_ipv4_process_in on a null
+ *   device that owns one /24 IPv4 link per destination added with rr_ipv4_link.  Result bits:
+ *     1 FRAG seen, 2 delivered (protocol in bits 8-15; the UDP / ICMPv4 broadcast enqueues of
+ *     pico_ipv4_process_bcast_in count as delivered), 4 transport check passed (TCP / UDP
+ *     delivered), 16 the header checksum passed (pico_ipv4_crc_check on a copy with
+ *     f->net_len = 20 + 4 (IHL - 5) as :394-400 sets it).
+ * rr_ipv6_rx(datagram, avail, &net_len, &proto): pico_ipv6_extension_headers on the frame;
+ *   returns 0 discarded, 1 transport reached (net_len / proto = f->net_len and the returned
+ *   protocol), 2 handed to pico_ipv6_process_frag; for 1 with TCP / UDP, bit 4 = the transport
+ *   check (pico_transport_crc_check, with f->transport_hdr / transport_len as the walk set them)
+ *   passed.
+ * Callers (tests/golden/make_ref_rx.py) only pass datagrams whose reference reads stay inside
+ * avail and whose walk terminates (the oracle restatement decides which; the others are
+ * restatement-only and documented so).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "pico_stack.h"
+#include "pico_frame.h"
+#include "pico_device.h"
+#include "pico_ipv4.h"
+#include "pico_ipv6.h"
+#include "pico_udp.h"
+#include "pico_icmp4.h"
+#include "pico_queue.h"
+#include "pico_dev_null.h"
+
+int rr_ipv4_process_in(struct pico_frame *f);
+int rr_ipv4_crc_check(struct pico_frame *f);
+int rr_ipv6_ext_headers(struct pico_frame *f);
+int rr_transport_crc_check(struct pico_frame *f);
+
+void __real_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto);
+void __real_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_frame *f, uint8_t proto);
+int32_t __real_pico_transport_receive(struct pico_frame *f, uint8_t proto);
+void __wrap_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto);
+void __wrap_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_frame *f, uint8_t proto);
+int32_t __wrap_pico_transport_receive(struct pico_frame *f, uint8_t proto);
+
+int rr_init(void);
+int rr_ipv4_link(uint32_t addr);
+int rr_ipv4_rx(const uint8_t *d, uint32_t avail);
+int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
+
+static struct pico_device *g_dev;
+static int g_frag, g_deliv_proto;
+static struct pico_frame *g_deliv;
+static int g_forward;          /* 1: call the real hand-offs (reassembly runs) */
+
+void __wrap_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto)
+{
+    g_frag = 1;
+    if (g_forward)
+        __real_pico_ipv4_process_frag(hdr, f, proto);
+}
+
+void __wrap_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_frame *f, uint8_t proto)
+{
+    g_frag = 1;
+    if (g_forward)
+        __real_pico_ipv6_process_frag(frag, f, proto);
+}
+
+int32_t __wrap_pico_transport_receive(struct pico_frame *f, uint8_t proto)
+{
+    if (g_deliv)
+        pico_frame_discard(g_deliv);
+    g_deliv = f;
+    g_deliv_proto = proto;
+    return 0;
+}
+
+int rr_init(void)
+{
+    if (g_dev)
+        return 0;
+    /* the reference's dbg() is printf (include/arch/pico_posix.h:19): unbuffered, so its lines
+     * reach fd 1 at once (a test runner's capture) instead of a buffer flushed at exit */
+    setvbuf(stdout, NULL, _IONBF, 0);
+    if (pico_stack_init() != 0)
+        return -1;
+    g_dev = pico_null_create("rr0");
+    return g_dev ? 0 : -1;
+}
+
+int rr_ipv4_link(uint32_t addr)
+{
+    struct pico_ip4 a, m;
+    a.addr = addr;
+    m.addr = 0x00FFFFFFu;    /* 255.255.255.0: only x.y.z.255 of the link's /24 is a broadcast */
+    return pico_ipv4_link_add(g_dev, a, m);
+}
+
+#define RR_PAD 70000u   /* zero bytes behind avail: a read past avail is defined (callers avoid it) */
+
+static struct pico_frame *mk(const uint8_t *d, uint32_t avail)
+{
+    struct pico_frame *f = pico_frame_alloc(avail + RR_PAD);
+    if (!f)
+        return NULL;
+    memset(f->buffer, 0, avail + RR_PAD);
+    memcpy(f->buffer, d, avail);
+    f->buffer_len = avail;
+    f->start = f->buffer;
+    f->len = avail;
+    f->datalink_hdr = f->buffer;
+    f->net_hdr = f->buffer;
+    f->transport_hdr = NULL;
+    f->dev = g_dev;
+    return f;
+}
+
+/* the delivered frame of the last call, if any: its transport check for TCP / UDP */
+static int delivered_check(void)
+{
+    int ok = 0;
+    struct pico_frame *f = g_deliv;
+    g_deliv = NULL;
+    if (!f)
+        return 0;
+    if (g_deliv_proto == 6 || g_deliv_proto == 17) {
+        ok = rr_transport_crc_check(f);      /* discards f when it fails */
+        if (ok)
+            pico_frame_discard(f);
+    } else {
+        pico_frame_discard(f);
+    }
+    return ok;
+}
+
+int rr_ipv4_rx(const uint8_t *d, uint32_t avail)
+{
+    struct pico_frame *f, *c;
+    struct pico_frame *q;
+    int r = 0;
+    if (!g_dev || avail < 20)
+        return -1;
+    /* the header check alone, on a copy (net_len as pico_ipv4_process_in :394-400 sets it) */
+    c = mk(d, avail);
+    if (!c)
+        return -1;
+    c->net_len = (uint16_t)(20u + ((d[0] & 0x0Fu) > 5u ? 4u * ((d[0] & 0x0Fu) - 5u) : 0u));
+    if (rr_ipv4_crc_check(c)) {
+        r |= 16;
+        pico_frame_discard(c);
+    }
+    f = mk(d, avail);
+    if (!f)
+        return -1;
+    g_frag = 0;
+    g_deliv = NULL;
+    rr_ipv4_process_in(f);
+    if (g_frag)
+        r |= 1;
+    /* pico_ipv4_process_bcast_in / _local_unicast_in enqueue UDP and ICMPv4 directly (:299,
+     * :309, :359) */
+    while ((q = pico_dequeue(pico_proto_udp.q_in)) != NULL) {
+        if (g_deliv)
+            pico_frame_discard(g_deliv);
+        g_deliv = q;
+        g_deliv_proto = 17;
+    }
+    while ((q = pico_dequeue(pico_proto_icmp4.q_in)) != NULL) {
+        if (g_deliv)
+            pico_frame_discard(g_deliv);
+        g_deliv = q;
+        g_deliv_proto = 1;
+    }
+    if (g_deliv) {
+        r |= 2 | (g_deliv_proto << 8);
+        if (delivered_check())
+            r |= 4;
+    }
+    return r;
+}
+
+int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto)
+{
+    struct pico_frame *f;
+    int ret, r;
+    if (avail < 40)
+        return -1;
+    f = mk(d, avail);
+    if (!f)
+        return -1;
+    g_frag = 0;
+    ret = rr_ipv6_ext_headers(f);
+    *net_len = f->net_len;
+    *proto = ret > 0 ? (uint32_t)ret : 0u;
+    if (g_frag) {
+        pico_frame_discard(f);
+        return 2;
+    }
+    if (ret <= 0) {
+        pico_frame_discard(f);
+        return 0;
+    }
+    r = 1;
+    if (ret == 6 || ret == 17) {
+        /* what pico_transport_receive hands on: net_hdr, transport_hdr, transport_len as set */
+        if (rr_transport_crc_check(f)) {
+            r |= 4;
+            pico_frame_discard(f);
+        }
+    } else {
+        pico_frame_discard(f);
+    }
+    return r;
+}

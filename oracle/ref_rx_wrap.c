@@ -1,0 +1,32 @@
+/*
+ * ref_rx_wrap.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * One of three translation units that compile an UNMODIFIED reference source file together
+ * with a few exported accessors for its static functions (the technique of the reference's
+ * own module tests, test/unit/modunit_*.c, which #include the module they test).  Built by
+ * oracle/Makefile (`make refrx`) three times, once per REF_RX_UNIT:
+ *   1: modules/pico_ipv4.c   rr_ipv4_process_in  = pico_ipv4_process_in   (:381-470)
+ *                            rr_ipv4_crc_check   = pico_ipv4_crc_check    (:243-257)
+ *   2: modules/pico_ipv6.c   rr_ipv6_ext_headers = pico_ipv6_extension_headers (:707-809)
+ *   3: stack/pico_socket.c   rr_transport_crc_check = pico_transport_crc_check (:1916-1968)
+ * and linked with the rest of the reference stack (every other object compiled from its own
+ * source) into oracle/_ref/libref_rx.so, driven by ref_rx_driver.c.  Nothing here is product
+ * code; nothing of the reference is copied (the #include names the file where it lies).
+ */
+#if REF_RX_UNIT == 1
+#include "pico_ipv4.c"
+int rr_ipv4_process_in(struct pico_frame *f);
+int rr_ipv4_crc_check(struct pico_frame *f);
+int rr_ipv4_process_in(struct pico_frame *f) { return pico_ipv4_process_in(&pico_proto_ipv4, f); }
+int rr_ipv4_crc_check(struct pico_frame *f) { return pico_ipv4_crc_check(f); }
+#elif REF_RX_UNIT == 2
+#include "pico_ipv6.c"
+int rr_ipv6_ext_headers(struct pico_frame *f);
+int rr_ipv6_ext_headers(struct pico_frame *f) { return pico_ipv6_extension_headers(f); }
+#elif REF_RX_UNIT == 3
+#include "pico_socket.c"
+int rr_transport_crc_check(struct pico_frame *f);
+int rr_transport_crc_check(struct pico_frame *f) { return pico_transport_crc_check(f); }
+#else
+#error "REF_RX_UNIT must be 1, 2 or 3"
+#endif

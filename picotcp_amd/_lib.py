@@ -46,8 +46,10 @@ EXPORTED = (
 
 F_WRITE = 0x1
 F_TX = 0x2
-F_REF_DISPATCH = 0x4   # IPv6 RX: pico_transport_crc_check's byte-9 dispatch (include/pico_csum.h)
+F_NXTHDR_DISPATCH = 0x4   # IPv6 RX: TCP / UDP by next header, not the reference's byte 9 (include/pico_csum.h)
 V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
+V_FRAG = 16                # RX / TX batches (V_EXPIRED: the forwarding batch)
+ABI_VERSION = 2
 V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
 EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12
 
@@ -105,6 +107,8 @@ def load() -> ctypes.CDLL:
     sig("pico_csum_last_error", ctypes.c_char_p)
     sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32, u32, u32, u32)
     del u8p
+    if lib.pico_csum_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {lib.pico_csum_abi_version()}, this binding {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

@@ -10,7 +10,8 @@ Reference interfaces mirrored (per frame in the reference, per batch here):
   checksum_uniform / checksum_batch  <- pico_checksum, pico_dualbuffer_checksum
                                         (stack/pico_frame.c:312-328)
   ipv4_checksum_batch                <- pico_ipv4_checksum / pico_ipv4_crc_check
-                                        (modules/pico_ipv4.c:231-257),
+                                        (modules/pico_ipv4.c:231-257), pico_ipv4_process_in
+                                        (:381-456: source, evil bit, IHL, fragments),
                                         pico_tcp_checksum_ipv4 (pico_tcp.c:422),
                                         pico_udp_checksum_ipv4 (pico_udp.c:36),
                                         pico_icmp4_checksum (pico_icmp4.c:30),
@@ -24,8 +25,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (F_REF_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_IPV6, V_L4_BAD,  # noqa: F401
-                   V_MALFORMED, V_NET_BAD)
+from ._lib import (F_NXTHDR_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_FRAG,  # noqa: F401
+                   V_IPV6, V_L4_BAD, V_MALFORMED, V_NET_BAD)
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
 assert DESC_DTYPE.itemsize == 16
@@ -214,6 +215,11 @@ def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: 
     return verdict
 
 
+def _require_u8(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.uint8 or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous uint8 tensor")
+
+
 def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: int, groups: torch.Tensor,
                           out: torch.Tensor, out_desc: torch.Tensor, stream=None, results=None):
     """IPv4 reassembly gather + transport check (pico_fragments.c:216-358): groups = uint32
@@ -222,10 +228,14 @@ def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: i
     int16[n], verdict uint8[n])."""
     for t, nm in ((base, "base"), (frag_desc, "frag_desc"), (groups, "groups"), (out, "out"), (out_desc, "out_desc")):
         _require_device(t, nm)
+        if t.device != base.device:
+            raise ValueError(f"{nm} is on {t.device}, the batch on {base.device}")
+    _require_u8(base, "base")
+    _require_u8(out, "out")
     n = groups.numel() // 2
     if groups.element_size() != 4 or not groups.is_contiguous():
         raise ValueError("groups must be a contiguous 32-bit tensor of (first, count) pairs")
-    if frag_desc.numel() < 16 * n_frag or out_desc.numel() < 16 * n:
+    if frag_desc.numel() * frag_desc.element_size() < 16 * n_frag or out_desc.numel() * out_desc.element_size() < 16 * n:
         raise ValueError("descriptor tensor shorter than its count")
     dev = base.device
     if results is None:
@@ -244,13 +254,15 @@ def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: i
 
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
-    """Force a kernel launch shape (tests / bench sweeps); group == 0 = automatic,
-    1 = flat work-list kernel, 2 = sorted-rounds kernel (unroll defaults to 0 there,
-    to 1 elsewhere)."""
+    """Force a kernel launch shape (tests / bench sweeps): group 0 = automatic; 2 = descriptor
+    batches with `fpw` frames per wave; 4..64 = uniform rings (lanes per frame, cpl, fpw,
+    unroll, nt, pipeline as in include/pico_csum.h)."""
     if unroll is None:
         unroll = 0 if group == 2 else 1
-    if group == 0:
-        unroll = fpw = cpl = nt = pipeline = 0
+    if group in (0, 2):
+        unroll = cpl = nt = pipeline = 0
+        if group == 0:
+            fpw = 0
     _lib.check("pico_csum_set_launch_override",
                _lib.load().pico_csum_set_launch_override(group, cpl, unroll, fpw, nt, pipeline))
 

@@ -5,8 +5,9 @@
  *          (ref stack/pico_frame.c:279-328) -- synchronous host code, the
  *          reference calls them inline per frame (see include/pico_csum.h).
  * Layer 2: argument checking + launch-shape choice for the batched HIP
- *          kernels (picotcp_amd/csrc/pico_csum_kernels.hip), reached through
- *          the thin extern "C" launchers declared below.
+ *          kernels (pico_csum_k_raw.hip: uniform rings; pico_csum_k_sorted.hip:
+ *          every descriptor batch and the forwarding step; pico_csum_k_frag.hip:
+ *          reassembly), reached through the thin extern "C" launchers declared below.
  * Layer 3: host-resident batches: pinned staging, two streams, chunked
  *          H2D -> kernel -> D2H overlap.
  */
@@ -22,34 +23,22 @@
 
 #include "pico_csum.h"
 
-/* kernels TU (C++/HIP), extern "C" */
-int pico_csum_launch_raw(void *base, uint64_t base_len, const void *desc, uint64_t stride, uint32_t len,
-                         uint32_t n, uint32_t seed, int32_t crc_off, uint32_t flags, uint16_t *out,
-                         uint32_t *bad, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt, uint32_t fpw,
-                         int uniform, void *stream);
-int pico_csum_launch_desc_adaptive(void *base, uint64_t base_len, const void *desc, uint32_t n, int32_t crc_off,
-                                   uint32_t flags, uint16_t *out, uint32_t *bad, uint32_t nt, void *stream);
+/* kernel TUs (C++/HIP), extern "C" */
+int pico_csum_launch_raw(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
+                         uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t U, uint32_t nt,
+                         uint32_t fpw, void *stream);
 int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
                                 uint32_t win, void *stream);
-int pico_csum_launch_flat(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode,
-                          int32_t crc_off, uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net,
-                          uint16_t *out_l4, uint8_t *verdict, uint32_t CPL, uint32_t nt, uint32_t fpw,
-                          uint32_t max_blocks, void *stream);
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
-                            uint8_t *verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
-                            uint64_t mac48, void *stream);
+                            uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
                                   void *stream);
 int pico_csum_launch_ipv4_reassemble(const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
                                      const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len,
                                      const void *out_desc, uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict,
                                      void *stream);
-int pico_csum_launch_ipv4(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
-                          uint16_t *out_net,
-                          uint16_t *out_l4, uint8_t *verdict, uint32_t G, uint32_t CPL, uint32_t fpw,
-                          void *stream);
 
 /* ------------------------------------------------------------------ errors */
 
@@ -152,26 +141,23 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
         g_ovr_group = g_ovr_cpl = g_ovr_unroll = g_ovr_fpw = g_ovr_nt = g_ovr_pipe = 0;
         return 0;
     }
+    if (group == 2) {            /* descriptor batches: the sorted-rounds kernel, fpw frames per wave */
+        if (fpw == 0 || fpw > 64)
+            return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: fpw in [1, 64]");
+        g_ovr_group = 2; g_ovr_fpw = fpw;
+        g_ovr_cpl = g_ovr_unroll = g_ovr_nt = g_ovr_pipe = 0;
+        return 0;
+    }
     if (pipeline > 3)
         return fail(PICO_CSUM_EINVAL, "pipeline must be 0 (auto), 1 (off), 2 (on) or 3 (on, global loads "
                                         "instead of the buffer window)");
-    if (!(group == 1 || group == 2 || group == 3 || group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
-        return fail(PICO_CSUM_EINVAL, "group must be 1 (flat work-list kernel), 2 (sorted rounds), 3 (per-wave adaptive), "
-                                        "4, 8, 16, 32 or 64");
+    if (!(group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
+        return fail(PICO_CSUM_EINVAL, "group must be 2 (descriptor batches) or 4, 8, 16, 32, 64 (uniform rings)");
     if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
         return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
-    if (group == 1 && unroll > 8)
-        return fail(PICO_CSUM_EINVAL, "flat kernel: unroll = persistent blocks per CU, 1..8 (0 = one batch per wave)");
-    if (group == 2 && (!(unroll == 0 || unroll == 1 || unroll == 2 || unroll == 4) || !(cpl == 4 || cpl == 8) ||
-                       ((unroll == 1 || unroll == 2) && cpl != 8)))
-        return fail(PICO_CSUM_EINVAL, "sorted-rounds kernel: cpl 4 or 8; unroll = narrowest round width "
-                                        "0 (auto), 1 (cpl 8 only), 2 (as 1, plus the span stream for dense "
-                                        "waves) or 4");
-    if (group == 3 && (unroll != 0 || cpl != 8 || fpw != 16))
-        return fail(PICO_CSUM_EINVAL, "per-wave adaptive kernel: unroll 0, cpl 8, fpw 16");
-    if (group > 3 && (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8))
+    if (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8)
         return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
-    if (fpw == 0 || fpw > 64 || (group > 3 && fpw % (64 / group) != 0))
+    if (fpw == 0 || fpw > 64 || fpw % (64 / group) != 0)
         return fail(PICO_CSUM_EINVAL, "fpw must be a multiple of 64/group in [1, 64]");
     if (nt > 3)
         return fail(PICO_CSUM_EINVAL, "nt must be 0 (auto), 1 (off), 2 (on) or 3 (on except frame edges)");
@@ -182,67 +168,40 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
 
 struct shape { uint32_t G, CPL, U, nt, fpw, pipe; };
 
-/* Launch shape from the typical frame length (measured on MI355X, see
- * DESIGN.md "Launch shapes"): a lane group spans the frame in about 6-8
- * 16-byte chunks per lane, all issued in one pass (CPL = 8), so a wave keeps
- * 8 KiB of loads in flight and the per-frame head/tail corrections and group
- * reductions are shared by 64/G frames.  Frames per wave: about 16K waves in
- * the grid (2 residency rounds on 256 CUs) balances the tail; at most 64 (one
- * coalesced result store per wave).  Non-temporal loads pay on streams of
- * frames >= 1 KiB (C1 +3 %, C3 +10 %) and cost a little on small IMIX frames. */
-static uint32_t pick_fpw(uint32_t n, uint32_t G)
-{
-    uint32_t ng = 64u / G, f = n / 16384u;
-    if (f > 64u) f = 64u;
-    f -= f % ng;
-    if (f < ng) f = ng;
-    return f;
-}
-
-static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
+/* Uniform rings (measured on MI355X, DESIGN.md "Launch shapes"): a lane group spans the frame in
+ * about 6-8 16-byte chunks per lane, all issued in one pass (CPL = 8), so a wave keeps 8 KiB of
+ * loads in flight and the per-frame head/tail corrections and group reductions are shared by
+ * 64/G frames.  Frames that fit one pass take the software-pipelined kernel (two frame sets in
+ * registers; C1 8 frames per wave, bursts of <= 4K frames one set per group).  Larger frames
+ * (C3 9000 B): the multi-pass kernel, ~16K waves in the grid.  Non-temporal loads pay on
+ * frames >= 1 KiB (C1 +3 %, C3 +10 %). */
+static struct shape uniform_shape(uint32_t n, uint32_t len)
 {
     struct shape s;
-    uint32_t chunks = typical_len / 16u + 1u, per;
+    uint32_t chunks = len / 16u + 1u, per, ng, f;
     s.G = 4;
     while (s.G < 64 && s.G * 8u < chunks)
         s.G *= 2;
     per = (chunks + s.G - 1) / s.G;
     s.CPL = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
     s.U = 1;
-    s.nt = typical_len >= 1024u;
-    s.fpw = pick_fpw(n, s.G);
-    /* uniform frames that fit one pass: the software-pipelined kernel, with two
-     * frame sets per wave (more, shorter waves balance best: C1 8 frames/wave) */
-    s.pipe = uniform && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)typical_len + 15u;
+    s.nt = len >= 1024u;
+    ng = 64u / s.G;
+    s.pipe = (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u;
     if (s.pipe) {
-        uint32_t ng = 64u / s.G, f = n / 32768u;
+        f = n / 32768u;
         f -= f % ng;
         s.fpw = f < 2 * ng ? 2 * ng : f > 64 ? 64 : f;
-        /* bursts of <= 4K frames: one frame set per lane group (more, shorter waves), -10 %
-         * at 1K-4K x 1500 B (tools/burst_sweep.py, r02g) */
-        if (n <= 4096u)
+        if (n <= 4096u)          /* bursts of <= 4K frames (tools/burst_sweep.py, r02g) */
             s.fpw = ng;
+    } else {
+        f = n / 16384u;
+        if (f > 64u) f = 64u;
+        f -= f % ng;
+        s.fpw = f < ng ? ng : f;
     }
-    if (!uniform) {
-        /* descriptor batches: sorted-rounds kernel (each wave sorts its frames by
-         * length and runs lane-group rounds sized per round).  8 chunks per lane
-         * (<= 128 VGPRs, 4 waves per SIMD); ~4K waves, so a 256K-frame batch is
-         * one residency round of 64-frame waves; non-temporal loads in the wide
-         * (>= 16-lane) rounds only.  Measured on MI355X: DESIGN.md "Launch shapes". */
-        uint32_t f = n / 2048u;
-        s.G = 2;
-        s.CPL = 8;
-        s.U = 1;            /* narrowest round width: 1 = one frame per lane for <= 8-chunk frames */
-        s.nt = 1;
-        /* n / 2048 frames per wave in [4, 64]: 1K-4K bursts 4 (-20 % vs 16), 16K 8, 64K 32,
-         * 256K 64 (one residency round of 64-frame waves) -- tools/burst_sweep.py, r02g */
-        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
-    }
-    if (g_ovr_group) {
-        uint32_t auto_u = s.U;
+    if (g_ovr_group >= 4) {
         s.G = g_ovr_group; s.CPL = g_ovr_cpl; s.U = g_ovr_unroll; s.fpw = g_ovr_fpw;
-        if (s.G == 2 && s.U == 0)
-            s.U = s.CPL == 8 ? auto_u : 4;
         s.nt = g_ovr_nt >= 2 ? g_ovr_nt - 1 : 0;
         if (g_ovr_pipe)
             s.pipe = g_ovr_pipe >= 2;
@@ -250,12 +209,24 @@ static struct shape pick_shape(uint32_t n, uint32_t typical_len, int uniform)
     return s;
 }
 
-/* sorted-rounds kernel: U -> the launcher's variant (1: 1-lane class, 2: + span stream) */
-#define SMALL_ARG(u) ((u) == 1 ? 1u : (u) == 2 ? 2u : 0u)
+/* Descriptor batches: the sorted-rounds kernel (each wave orders its <= 64 frames by size class
+ * and sums them in lane-group rounds sized per round).  n / 2048 frames per wave in [4, 64]:
+ * 1K-4K bursts 4 (-20 % vs 16), 16K 8, 64K 32, 256K 64 (one residency round of 64-frame waves)
+ * -- tools/burst_sweep.py, r02g. */
+static int desc_fpw(uint32_t n, uint32_t *fpw)
+{
+    uint32_t f = n / 2048u;
+    if (g_ovr_group >= 4)
+        return fail(PICO_CSUM_EINVAL, "launch override group %u is for uniform rings; descriptor batches take "
+                                        "group 2", g_ovr_group);
+    *fpw = g_ovr_group == 2 ? g_ovr_fpw : f < 4 ? 4 : f > 64 ? 64 : f;
+    return 0;
+}
 
-/* Ablation bits for the sorted-rounds kernel (PICO_CSUM_ABLATE, measurement only):
- * 1 = skip the rounds, 2 = skip the head-window loads, 4 = skip the IPv4 TX crc writes.
- * Passed in flags bits 8+, which the public API rejects. */
+/* Ablation bits for measurement builds of the sorted-rounds kernel (-DPICO_CSUM_AB, see
+ * pico_csum_dev.h): PICO_CSUM_ABLATE bit 1 = skip the rounds, 2 = skip the head-window loads,
+ * 4 = skip the IPv4 TX crc writes; passed in flags bits 8+, which the public API rejects.  The
+ * product library compiles them out. */
 static uint32_t ablate_flags(void)
 {
     const char *e = getenv("PICO_CSUM_ABLATE");
@@ -292,15 +263,6 @@ static int need_device(void)
     return 0;
 }
 
-/* compute units of the calling thread's current device */
-static uint32_t cur_cus(void)
-{
-    int d = 0;
-    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= g_dev_count)
-        return 256u;
-    return g_dev_cus[d];
-}
-
 static int launch_status(int herr, const char *what)
 {
     if (herr == (int)hipSuccess)
@@ -313,15 +275,11 @@ static int launch_status(int herr, const char *what)
     return fail(PICO_CSUM_EIO, "%s: %s", what, hipGetErrorString((hipError_t)herr));
 }
 
-/* Typical frame length for descriptor batches (unknown on the host without a
- * sync): the simple-IMIX mean (354 B). */
-#define DESC_TYPICAL_LEN 354u
-
 int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
                             uint32_t n, int32_t crc_off, uint32_t flags, uint16_t *d_out,
                             uint32_t *d_bad, void *stream)
 {
-    struct shape s;
+    uint32_t fpw = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -335,25 +293,10 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && crc_off < 0)
         return fail(PICO_CSUM_EINVAL, "F_WRITE needs crc_off >= 0");
-    if ((rc = need_device()) != 0)
+    if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (s.G == 3)       /* lane groups sized per wave from its frames' mean length */
-        return launch_status(pico_csum_launch_desc_adaptive(d_base, base_len, d_desc, n, crc_off, flags, d_out,
-                                                            d_bad, 0, stream),
-                             "pico_checksum_batch_dev");
-    if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
-                                                     d_out, d_bad,
-                                                     NULL, NULL, NULL, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U), 0, stream),
-                             "pico_checksum_batch_dev");
-    if (s.G == 1)
-        return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 0, crc_off, flags, d_out, d_bad,
-                                                   NULL, NULL, NULL, s.CPL, s.nt, s.fpw,
-                                                   s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
-                             "pico_checksum_batch_dev");
-    return launch_status(pico_csum_launch_raw(d_base, base_len, d_desc, 0, 0, n, 0, crc_off, flags, d_out,
-                                              d_bad, s.G, s.CPL, s.U, s.nt, s.fpw, 0, stream),
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
+                                                 d_out, d_bad, NULL, NULL, NULL, fpw, 0, stream),
                          "pico_checksum_batch_dev");
 }
 
@@ -371,15 +314,15 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return fail(PICO_CSUM_EINVAL, "frames exceed base_len");
     if ((rc = need_device()) != 0)
         return rc;
-    s = pick_shape(n, len, 1);
-    if (s.G <= 3)
-        return fail(PICO_CSUM_EINVAL, "groups 1-3 (flat, sorted, adaptive) serve descriptor batches only");
+    if (g_ovr_group == 2)
+        return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
+    s = uniform_shape(n, len);
     if (s.pipe && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u)
         return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,
                                                          s.nt, s.fpw, g_ovr_pipe != 3, stream),
                              "pico_checksum_batch_uniform_dev");
-    return launch_status(pico_csum_launch_raw((void *)d_base, base_len, NULL, stride, len, n, seed, -1, 0,
-                                              d_out, NULL, s.G, s.CPL, s.U, s.nt, s.fpw, 1, stream),
+    return launch_status(pico_csum_launch_raw(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL, s.U, s.nt,
+                                              s.fpw, stream),
                          "pico_checksum_batch_uniform_dev");
 }
 
@@ -387,7 +330,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_net,
                                  uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
 {
-    struct shape s;
+    uint32_t fpw = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -399,24 +342,10 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
-    if ((rc = need_device()) != 0)
+    if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (s.G == 3)
-        return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
-    if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
-                                                     NULL,
-                                                     d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U),
-                                                     0, stream),
-                             "pico_ipv4_checksum_batch_dev");
-    if (s.G == 1)
-        return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 1, -1, flags, NULL, NULL,
-                                                   d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                                   s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
-                             "pico_ipv4_checksum_batch_dev");
-    return launch_status(pico_csum_launch_ipv4(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
-                                               d_verdict, s.G, s.CPL, s.fpw, stream),
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
+                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv4_checksum_batch_dev");
 }
 
@@ -424,7 +353,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream)
 {
-    struct shape s;
+    uint32_t fpw = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -432,39 +361,16 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "NULL buffer");
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
-    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_REF_DISPATCH))
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_NXTHDR_DISPATCH))
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
-    if ((flags & PICO_CSUM_F_REF_DISPATCH) && (flags & PICO_CSUM_F_TX))
-        return fail(PICO_CSUM_EINVAL, "F_REF_DISPATCH is an RX option");
-    if ((rc = need_device()) != 0)
+    if ((flags & PICO_CSUM_F_NXTHDR_DISPATCH) && (flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_NXTHDR_DISPATCH is an RX option");
+    if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (s.G == 3)
-        return fail(PICO_CSUM_EINVAL, "the per-wave adaptive kernel (group 3) serves raw batches only");
-    if (s.G != 2 && (flags & PICO_CSUM_F_REF_DISPATCH)) {   /* the sorted-rounds kernel implements it */
-        uint32_t f = n / 2048u;
-        s.G = 2;
-        s.CPL = 8;
-        s.U = 1;
-        s.nt = 1;
-        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
-    }
-    if (s.G == 2)
-        return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
-                                                     NULL, NULL,
-                                                     d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U), 0, stream),
-                             "pico_ipv6_checksum_batch_dev");
-    if (s.G != 1) {           /* the IPv6 mode exists in the flat and sorted kernels only */
-        s.G = 1;
-        s.CPL = 2;
-        s.U = 0;
-        s.fpw = n / 16384u < 1 ? 1 : n / 16384u > 64 ? 64 : n / 16384u;
-    }
-    return launch_status(pico_csum_launch_flat(d_base, base_len, d_desc, n, 2, -1, flags, NULL, NULL, NULL,
-                                               d_out_transport, d_verdict, s.CPL, s.nt, s.fpw,
-                                               s.U ? s.U * cur_cus() : 0xFFFFFFFFu, stream),
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
+                                                 NULL, NULL, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv6_checksum_batch_dev");
 }
 
@@ -475,8 +381,8 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
                                 uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
                                 uint8_t *d_verdict, void *stream)
 {
-    struct shape s;
     uint64_t mac48 = 0;
+    uint32_t fpw = 0;
     int rc, i;
     if (n == 0)
         return 0;
@@ -484,31 +390,21 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
         return fail(PICO_CSUM_EINVAL, "NULL buffer");
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
-    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_REF_DISPATCH))
+    if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_NXTHDR_DISPATCH))
         return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
-    if ((flags & PICO_CSUM_F_REF_DISPATCH) && (flags & PICO_CSUM_F_TX))
-        return fail(PICO_CSUM_EINVAL, "F_REF_DISPATCH is an RX option");
-    if ((rc = need_device()) != 0)
+    if ((flags & PICO_CSUM_F_NXTHDR_DISPATCH) && (flags & PICO_CSUM_F_TX))
+        return fail(PICO_CSUM_EINVAL, "F_NXTHDR_DISPATCH is an RX option");
+    if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
     if (mac) {
         for (i = 0; i < 6; i++)
             mac48 |= (uint64_t)mac[i] << (8 * i);
         flags |= KF_MACF;
     }
-    s = pick_shape(n, DESC_TYPICAL_LEN, 0);
-    if (s.G != 2) {           /* the Ethernet mode exists in the sorted-rounds kernel only */
-        uint32_t f = n / 2048u;
-        s.G = 2;
-        s.CPL = 8;
-        s.U = 1;
-        s.nt = 1;
-        s.fpw = f < 4 ? 4 : f > 64 ? 64 : f;
-    }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags | ablate_flags(), NULL, NULL,
-                                                 d_out_net, d_out_transport, d_verdict, s.CPL, s.nt, s.fpw, SMALL_ARG(s.U),
-                                                 mac48, stream),
+                                                 d_out_net, d_out_transport, d_verdict, fpw, mac48, stream),
                          "pico_eth_checksum_batch_dev");
 }
 

@@ -1,5 +1,5 @@
 // pico_csum_dev.h -- device helpers shared by the gfx950 kernel TUs of libpicocsum
-// (pico_csum_k_raw.hip, pico_csum_k_flat.hip, pico_csum_k_sorted.hip).  Header-only,
+// (pico_csum_k_raw.hip, pico_csum_k_sorted.hip, pico_csum_k_frag.hip).  Header-only,
 // internal; everything lives in an anonymous namespace (one copy per TU).
 //
 // The kernels of picoTCP's Internet checksum.
@@ -226,22 +226,21 @@ struct RawArgs {
 };
 
 
-struct Ipv4Args {
-    uint8_t* base;
-    uint64_t base_len;
-    const pico_csum_desc_dev* desc;
-    uint32_t n;
-    uint32_t flags;
-    uint32_t fpw;
-    uint16_t* out_net;
-    uint16_t* out_l4;
-    uint8_t* verdict;
-};
-
 constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8u, V_EXPIRED = 16u;
+constexpr uint32_t V_FRAG = 16u;        // RX / TX batches (V_EXPIRED: the forwarding batch only)
 constexpr uint32_t V_DROP_L2 = 32u, V_ARP = 64u, V_IPV6 = 128u;   // Ethernet mode (include/pico_csum.h)
 constexpr uint32_t F_MACF = 0x10000u;   // kernel flag (set by the host layer): filter destination MACs
-constexpr uint32_t F_REFD = 0x4u;       // PICO_CSUM_F_REF_DISPATCH (IPv6 RX)
+constexpr uint32_t F_NXD = 0x4u;        // PICO_CSUM_F_NXTHDR_DISPATCH (IPv6 RX)
+// phase-1 outcomes applied after the IPv4 header check (sorted kernel)
+constexpr uint32_t PV_DROP = 1u, PV_FRAG = 2u;
+
+// Phase ablations for measurement builds only (-DPICO_CSUM_AB, flags bits 8-10 from the
+// PICO_CSUM_ABLATE environment variable); the product library compiles them out.
+#ifdef PICO_CSUM_AB
+#define ABLATE(p, bit) (((p).flags & (bit)) != 0u)
+#else
+#define ABLATE(p, bit) false
+#endif
 
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
@@ -304,7 +303,7 @@ struct FlatArgs {
     uint32_t flags;
     uint16_t* out;        // RAW
     uint32_t* bad;        // RAW
-    uint16_t* out_net;    // IPV4
+    uint16_t* out_net;    // fused modes
     uint16_t* out_l4;
     uint8_t* verdict;
     uint32_t mac_lo;      // ETH: the device's MAC as stored (bytes 0-3, 4-5), with F_MACF
@@ -312,13 +311,12 @@ struct FlatArgs {
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t BIG_CHUNKS = 1u << 16;   // frames above this stream on their own
 
 
 // ---------------------------------------------------------------- dispatch
 
-// (G, CPL) shapes of the IPv4 kernel; the RAW kernel adds U (frames in flight per
-// group) and NT (non-temporal loads), with CPL*U <= 8 (<= 32 data VGPRs).
+// (G, CPL) shapes of the pipelined uniform kernel; the multi-pass uniform kernel adds U (frames
+// in flight per group) and NT (non-temporal loads), with CPL*U <= 8 (<= 32 data VGPRs).
 #define PICO_FOR_SHAPES(X) \
     X(64, 1) X(64, 2) X(64, 4) X(64, 8) \
     X(32, 1) X(32, 2) X(32, 4) X(32, 8) \

@@ -27,7 +27,7 @@ __device__ uint32_t g_stamps_n;
 
 // ---------------------------------------------------------------- sorted-rounds kernel
 //
-// Descriptor batches of any size mix, all modes (RAW / fused IPv4 / fused IPv6).
+// Descriptor batches of any size mix, all modes (RAW / fused IPv4 / fused IPv6 / Ethernet).
 // The lane-group body is the cheapest per chunk (an unmasked v_dot2 chain, edge
 // corrections only at frame edges) but a fixed group width G fits no size mix:
 // a wave waits for its largest frame.  Here a wave
@@ -152,186 +152,9 @@ __device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L
     }
 }
 
-// ---------------------------------------------------------------- span stream (dense waves)
-//
-// Most descriptor batches are bursts laid out back to back (a TAP / pico_device ring, the
-// C2 layout: datagrams behind 14-byte Ethernet headers).  For such a wave -- frames in
-// ascending order, each >= 16 bytes and < 64 KiB, gaps < 16 bytes -- the rounds are replaced
-// by ONE coalesced stream over the wave's span: step t reads chunks 64t .. 64t+63 (1 KiB, lane
-// l = chunk 64t + l; 8 steps in flight), so every line is fetched once and whole.  Per step,
-// no masks: each chunk gives two unmasked sums in the batch's own (absolute) pairing,
-// a = E + 256 O (v_dot2) and b = E + O (v_sad_u8); a frame owns the whole chunks from the one
-// holding its first byte up to the next frame's, and lane j (= frame j) adds its owned
-// chunks' a and b through two wave prefix sums (differences: exact, the reference's
-// wrapping uint32 arithmetic).  Once per frame: the bytes before its start in the first chunk
-// and past its end in the last (or its tail in the next frame's first chunk) are corrected
-// from those two chunks (kept in LDS), and an odd start swaps the pairing:
-// O = (a - b) / 255, E = b - O, sum = O + 256 E (exact: a frame < 64 KiB never wraps a).
-// Fused modes: a chunk inside a frame's first HW chunks is also written to its LDS
-// head-window row (the owner frame: a ballot of the chunks holding a frame's first byte +
-// mbcnt), so the header is parsed from LDS as before; the region (transport) sum is the total
-// minus the bytes before the region (Ethernet / IPv6 headers) and after it (padding).
-template <bool RAWM>
-struct StreamLds {
-    uint16_t mk[512];      // batch markers, chunk c: low byte = frame + 1 whose first byte, high = last byte is in c
-    uint4 tbuf[64];        // frame j's last chunk
-    uint4 hbuf[64];        // frame j's first chunk (RAW; the fused modes have it in the head-window row)
-};
-template <>
-struct StreamLds<false> {
-    uint16_t mk[512];
-    uint4 tbuf[64];
-};
-template <bool STREAM, bool RAWM>
-struct StreamSmem {
-    StreamLds<RAWM> s;
-};
-template <bool RAWM>
-struct StreamSmem<false, RAWM> {
-    uint32_t s;
-};
-
-// Dense: every frame of the wave in bounds, >= 16 bytes and < 64 KiB, each starting at or after
-// the previous one's end and less than 16 bytes behind it, and an even IPv6 network-header
-// length in the seed (MODE 2 / 3: the transport pairing is the frame's).  Wave-uniform.
-template <int MODE>
-__device__ __forceinline__ bool wave_dense(const FlatArgs& p, uint32_t lane, uint32_t cnt, bool oob, uint64_t off,
-                                           uint32_t len, uint32_t seed) {
-    const int prev = (int)(lane ? lane - 1u : 0u);
-    const uint64_t poff = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), prev) << 32) |
-                          (uint32_t)__shfl((int)(uint32_t)off, prev);
-    const uint32_t plen = (uint32_t)__shfl((int)len, prev);
-    bool ok = lane >= cnt || (!oob && len >= 16u && len < 65536u &&
-                              (lane == 0 || (off >= poff + plen && off < poff + plen + 16u)));
-    if (MODE == 2 || MODE == 3) ok = ok && (lane >= cnt || (seed & 1u) == 0u);
-    return __builtin_amdgcn_ballot_w64(!ok) == 0;
-}
-
-// Masked sums of chunk v's bytes in [x0, x1) (positions from the batch's 16-byte line, absolute
-// pairing): a = E + 256 O, b = E + O.
-__device__ __forceinline__ void masked_ab(const uint4 v, uint32_t ch, uint32_t x0, uint32_t x1, uint32_t& a,
-                                          uint32_t& b) {
-    const uint32_t lo = x0 <= ch ? 0u : min(x0 - ch, 16u);
-    const uint32_t hi = x1 <= ch ? 0u : min(x1 - ch, 16u);
-    const uint64_t ALL = ~0ull;
-    uint64_t m0 = lo >= 8u ? 0ull : (ALL << (8u * lo));
-    m0 &= hi >= 8u ? ALL : ~(ALL << (8u * hi));
-    uint64_t m1 = lo >= 16u ? 0ull : (lo <= 8u ? ALL : (ALL << (8u * (lo - 8u))));
-    m1 &= hi >= 16u ? ALL : (hi <= 8u ? 0ull : ~(ALL << (8u * (hi - 8u))));
-    const uint32_t x = v.x & (uint32_t)m0, y = v.y & (uint32_t)(m0 >> 32);
-    const uint32_t z = v.z & (uint32_t)m1, w = v.w & (uint32_t)(m1 >> 32);
-    a = dot2_add(w, dot2_add(z, dot2_add(y, dot2_add(x, 0u))));
-    b = __builtin_amdgcn_sad_u8(w, 0u, __builtin_amdgcn_sad_u8(z, 0u, __builtin_amdgcn_sad_u8(y, 0u, __builtin_amdgcn_sad_u8(x, 0u, 0u))));
-}
-
-// The stream over a dense wave's span; returns lane j's frame total (pairing from the
-// frame's start), fills the head-window rows (fused modes).
-template <int MODE>
-__device__ __forceinline__ uint32_t span_stream(const FlatArgs& p, StreamLds<MODE == 0>& T, uint4* stage,
-                                                uint32_t lane, uint32_t cnt, uint64_t off, uint32_t len) {
-    const uint64_t a0 = reinterpret_cast<uintptr_t>(p.base) + off;
-    const uint64_t B = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a0 >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a0)) & ~(uint64_t)15;
-    const bool fr = lane < cnt;
-    const uint32_t s = fr ? (uint32_t)(a0 - B) : 0u, e = fr ? s + len : 16u;
-    const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)cnt - 1);
-    const uint32_t fc = s >> 4, tc = (e - 1u) >> 4;                  // first / last chunk
-    const uint32_t nfc = (uint32_t)__shfl((int)fc, (int)min(lane + 1u, 63u));
-    const uint32_t oe = lane + 1u < cnt ? nfc : tc + 1u;               // owned chunks [fc, oe)
-    reinterpret_cast<uint4*>(T.mk)[lane] = make_uint4(0, 0, 0, 0);
-    uint8_t* mk8 = reinterpret_cast<uint8_t*>(T.mk);
-    const uint32_t nsteps = (E + 1023u) >> 10;
-    const Window w = make_window(B, (E + 15u) & ~15u);
-    uint32_t accA = 0u, accB = 0u, carry = 0u;
-    asm volatile("" ::: "memory");
-    // one batch = 8 steps (8 KiB) of loads in flight (loads past the span read zeros without a
-    // memory access)
-    auto load_batch = [&](uint4 (&v)[8], uint32_t tb) {
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) v[k] = load_win<false>(w, ((tb << 6) + 64u * k + lane) << 4);
-    };
-    auto sum_batch = [&](const uint4 (&v)[8], uint32_t tb) {
-        const uint32_t cb = tb << 6;                              // the batch's first chunk
-        if (fr && fc >= cb && fc < cb + 512u) mk8[2u * (fc - cb)] = (uint8_t)(lane + 1u);
-        if (fr && tc >= cb && tc < cb + 512u) mk8[2u * (tc - cb) + 1u] = (uint8_t)(lane + 1u);
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) {
-            const uint32_t ci = cb + 64u * k + lane;
-            const uint32_t m = T.mk[64u * k + lane];
-            T.mk[64u * k + lane] = 0;
-            const uint32_t hd = m & 0xFFu, tl = m >> 8;
-            const uint64_t M = __builtin_amdgcn_ballot_w64(hd != 0u);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-            const uint32_t f = min(carry + below + (hd ? 1u : 0u), 64u) - 1u;   // the owner (last frame started)
-            carry += (uint32_t)__builtin_popcountll(M);
-            const uint4 x = v[k];
-            const uint32_t a = dot2_add(x.w, dot2_add(x.z, dot2_add(x.y, dot2_add(x.x, 0u))));
-            const uint32_t b = __builtin_amdgcn_sad_u8(x.w, 0u, __builtin_amdgcn_sad_u8(x.z, 0u,
-                               __builtin_amdgcn_sad_u8(x.y, 0u, __builtin_amdgcn_sad_u8(x.x, 0u, 0u))));
-            if constexpr (MODE != 0) {
-                const uint32_t t = tl ? tl - 1u : f;
-                const uint32_t ffc = (uint32_t)__shfl((int)fc, (int)f), ftc = (uint32_t)__shfl((int)tc, (int)f);
-                const uint32_t tfc = (uint32_t)__shfl((int)fc, (int)t);
-                const uint32_t wi = ci - ffc, wt = ci - tfc;
-                if (wi < HW && ci <= ftc) stage[f * HW + (wi ^ (f & (HW - 1u)))] = x;
-                if (tl && t != f && wt < HW) stage[t * HW + (wt ^ (t & (HW - 1u)))] = x;
-            } else {
-                if (hd) T.hbuf[hd - 1u] = x;
-            }
-            if (tl) T.tbuf[tl - 1u] = x;
-            const uint32_t PA = wave_scan_add(a), PB = wave_scan_add(b);
-            const uint32_t bc = cb + 64u * k;
-            const bool in = fr && fc < bc + 64u && oe > bc;
-            const uint32_t lo = fc > bc ? fc - bc : 0u, hi = in ? min(oe - bc, 64u) : 1u;
-            const int ih = (int)hi - 1, il = lo ? (int)lo - 1 : 0;
-            const uint32_t PAh = (uint32_t)__shfl((int)PA, ih), PAl = (uint32_t)__shfl((int)PA, il);
-            const uint32_t PBh = (uint32_t)__shfl((int)PB, ih), PBl = (uint32_t)__shfl((int)PB, il);
-            if (in) {
-                accA += PAh - (lo ? PAl : 0u);
-                accB += PBh - (lo ? PBl : 0u);
-            }
-        }
-        asm volatile("" ::: "memory");
-    };
-    // (two batches in flight -- the next one's loads issued before the current one is summed --
-    // measured slower: C2 35.4 vs 32.6 us, the 1500-byte batch unchanged; profiles/r02u)
-    for (uint32_t tb = 0; tb < nsteps; tb += 8u) {
-        uint4 v[8];
-        load_batch(v, tb);
-        sum_batch(v, tb);
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    // the first chunk's bytes before the frame; the last chunk's bytes past it (owned) or the
-    // frame's tail in the next frame's first chunk (not owned)
-    uint4 H;
-    if constexpr (MODE != 0) H = stage[lane * HW + (lane & (HW - 1u))];
-    else H = T.hbuf[lane];
-    const uint4 L = T.tbuf[lane];
-    uint32_t ca, cbs;
-    masked_ab(H, 16u * fc, 16u * fc, s, ca, cbs);
-    accA -= ca;
-    accB -= cbs;
-    if (tc < oe) {
-        masked_ab(L, 16u * tc, e, 16u * tc + 16u, ca, cbs);
-        accA -= ca;
-        accB -= cbs;
-    } else {
-        masked_ab(L, 16u * tc, 16u * tc, e, ca, cbs);
-        accA += ca;
-        accB += cbs;
-    }
-    if (s & 1u) {                                                 // odd start: the swapped pairing
-        const uint32_t o = (uint32_t)(((uint64_t)(accA - accB) * 0x80808081ull) >> 39);
-        return o + 256u * (accB - o);
-    }
-    return accA;
-}
-
 // MODE: 0 RAW (p.crc_off / p.flags / p.out / p.bad), 1 fused IPv4, 2 fused IPv6,
 // 3 Ethernet front end (per frame: destination filter, ethertype -> IPv4 / IPv6 / ARP / drop;
-// pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in Ipv4Args-compatible fields of FlatArgs.
+// pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in the out_net / out_l4 / verdict fields of FlatArgs.
 // Phase 4: lane `lane` finalizes its frame (output index idx) from the LDS state.
 template <int MODE>
 __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t idx,
@@ -342,7 +165,8 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
     const uint32_t xpos = L.xo[lane].x;
     const uint32_t r = info.w & 15u;
     uint8_t* fp = p.base + (((((uint64_t)info.y) << 32) | info.x) + r);
-    uint32_t verdict = fin.x & 15u;
+    uint32_t verdict = fin.x & 8u;               // V_MALFORMED from phase 1, or 0
+    const uint32_t post = fin.x & 3u;            // PV_DROP / PV_FRAG: decided after the header check
     const bool parsed = fin.x & 16u, l4_needed = fin.x & 32u, oob = fin.x & 64u;
     const bool fam6 = MODE == 2 || (MODE == 3 && (fin.x & 128u));
     const uint32_t proto = (fin.x >> 8) & 0xFFu, tl = fin.x >> 16;
@@ -363,8 +187,10 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
             verdict = l2v;                   // dropped by the Ethernet layer, or ARP: no checksum
         } else if (fam6) {
             if (parsed) {
-                if (l4_needed) {
-                    if (!tx && (p.flags & F_REFD) && (proto == 6u || proto == 17u)) {
+                if (post == PV_FRAG) {
+                    verdict = V_FRAG;                // pico_ipv6_process_frag (pico_ipv6.c:791-795)
+                } else if (l4_needed) {
+                    if (!tx && !(p.flags & F_NXD) && (proto == 6u || proto == 17u)) {
                         // pico_socket.c:1919-1958 with net_hdr->proto = byte 9 of the IPv6 header
                         if (ipcrc == 6u || (ipcrc == 17u && acc_x != 0u)) {
                             l4 = finalize(pseudo - (proto << 8) + (ipcrc << 8) + acc_all);
@@ -388,11 +214,19 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
             if (MODE == 3) verdict |= V_IPV6;
         } else {
             if (parsed) {
+                // pico_ipv4_process_in's order (pico_ipv4.c:420-455): the header check, then the
+                // discards decided in phase 1 (source, evil bit, IHL < 5), then the fragment
+                // hand-off; TX: a fragment gets its header checksum only
                 const uint32_t acc_hdr = hdr20 + acc_opt;
                 net = finalize(acc_hdr - (tx ? ipcrc : 0u));
-                if (!tx && net != 0) verdict |= V_NET_BAD;
                 const uint32_t tsum = acc_all - acc_hdr;
-                if (l4_needed) {
+                if (!tx && net != 0) {
+                    verdict = V_NET_BAD;
+                } else if (post == PV_DROP) {
+                    verdict = V_MALFORMED;
+                } else if (post == PV_FRAG) {
+                    verdict = V_FRAG;
+                } else if (l4_needed) {
                     if (!tx) {
                         if (proto == 6u || acc_x != 0u) {
                             l4 = finalize(pseudo + tsum);
@@ -406,10 +240,14 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
                 }
                 if (verdict == 0) verdict = V_ACCEPT;
             }
-            if (tx && (p.flags & 0x401u) == 1u && verdict == V_ACCEPT) {   // 0x400: ablation
-                store_crc(fp + 10, net);
-                if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
-                else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+            if (tx && (p.flags & 1u) && !ABLATE(p, 0x400u)) {
+                if (verdict == V_ACCEPT) {
+                    store_crc(fp + 10, net);
+                    if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
+                    else if (proto == 17u && tl >= 8u) store_crc(fp + hl + 6u, 0u);
+                } else if (verdict == V_FRAG) {
+                    store_crc(fp + 10, net);
+                }
             }
         }
         if (MODE != 2 && p.out_net) p.out_net[idx] = (uint16_t)net;
@@ -444,12 +282,156 @@ __device__ __forceinline__ void window_words(const uint4 (&hw)[HW], uint32_t pos
     for (int m = 0; m < NW; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
 }
 
+// ---------------------------------------------------------------- IPv6 extension headers
+//
+// pico_ipv6_extension_headers (modules/pico_ipv6.c:707-809) with the sequence check before it
+// (pico_ipv6_check_headers_sequence, :659-694), for an RX datagram whose descriptor carries no
+// seed and whose next header is not TCP / UDP / ICMPv6 -- rare traffic: one lane walks its own
+// datagram with byte loads (L2 hits: the head window was just fetched), the rest of the wave
+// idles.  Reads stay inside avail; where the reference would read past its buffer, or loop
+// forever (a zero-length step: (uint8)((len + 1) << 3) wraps for len >= 31, an option length
+// of 254), or let its uint16 f->net_len wrap, the datagram is WALK_BAD (MALFORMED).
+//   WALK_DROP   the reference discards it (invalid / misplaced header, an option or routing
+//               type that discards, M with a payload length not a multiple of 8, ESP / AUTH /
+//               no next header)
+//   WALK_PROTO  the transport is reached: net_len, proto
+//   WALK_FRAG   the transport is reached behind a fragment header: pico_ipv6_process_frag
+constexpr int WALK_BAD = -1, WALK_DROP = 0, WALK_PROTO = 1, WALK_FRAG = 2;
+
+#define WBYTE(k, dst)                          \
+    do {                                       \
+        if ((uint32_t)(k) >= avail) return -2; \
+        (dst) = h[(uint32_t)(k)];              \
+    } while (0)
+
+// pico_ipv6_process_hopbyhop (:525-582): must_align 1 / 0, -1 discard, -2 bad
+__device__ __noinline__ int walk_hbh(const uint8_t* __restrict__ h, uint32_t avail, uint32_t e) {
+    uint32_t b1, type, olen;
+    WBYTE(e + 1, b1);
+    uint32_t len = (((b1 + 1u) << 3) - 2u) & 0xFFu, opt = e + 2u;
+    int must_align = 1;
+    while (len) {
+        WBYTE(opt, type);
+        if (type == 0u) { ++opt; --len; continue; }                 // Pad1
+        WBYTE(opt + 1u, olen);
+        const uint32_t optlen = (olen + 2u) & 0xFFu;
+        if (type == 5u) { if (olen == 2u) must_align = 0; }         // router alert (MLD)
+        else if (type != 1u && (type & 0xC0u) != 0u) return -1;     // action: discard
+        if (optlen == 0u) return -2;                                // the reference loops forever
+        opt += optlen;
+        len = (len - optlen) & 0xFFu;
+    }
+    return must_align;
+}
+
+// pico_ipv6_process_destopt (:610-657): 0 pass, -1 discard, -2 bad; every option advances opt[1] + 2
+__device__ __noinline__ int walk_dst(const uint8_t* __restrict__ h, uint32_t avail, uint32_t e) {
+    uint32_t b1, type, olen;
+    WBYTE(e + 1, b1);
+    uint32_t len = (((b1 + 1u) << 3) - 2u) & 0xFFu, opt = e + 2u;
+    while (len) {
+        WBYTE(opt, type);
+        WBYTE(opt + 1u, olen);
+        const uint32_t optlen = (olen + 2u) & 0xFFu;
+        if (type != 0u && type != 1u && type != 201u && (type & 0xC0u) != 0u) return -1;
+        if (optlen == 0u) return -2;
+        opt += optlen;
+        len = (len - optlen) & 0xFFu;
+    }
+    return 0;
+}
+#undef WBYTE
+
+#define WBYTE(k, dst)                                \
+    do {                                             \
+        if ((uint32_t)(k) >= avail) return WALK_BAD; \
+        (dst) = h[(uint32_t)(k)];                    \
+    } while (0)
+
+__device__ __noinline__ __attribute__((unused)) int ipv6_walk(const uint8_t* __restrict__ h, uint32_t avail, uint32_t& net_len_out,
+                                      uint32_t& proto_out) {
+    const uint32_t plen = ((uint32_t)h[4] << 8) | h[5];
+    uint32_t nx = h[6], b, ptr = 40u;
+    // sequence check: steps of (uint8)((len + 1) << 3) (0 when len >= 31: the next step reads
+    // the same header again), 8 for a fragment header; at most 2 steps per 8 bytes of avail
+    for (uint32_t it = 0;; ++it) {
+        if (it > 2u * (avail >> 3) + 8u) return WALK_BAD;
+        uint32_t optlen;
+        if (nx == 0u || nx == 43u || nx == 60u || nx == 50u || nx == 51u) {
+            WBYTE(ptr + 1u, b);
+            optlen = ((b + 1u) << 3) & 0xFFu;
+        } else if (nx == 44u) {
+            optlen = 8u;
+        } else if (nx == 59u || nx == 6u || nx == 17u || nx == 58u) {
+            break;
+        } else {
+            return WALK_DROP;
+        }
+        WBYTE(ptr, nx);
+        ptr += optlen;
+    }
+    // the walk: f->net_len (uint16) moves by >= 8 bytes a step
+    uint32_t net_len = 40u, cur_nexthdr = 6u;
+    bool must_align = false, frag = false;
+    nx = h[6];
+    ptr = 40u;
+    for (;;) {
+        const uint32_t e = net_len;
+        uint32_t cur_optlen;
+        if (nx == 6u || nx == 17u || nx == 58u) {
+            if (must_align && (plen & 7u) != 0u) return WALK_DROP;
+            net_len_out = net_len;
+            proto_out = nx;
+            return frag ? WALK_FRAG : WALK_PROTO;
+        } else if (nx == 0u) {                                      // hop-by-hop: only first
+            if (cur_nexthdr != 6u) return WALK_DROP;
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            const int r = walk_hbh(h, avail, e);
+            if (r == -2) return WALK_BAD;
+            if (r < 0) return WALK_DROP;
+            must_align = r != 0;
+        } else if (nx == 43u) {                                     // routing
+            uint32_t segleft, type;
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            WBYTE(e + 3u, segleft);
+            if (segleft != 0u) {
+                WBYTE(e + 2u, type);
+                if (type != 2u) return WALK_DROP;
+            }
+        } else if (nx == 44u) {                                     // fragment
+            uint32_t om1;
+            cur_optlen = 8u;
+            WBYTE(e + 3u, om1);
+            if (e + 2u >= avail) return WALK_BAD;                   // om[0] is read too
+            frag = true;
+            if ((om1 & 1u) && (plen & 7u) != 0u) return WALK_DROP;
+        } else if (nx == 60u) {                                     // destination options
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            must_align = true;
+            const int r = walk_dst(h, avail, e);
+            if (r == -2) return WALK_BAD;
+            if (r < 0) return WALK_DROP;
+        } else {                                                    // ESP, AUTH, none, invalid
+            return WALK_DROP;
+        }
+        if (net_len + cur_optlen > 0xFFFFu) return WALK_BAD;        // the uint16 would wrap
+        net_len += cur_optlen;
+        WBYTE(e, nx);                                               // exthdr->nxthdr (:805)
+        cur_nexthdr = ptr;
+        ptr += cur_optlen;
+    }
+}
+#undef WBYTE
+
 // CPL 8 keeps 8 KiB of loads in flight per wave within 128 VGPRs (4 waves per
 // SIMD: a 256K-frame batch at 64 frames per wave is one residency round); CPL 4
 // fits 64 VGPRs (8 waves per SIMD).
-template <int MODE, bool NT, int CPL, bool SMALL, bool STREAM>
-__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, StreamSmem<STREAM, MODE == 0>& SS,
-                                             uint32_t lane, uint64_t f0) {
+template <int MODE, bool NT, int CPL, bool SMALL>
+__device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L, uint4* stage, uint32_t lane,
+                                             uint64_t f0) {
     constexpr bool IPV4 = MODE == 1, IPV6 = MODE == 2, ETH = MODE == 3;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = MODE != 0 && (p.flags & 2u) != 0;
@@ -466,18 +448,10 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(fp) & 15u);
     uint64_t a0off = off - r;
     uint32_t odd = r & 1u;
-    const uint32_t r_desc = r;                   // the descriptor's start in its head window
-
-    // dense waves: the span stream (phase 1 then parses from the rows it filled; no rounds)
-    bool dense = false;
-    uint32_t total = 0;
-    if constexpr (STREAM) {
-        dense = wave_dense<MODE>(p, lane, cnt, oob, off, len, seed);
-        if (dense) total = span_stream<MODE>(p, SS.s, stage, lane, cnt, off, len);
-    }
 
     uint32_t span = 0, ext = 0, xpos = NONE, optend = 0;
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, l2v = 0;
+    uint32_t post = 0;                           // PV_DROP / PV_FRAG (sorted_finish applies them)
     bool parsed = false, l4_needed = false, is6 = false;
     const uint64_t a0h = a0off;                  // the head window's first chunk (fused modes)
     uint4 hw[HW];
@@ -494,13 +468,8 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         // (64-byte IMIX frames), the whole datagram: their sums are taken here and the
         // rounds start behind the window (or are skipped).
         constexpr uint32_t HDR = IPV6 ? 40u : IPV4 ? 20u : 14u;
-        nlh = len >= HDR && !(p.flags & 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;   // 0x200: ablation
-        if (STREAM && dense) {
-#pragma unroll
-            for (uint32_t i = 0; i < HW; ++i) hw[i] = stage[lane * HW + (i ^ (lane & (HW - 1)))];
-            staged = true;
-            asm volatile("" ::: "memory");
-        } else {
+        nlh = len >= HDR && !ABLATE(p, 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;
+        {
             // Buffer loads through a window over the batch (from base's 16-byte line to
             // base_len rounded up -- the bytes load_chunk may touch -- at most 2 GiB, from
             // 1 GiB below the wave's first frame): all HW slots issue back to back and
@@ -608,11 +577,22 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                     pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) +
                              (proto << 8) + (((tl & 0xFFu) << 8) | (tl >> 8));
                     if (hl > 20u) optend = r + hl;
-                    if (!tx) {
+                    // after the header check (sorted_finish): pico_ipv4_is_valid_src (:425-428,
+                    // :187-229 -- 255.255.255.255, 224-254.x.x.x, 127/8 from a device that is not
+                    // "loop"), the evil bit (:431-435), IHL < 5 (:438-443): discarded; MF or an
+                    // offset (:446-455): handed to reassembly.  Then only the header is summed.
+                    const uint32_t frag = ((H[1] >> 8) & 0xFF00u) | (H[1] >> 24);
+                    const uint32_t s0 = H[3] & 0xFFu;
+                    const bool bad_src = H[3] == 0xFFFFFFFFu || (s0 != 0xFFu && (s0 & 0xE0u) == 0xE0u) || s0 == 0x7Fu;
+                    if (!tx && (bad_src || (frag & 0x8000u) || ihl < 5u)) post = PV_DROP;
+                    else if (frag & 0x3FFFu) post = PV_FRAG;
+                    if (post) {
+                        span = ext = hl;
+                    } else if (!tx) {
                         if (proto == 6u) {
                             l4_needed = true;
-                        } else if (proto == 17u) {
-                            if (hl + 8u > avail) verdict |= V_MALFORMED;
+                        } else if (proto == 17u) {     // the UDP crc field lies past the frame: MALFORMED
+                            if (hl + 8u > avail) { post = PV_DROP; span = ext = hl; }
                             else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
                         }
                     } else {
@@ -633,9 +613,23 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                 const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
                 uint32_t net_len = seed & 0xFFFFu;
                 proto = (seed >> 16) & 0xFFu;
-                if (seed == 0) { net_len = 40u; proto = (H[1] >> 16) & 0xFFu; }
+                bool walked = true;
+                if (seed == 0) {
+                    net_len = 40u;
+                    proto = (H[1] >> 16) & 0xFFu;
+                    // RX with extension headers and no seed: walk them here, as
+                    // pico_ipv6_extension_headers does (ipv6_walk)
+                    if (!tx && proto != 6u && proto != 17u && proto != 58u) {
+                        const int k = ipv6_walk(p.base + off, avail, net_len, proto);
+                        if (k == WALK_FRAG) post = PV_FRAG;
+                        else walked = k == WALK_PROTO;
+                    }
+                }
                 tl = (plen - (net_len - 40u)) & 0xFFFFu;                // pico_ipv6.c:790
-                if (net_len >= 40u && net_len <= avail && net_len + tl <= avail) {
+                if (post == PV_FRAG) {
+                    parsed = true;                   // handed to reassembly: nothing to sum
+                    verdict = 0;
+                } else if (walked && net_len >= 40u && net_len <= avail && net_len + tl <= avail) {
                     uint32_t addr = 0, xrel = NONE;
 #pragma unroll
                     for (int m = 2; m < 10; ++m) addr = dot2_add(H[m], addr);
@@ -644,9 +638,9 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                     verdict = 0;
                     ext = tl;
                     if (!tx) {
-                        // F_REF_DISPATCH: pico_transport_crc_check's proto is byte 9 (kept in ipcrc)
+                        // pico_transport_crc_check's proto is byte 9 (kept in ipcrc) unless F_NXD
                         ipcrc = (H[2] >> 8) & 0xFFu;
-                        const bool ref17 = (p.flags & F_REFD) && ipcrc == 17u;
+                        const bool ref17 = !(p.flags & F_NXD) && ipcrc == 17u;
                         if (proto == 6u && !ref17) {
                             l4_needed = true;
                         } else if (proto == 17u || proto == 6u) {   // the UDP crc field is read
@@ -681,61 +675,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     }
     const uint64_t nch64 = ext ? ((uint64_t)r + ext + 15u) >> 4 : 0u;
     uint32_t nch = (uint32_t)min(nch64, (uint64_t)0xFFFFFFFFu);
-    if constexpr (STREAM && MODE == 0) {
-        if (dense) {
-            p_all = total;
-            if (xpos != NONE) {                  // the crc field's word (crc_off even: frame pairing)
-                const uint8_t* q = p.base + a0off + xpos;
-                p_x = (uint32_t)q[0] | ((uint32_t)q[1] << 8);
-            }
-            nch = 0;
-        }
-    }
-    if constexpr (STREAM && MODE != 0) {
-        if (dense) {
-            // window coordinates (origin a0h): the descriptor's bytes [r_desc, r_desc + len), the
-            // region [rs, rs + span); region = total - the bytes before it - the bytes after it
-            // (even offsets apart: one pairing throughout)
-            const uint32_t d = (uint32_t)((a0off - a0h) >> 4);
-            const uint32_t rs = 16u * d + r, sl = odd ? SEL_ODD : SEL_EVEN;
-            const uint32_t e0 = r_desc + len;
-            auto range_sum = [&](uint32_t x0, uint32_t x1) {
-                uint32_t acc = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < HW; ++i)
-                    if (x1 > x0 && 16u * i < x1 && 16u * i + 16u > x0) acc += masked_chunk_sum<true>(hw[i], 16u * i, x0, x1, sl);
-                if (x1 > x0 && x1 > 16u * HW)
-                    for (uint32_t k = max(HW, x0 >> 4); 16u * k < x1; ++k)
-                        acc += masked_chunk_sum<true>(load_chunk(p.base + a0h, k), 16u * k, x0, x1, sl);
-                return acc;
-            };
-            const bool cut = parsed && (rs > r_desc || rs + span < e0);
-            uint32_t c = 0;
-            if (__builtin_amdgcn_ballot_w64(cut)) {
-                if (cut) c = range_sum(r_desc, rs) + range_sum(rs + span, e0);
-            }
-            p_all = total - c;
-            if (xpos != NONE) {
-                const uint32_t xs = 16u * d + xpos;
-                if (xs + 2u <= 16u * HW) {
-                    const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
-                    const uint32_t sw = (lane & (HW - 1)) << 4;
-                    p_x = (uint32_t)row[xs ^ sw] | ((uint32_t)row[(xs + 1u) ^ sw] << 8);
-                } else {
-                    const uint8_t* q = p.base + a0h + xs;
-                    p_x = (uint32_t)q[0] | ((uint32_t)q[1] << 8);
-                }
-            }
-            if (__builtin_amdgcn_ballot_w64(optend != 0u)) {      // IPv4 options (always inside the window)
-                if (optend != 0u) p_opt = range_sum(rs + 20u, 16u * d + optend);
-            }
-            asm volatile("" ::: "memory");
-            xpos = NONE;
-            optend = 0;
-            nch = 0;
-        }
-    }
-    if (MODE != 0 && !(STREAM && dense)) {
+    if (MODE != 0) {
         // sums over the head window: the region's chunks [0, k0) = window chunks
         // [d, d + k0) (d: where the region's chunk grid starts in the window -- IPv6:
         // behind the header); the rounds take region chunks [k0, nch).  A field
@@ -819,7 +759,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     L.nch[lane] = nch;
     L.info[lane] = make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), r + span, r | (odd << 4) | (k0 << 5));
     L.xo[lane] = make_uint2(xpos, optend);
-    L.fin[lane] = make_uint4(verdict | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
+    L.fin[lane] = make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
                                  (is6 ? 128u : 0u) | (proto << 8) | (tl << 16),
                              hl | (l2v << 8) | (ipcrc << 16), MODE == 0 ? seed : pseudo, hdr20);
     const bool any_odd = __builtin_amdgcn_ballot_w64(nch != 0 && odd) != 0;
@@ -856,10 +796,10 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
     // ---- 3. rounds over the sorted frames
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
-    // ablation only (PICO_CSUM_ABLATE): flags bit 8 skips the rounds (times phases 1, 2, 4);
-    // bit 9 skips the head-window loads (then nothing parses: descriptors + stores alone);
-    // bit 10 skips the IPv4 TX in-place crc writes
-    if (m && !(p.flags & 0x100u)) {
+    // measurement builds only (ABLATE, -DPICO_CSUM_AB): bit 8 skips the rounds (times phases 1,
+    // 2, 4); bit 9 skips the head-window loads (then nothing parses: descriptors + stores
+    // alone); bit 10 skips the IPv4 TX in-place crc writes
+    if (m && !ABLATE(p, 0x100u)) {
         if (any_odd) {
             if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
             else sorted_rounds<CPL, true, NT, false, SMALL>(ra, L, e, m);
@@ -882,15 +822,16 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 #ifndef PICO_SORTED_WPB
 #define PICO_SORTED_WPB 4    // waves per workgroup (A/B builds: 8)
 #endif
-template <int MODE, bool NT, int CPL, bool SMALL = false, bool STREAM = false>
-__global__ __launch_bounds__(64 * PICO_SORTED_WPB, CPL >= 8 || MODE != 0 ? 4 : 5) void csum_sorted_kernel(FlatArgs p) {
+// The product shape (measured): 8 chunks per lane per round, the 1-lane class for
+// frames of <= 8 chunks, non-temporal loads in the >= 16-lane rounds; 4 waves per SIMD.
+template <int MODE, bool NT = true, int CPL = 8, bool SMALL = true>
+__global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveSmem<MODE != 0> lds_all[PICO_SORTED_WPB];
-    __shared__ StreamSmem<STREAM, MODE == 0> lds_stream[PICO_SORTED_WPB];
     const uint32_t lane = threadIdx.x & 63u;
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
     STAMP(0);
-    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL, STREAM>(p, S.s, S.stage, lds_stream[threadIdx.x >> 6], lane, f0);
+    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
     STAMP(3);
 }
 
@@ -966,48 +907,37 @@ int pico_csum_diag_set_stamps(void* d_buf, uint32_t waves) {
 #endif
 #endif
 
-// One kernel table per mode: this TU is compiled once per SORTED_MODE (parallel build).
+// One kernel per mode: this TU is compiled once per SORTED_MODE (parallel build).
 #define SORTED_LAUNCH SORTED_CAT(pico_csum_sorted_launch_mode, SORTED_MODE)
-int SORTED_LAUNCH(const void* args, uint32_t nt, int v, void* stream);
-int SORTED_LAUNCH(const void* args, uint32_t nt, int v, void* stream) {
+int SORTED_LAUNCH(const void* args, void* stream);
+int SORTED_LAUNCH(const void* args, void* stream) {
     const FlatArgs& a = *static_cast<const FlatArgs*>(args);
-    using K = void (*)(FlatArgs);
-    constexpr int M = SORTED_MODE;
-    // [nt][cpl 4 | cpl 8 | cpl 8 + 1-lane | cpl 8 + 1-lane + span stream]
-#define SK(t) {csum_sorted_kernel<M, t, 4>, csum_sorted_kernel<M, t, 8>, csum_sorted_kernel<M, t, 8, true>,       \
-               csum_sorted_kernel<M, t, 8, true, true>}
-    static const K table[2][4] = {SK(false), SK(true)};
-#undef SK
     const uint64_t waves = ((uint64_t)a.n + a.fpw - 1) / a.fpw;
-    hipLaunchKernelGGL(table[nt ? 1 : 0][v], dim3((unsigned)((waves + PICO_SORTED_WPB - 1) / PICO_SORTED_WPB)),
+    hipLaunchKernelGGL(csum_sorted_kernel<SORTED_MODE>, dim3((unsigned)((waves + PICO_SORTED_WPB - 1) / PICO_SORTED_WPB)),
                        dim3(64 * PICO_SORTED_WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
 
 #if SORTED_MODE == 0
-int pico_csum_sorted_launch_mode1(const void* args, uint32_t nt, int v, void* stream);
-int pico_csum_sorted_launch_mode2(const void* args, uint32_t nt, int v, void* stream);
-int pico_csum_sorted_launch_mode3(const void* args, uint32_t nt, int v, void* stream);
+int pico_csum_sorted_launch_mode1(const void* args, void* stream);
+int pico_csum_sorted_launch_mode2(const void* args, void* stream);
+int pico_csum_sorted_launch_mode3(const void* args, void* stream);
 
 // Sorted-rounds descriptor kernel: mode 0 RAW, 1 fused IPv4, 2 fused IPv6, 3 Ethernet front end;
-// small (cpl 8 only): 0 none, 1 the 1-lane class, 2 the 1-lane class + the span stream for dense waves.
-// mac48 = the device MAC's 6 bytes (little-endian in a uint64), used when flags carry F_MACF
-// (set by the host layer).
+// fpw frames per wave (1..64).  mac48 = the device MAC's 6 bytes (little-endian in a uint64),
+// used when flags carry F_MACF (set by the host layer).
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t cpl, uint32_t nt, uint32_t fpw, uint32_t small,
-                            uint64_t mac48, void* stream) {
-    if (fpw < 1 || fpw > 64 || !(cpl == 4 || cpl == 8) || mode < 0 || mode > 3 || small > 2 || (small && cpl != 8))
-        return (int)hipErrorInvalidValue;
+                            uint8_t* verdict, uint32_t fpw, uint64_t mac48, void* stream) {
+    if (fpw < 1 || fpw > 64 || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32)};
-    const int v = cpl == 4 ? 0 : (int)small + 1;
     switch (mode) {
-        case 0: return pico_csum_sorted_launch_mode0(&a, nt, v, stream);
-        case 1: return pico_csum_sorted_launch_mode1(&a, nt, v, stream);
-        case 2: return pico_csum_sorted_launch_mode2(&a, nt, v, stream);
-        default: return pico_csum_sorted_launch_mode3(&a, nt, v, stream);
+        case 0: return pico_csum_sorted_launch_mode0(&a, stream);
+        case 1: return pico_csum_sorted_launch_mode1(&a, stream);
+        case 2: return pico_csum_sorted_launch_mode2(&a, stream);
+        default: return pico_csum_sorted_launch_mode3(&a, stream);
     }
 }
 

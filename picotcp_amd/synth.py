@@ -47,10 +47,13 @@ def imix_lengths(n: int, seed: int, mix=SIMPLE_IMIX) -> np.ndarray:
     return lens[perm]
 
 
-def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = True, ihl: int = 5):
+def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = True, ihl: int = 5,
+               frag=None):
     """IPv4 datagrams of the given total lengths, packed back to back, each with a
     valid header (vhl = 0x40|ihl, len, ttl 64, proto, random id/addresses/ports/payload)
-    and a transport header (TCP 20 B, UDP 8 B, ICMP 8 B).  Every crc field is zero:
+    and a transport header (TCP 20 B, UDP 8 B, ICMP 8 B).  frag = the flags / offset field
+    (host order) of every datagram, or an array cycled over them; default DF (0x4000).
+    Every crc field is zero:
     make them valid with the TX kernel (PICO_CSUM_F_TX | F_WRITE) or a host checker.
     eth=True puts a 14-byte Ethernet header in front of each datagram (pico_ethernet.c:183),
     so the IPv4 headers are 2-byte aligned as in the reference RX path.
@@ -81,7 +84,11 @@ def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = T
     put(2, (lengths >> 8).astype(np.uint8))
     put(3, (lengths & 0xFF).astype(np.uint8))
     put(4, rnd[:, 0]); put(5, rnd[:, 1])
-    put(6, 0x40); put(7, 0)
+    if frag is None:
+        put(6, 0x40); put(7, 0)
+    else:
+        fr = np.resize(np.asarray(frag, dtype=np.uint16), n) if n else np.zeros(0, np.uint16)
+        put(6, (fr >> 8).astype(np.uint8)); put(7, (fr & 0xFF).astype(np.uint8))
     put(8, 64)
     put(9, np.uint8(proto))
     put(10, 0); put(11, 0)
@@ -112,12 +119,15 @@ def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = T
 
 
 def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = True, hbh: bool = False,
-               icmp_type: int = 128):
-    """IPv6 datagrams of the given total lengths (40-byte header + optional 8-byte
-    hop-by-hop header + transport), packed back to back, crc fields zero.  proto
-    6 / 17 / 58 (ICMPv6 of `icmp_type`).  Returns (buffer, net offsets, available
-    bytes, descriptor seeds): seed = net_len | proto << 16 when a hop-by-hop header
-    is present (what pico_ipv6_extension_headers leaves in the frame), else 0."""
+               icmp_type: int = 128, frag=None, destopt: bool = False, walked: bool = False):
+    """IPv6 datagrams of the given total lengths (40-byte header + optional 8-byte extension
+    headers + transport), packed back to back, crc fields zero.  proto 6 / 17 / 58 (ICMPv6 of
+    `icmp_type`).  Extension headers, in RFC 8200 order: hop-by-hop (PadN) when `hbh`, a
+    destination-options header (PadN) when `destopt`, a fragment header carrying `frag` (the
+    offset / M field, host order; scalar or an array cycled over the datagrams) when frag is not
+    None.  Returns (buffer, net offsets, available bytes, descriptor seeds): seed =
+    net_len | proto << 16 when extension headers are present and not `walked` (what
+    pico_ipv6_extension_headers leaves in the frame), else 0 (the kernel walks them)."""
     lengths = np.asarray(lengths, dtype=np.uint32)
     n = lengths.size
     pre = 14 if eth else 0
@@ -128,24 +138,33 @@ def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = T
     buf = random_bytes(seed, int(frame_len.sum()))
     net = starts + np.uint64(pre)
     idx = net.astype(np.int64)
-    net_len = 48 if hbh else 40
+    chain = (["hbh"] if hbh else []) + (["dst"] if destopt else []) + (["frag"] if frag is not None else [])
+    net_len = 40 + 8 * len(chain)
     plen = (lengths - 40).astype(np.uint32)
     if eth:
         e = starts.astype(np.int64)
         buf[e + 12] = 0x86
         buf[e + 13] = 0xDD
+    code = {"hbh": 0, "dst": 60, "frag": 44}
     buf[idx + 0] = 0x60
     buf[idx + 4] = (plen >> 8).astype(np.uint8)
     buf[idx + 5] = (plen & 0xFF).astype(np.uint8)
-    buf[idx + 6] = 0 if hbh else proto
+    buf[idx + 6] = code[chain[0]] if chain else proto
     buf[idx + 7] = 255 if proto == 58 else 64
-    if hbh:
-        buf[idx + 40] = proto        # next header
-        buf[idx + 41] = 0            # length: 8 bytes
-        buf[idx + 42] = 1            # PadN
-        buf[idx + 43] = 4
-        for o in range(44, 48):
-            buf[idx + o] = 0
+    for k, c in enumerate(chain):
+        o = idx + 40 + 8 * k
+        buf[o] = code[chain[k + 1]] if k + 1 < len(chain) else proto   # next header
+        if c == "frag":
+            fr = np.resize(np.asarray(frag, dtype=np.uint16), n) if n else np.zeros(0, np.uint16)
+            buf[o + 1] = 0
+            buf[o + 2] = (fr >> 8).astype(np.uint8)
+            buf[o + 3] = (fr & 0xFF).astype(np.uint8)
+        else:
+            buf[o + 1] = 0            # length: 8 bytes
+            buf[o + 2] = 1            # PadN
+            buf[o + 3] = 4
+            for q in range(4, 8):
+                buf[o + q] = 0
     t = idx + net_len
     if proto == 6:
         buf[t + 12] = 0x50
@@ -163,12 +182,13 @@ def ipv6_batch(lengths: np.ndarray, seed: int = 3, proto: int = 6, eth: bool = T
         buf[t + 1] = 0
         buf[t + 2] = 0
         buf[t + 3] = 0
-    seeds = np.full(n, (net_len | (proto << 16)) if hbh else 0, dtype=np.uint32)
+    seeds = np.full(n, (net_len | (proto << 16)) if chain and not walked else 0, dtype=np.uint32)
     return buf, net, lengths.copy(), seeds
 
 
 ETH_KINDS = ("ipv4_tcp", "ipv4_udp", "ipv4_icmp", "ipv6_tcp", "ipv6_udp", "ipv6_icmp", "ipv6_hbh_tcp", "arp",
-             "lldp", "ipv4_bad_version", "ipv4_opt_tcp", "ipv4_opt_udp")
+             "lldp", "ipv4_bad_version", "ipv4_opt_tcp", "ipv4_opt_udp", "ipv4_frag", "ipv4_evil", "ipv6_frag",
+             "ipv6_dst_tcp")
 
 
 def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")):
@@ -177,9 +197,11 @@ def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")
     IMIX sizes, ARP, an unknown ethertype, an IPv4 ethertype carrying version 6), in seeded
     order with 0-3 byte gaps (every alignment), and destination MACs drawn from {mac,
     broadcast, 01:00:5e IPv4 multicast, 33:33 IPv6 multicast, a foreign unicast}.  Transport
-    crc fields are zero (TX input).  Returns (buffer, frame offsets uint64, frame bytes
-    uint32, descriptor seeds uint32 (IPv6 net_len | proto << 16 behind a hop-by-hop header,
-    else 0), kind index uint8 into ETH_KINDS)."""
+    crc fields are zero (TX input).  IPv4 fragments (first / middle / last) and evil-bit
+    datagrams, IPv6 datagrams behind a fragment or a destination-options header left for the
+    kernel to walk (seed 0).  Returns (buffer, frame offsets uint64, frame bytes uint32,
+    descriptor seeds uint32 (IPv6 net_len | proto << 16 behind a hop-by-hop header, else 0),
+    kind index uint8 into ETH_KINDS)."""
     rng = np.random.default_rng(seed)
     kind = rng.integers(0, len(ETH_KINDS), n).astype(np.uint8)
     frames, seeds = [], np.zeros(n, dtype=np.uint32)
@@ -189,17 +211,26 @@ def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")
         s = seed * 7919 + i
         if k.startswith("ipv4"):
             proto = {"ipv4_tcp": 6, "ipv4_udp": 17, "ipv4_icmp": 1, "ipv4_bad_version": 6, "ipv4_opt_tcp": 6,
-                     "ipv4_opt_udp": 17}[k]
+                     "ipv4_opt_udp": 17, "ipv4_frag": 6, "ipv4_evil": 17}[k]
             ihl = int(rng.integers(6, 16)) if "opt" in k else 5
+            fr = None
+            if k == "ipv4_frag":       # first / middle / last fragments
+                fr = int(rng.choice([0x2000, 0x2000 | int(rng.integers(1, 0x1FFF)), int(rng.integers(1, 0x1FFF))]))
+            elif k == "ipv4_evil":
+                fr = 0x8000 | 0x4000
             b, _, _ = ipv4_batch(np.array([max(int(lens[i]), 4 * ihl + 28)], np.uint32), seed=s, proto=proto, eth=True,
-                                 ihl=ihl)
+                                 ihl=ihl, frag=fr)
             if k == "ipv4_bad_version":
                 b[14] = 0x65
         elif k.startswith("ipv6"):
-            proto = 6 if "tcp" in k else 17 if "udp" in k else 58
+            proto = 6 if ("tcp" in k or k == "ipv6_frag") else 17 if "udp" in k else 58
+            fr = (int(rng.integers(0, 200)) << 3) | int(rng.integers(0, 2)) if k == "ipv6_frag" else None
             b, _, _, sd = ipv6_batch(np.array([max(int(lens[i]) + 20, 68)], np.uint32), seed=s, proto=proto,
-                                     eth=True, hbh="hbh" in k, icmp_type=int(rng.choice([128, 129, 135, 136, 143])))
+                                     eth=True, hbh="hbh" in k, icmp_type=int(rng.choice([128, 129, 135, 136, 143])),
+                                     frag=fr, destopt=k == "ipv6_dst_tcp", walked=k in ("ipv6_frag", "ipv6_dst_tcp"))
             seeds[i] = sd[0]
+            if proto != 58 and rng.random() < 0.6:
+                b[14 + 9] = proto        # the byte pico_transport_crc_check dispatches on (pico_socket.c:1923)
         elif k == "arp":
             b = random_bytes(s, 60)
             b[12], b[13] = 0x08, 0x06

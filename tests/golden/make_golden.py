@@ -8,7 +8,7 @@ pico_checksum / pico_dualbuffer_checksum, compiled unmodified from
 /root/reference/stack/pico_frame.c into oracle/_ref/libpicoref.so.  The
 IPv4 batch expectations additionally restate, in Python and independently
 of oracle/pico_csum_oracle.c, the caller logic of
-  pico_ipv4_process_in   modules/pico_ipv4.c:381-420
+  pico_ipv4_process_in   modules/pico_ipv4.c:381-456 (lengths, source, evil bit, IHL, fragments)
   pico_ipv4_crc_check    modules/pico_ipv4.c:243-257
   pico_transport_crc_check stack/pico_socket.c:1916-1968
   pico_tcp_checksum_ipv4 modules/pico_tcp.c:422-446 / pico_udp_checksum_ipv4 pico_udp.c:36-60
@@ -178,9 +178,11 @@ def raw_cases() -> dict:
 # --- IPv4 caller logic (independent Python restatement) ----------------------
 
 def ipv4_expect(buf: np.ndarray, off: int, avail: int, tx: bool):
-    """(out_net, out_l4, verdict, writes) for one datagram; see module doc."""
+    """(out_net, out_l4, verdict) for one datagram: the reference's first discard reason in
+    pico_ipv4_process_in's order (lengths, header crc, source, evil bit, IHL < 5, fragment
+    hand-off), then pico_transport_crc_check; see oracle_batch_ipv4 / include/pico_csum.h."""
     ref, refd = O.ref_checksum, O.ref_dualbuffer_checksum
-    MAL, NET, L4, ACC = 8, 2, 4, 1
+    MAL, NET, L4, ACC, FRAG = 8, 2, 4, 1, 16
     h = buf[off:off + avail].tobytes()
     if avail < 20:
         return 0, 0, MAL
@@ -188,56 +190,77 @@ def ipv4_expect(buf: np.ndarray, off: int, avail: int, tx: bool):
     opt = 4 * ((vhl & 0x0F) - 5) if (vhl & 0x0F) > 5 else 0
     net_len = 20 + opt
     tot = (h[2] << 8) | h[3]
-    tl = (tot - 20 - opt) & 0xFFFF                 # (uint16_t) cast, pico_ipv4.c:395
+    frag = (h[6] << 8) | h[7]
+    tl = (tot - 20 - opt) & 0xFFFF                 # (uint16_t) cast, pico_ipv4.c:399
     max_allowed = (avail - 20) & 0xFFFF            # pico_ipv4.c:386
     if net_len > avail or (not tx and tl > max_allowed) or net_len + tl > avail:
         return 0, 0, MAL
     proto = h[9]
     hdr = bytearray(h[:net_len])
     t = bytearray(h[net_len:net_len + tl])
-    v = 0
     l4 = 0
     if tx:
         hdr[10:12] = b"\0\0"
     net = ref(bytes(hdr))
-    if not tx and net != 0:
-        v |= NET
     ps = pseudo(bytes(hdr[12:16]), bytes(hdr[16:20]), proto, tl)
     if not tx:
+        if net != 0:
+            return net, 0, NET                                        # pico_ipv4.c:420-422
+        if h[12:16] == b"\xff" * 4 or (h[12] != 0xFF and (h[12] & 0xE0) == 0xE0) or h[12] == 0x7F:
+            return net, 0, MAL                                        # :425-428 (source)
+        if frag & 0x8000 or (vhl & 0x0F) < 5:
+            return net, 0, MAL                                        # :431-443
+        if frag & 0x3FFF:
+            return net, 0, FRAG                                       # :446-455
         if proto == 6:
             l4 = refd(ps, bytes(t))
-            if l4:
-                v |= L4
-        elif proto == 17:
+            return net, l4, (L4 if l4 else ACC)
+        if proto == 17:
             if net_len + 8 > avail:
-                v |= MAL
-            elif h[net_len + 6] or h[net_len + 7]:       # stored crc != 0 (pico_socket.c:1941)
+                return net, 0, MAL
+            if h[net_len + 6] or h[net_len + 7]:       # stored crc != 0 (pico_socket.c:1941)
                 l4 = refd(ps, bytes(t))
-                if l4:
-                    v |= L4
-    else:
-        if proto == 6:
-            if tl < 20:
-                v |= MAL
-            else:
-                t[16:18] = b"\0\0"
-                l4 = refd(ps, bytes(t))
-        elif proto == 1:
-            if tl < 8:
-                v |= MAL
-            else:
-                t[2:4] = b"\0\0"
-                l4 = ref(bytes(t))
-    return net, l4, (ACC if v == 0 else v)
+                return net, l4, (L4 if l4 else ACC)
+        return net, 0, ACC
+    if frag & 0x3FFF:
+        return net, 0, FRAG                            # a fragment: its own header crc only
+    v = ACC
+    if proto == 6:
+        if tl < 20:
+            v = MAL
+        else:
+            t[16:18] = b"\0\0"
+            l4 = refd(ps, bytes(t))
+    elif proto == 1:
+        if tl < 8:
+            v = MAL
+        else:
+            t[2:4] = b"\0\0"
+            l4 = ref(bytes(t))
+    return net, l4, v
+
+
+def fix_header_crc(buf: np.ndarray, off: int) -> None:
+    """Store the IPv4 header checksum of the header at off (after header bytes changed)."""
+    ihl = int(buf[off]) & 0xF
+    hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
+    buf[off + 10] = 0
+    buf[off + 11] = 0
+    c = O.ref_checksum(bytes(buf[off:off + hl]))
+    buf[off + 10] = c >> 8
+    buf[off + 11] = c & 0xFF
 
 
 def make_valid(buf: np.ndarray, off: int, avail: int):
-    """Insert correct checksums the way the reference TX path does."""
+    """Insert correct checksums the way the reference TX path does (a fragment: its header
+    checksum only; its transport was summed before fragmentation)."""
     n, l4, v = ipv4_expect(buf, off, avail, tx=True)
-    if v != 1:
+    if v not in (1, 16):
         return
     buf[off + 10] = n >> 8
     buf[off + 11] = n & 0xFF
+    if v == 16:
+        return
     h = buf[off:off + avail]
     ihl = int(h[0]) & 0xF
     hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
@@ -270,6 +293,11 @@ def ipv4_cases() -> dict:
         dict(lengths=rng.integers(40, 2000, 60).astype(np.uint32), proto=6, eth=False, ihl=15, seed=105),
         dict(lengths=np.array([64512, 9000, 40, 28, 20], dtype=np.uint32), proto=6, eth=True, ihl=5, seed=106),
         dict(lengths=rng.integers(28, 600, 30).astype(np.uint32), proto=47, eth=True, ihl=5, seed=107),
+        # fragments as they arrive: first (MF, offset 0), middle (MF, offset), last (offset)
+        dict(lengths=rng.integers(60, 1500, 60).astype(np.uint32), proto=6, eth=True, ihl=5, seed=108,
+             frag=np.array([0x2000, 0x2000 | 185, 370, 0x2000 | 7, 1], np.uint16)),
+        dict(lengths=rng.integers(36, 1500, 40).astype(np.uint32), proto=17, eth=False, ihl=6, seed=109,
+             frag=np.array([0x2000, 0x2000 | 46, 93, 0x4000 | 0x2000], np.uint16)),
     ]
     for sp in specs:
         if sp["proto"] == 6:
@@ -277,7 +305,7 @@ def ipv4_cases() -> dict:
         if sp["proto"] in (17, 1):
             sp["lengths"] = np.maximum(sp["lengths"], 4 * sp["ihl"] + 8).astype(np.uint32)
         buf, net, avail = synth.ipv4_batch(sp["lengths"], seed=sp["seed"], proto=sp["proto"],
-                                           eth=sp["eth"], ihl=sp["ihl"])
+                                           eth=sp["eth"], ihl=sp["ihl"], frag=sp.get("frag"))
         parts.append((buf, net, avail))
     # concatenate into one buffer
     bufs, nets, avs = [], [], []
@@ -295,30 +323,47 @@ def ipv4_cases() -> dict:
     tx_buf = buf.copy()
     for i in range(n):
         make_valid(buf, int(net[i]), int(avail[i]))
-    # corruptions for RX (index-stable): header byte, payload byte, length, crc fields, short buffers
+    # corruptions for RX (index-stable): header byte, payload byte, length, crc fields, short
+    # buffers; and, with a valid header checksum, the discards of pico_ipv4_process_in after it
+    # (bad sources, the evil bit, IHL < 5) and fragment hand-offs
     kind = np.zeros(n, dtype=np.uint8)
     for i in range(n):
         r = rng.random()
         o, a = int(net[i]), int(avail[i])
         ihl = int(buf[o]) & 0xF
         hl = 4 * ihl if ihl > 5 else 20
-        if r < 0.55:
+        if r < 0.45:
             continue
-        if r < 0.65:
+        if r < 0.52:
             buf[o + 8] ^= 0x01; kind[i] = 1                          # ttl flip -> NET_BAD
-        elif r < 0.75:
+        elif r < 0.60:
             p = o + hl + int(rng.integers(0, max(1, a - hl)))
             buf[p] ^= 0x40; kind[i] = 2                              # payload flip -> L4_BAD (TCP/UDP)
-        elif r < 0.80:
+        elif r < 0.64:
             avail[i] = max(0, a - int(rng.integers(1, 30))); kind[i] = 3   # truncated buffer -> MALFORMED
-        elif r < 0.85:
+        elif r < 0.68:
             buf[o + 2] = 0xFF; buf[o + 3] = 0xF0; kind[i] = 4        # tot len > buffer
-        elif r < 0.90 and buf[o + 9] == 17:
+        elif r < 0.72 and buf[o + 9] == 17:
             buf[o + hl + 6] = 0; buf[o + hl + 7] = 0; kind[i] = 5    # UDP crc 0 -> not verified
-        elif r < 0.95:
+        elif r < 0.76:
             buf[o + 2] = 0; buf[o + 3] = int(rng.integers(0, 20)); kind[i] = 6   # tot < hl: uint16 wrap
-        else:
+        elif r < 0.79:
             avail[i] = int(rng.integers(0, 20)); kind[i] = 7          # shorter than an IPv4 header
+        elif r < 0.85:
+            fr = int(rng.choice([0x2000, 0x2000 | int(rng.integers(1, 0x1FFF)), int(rng.integers(1, 0x1FFF))]))
+            buf[o + 6] = fr >> 8; buf[o + 7] = fr & 0xFF; kind[i] = 8     # a fragment -> FRAG
+            fix_header_crc(buf, o)
+        elif r < 0.89:
+            buf[o + 6] |= 0x80; kind[i] = 9                          # the evil bit -> MALFORMED
+            fix_header_crc(buf, o)
+        elif r < 0.93 and ihl == 5:
+            buf[o] = 0x40 | int(rng.integers(0, 5)); kind[i] = 10    # IHL < 5 -> MALFORMED
+            fix_header_crc(buf, o)
+        elif r < 0.97:
+            src = [b"\xff\xff\xff\xff", bytes([int(rng.integers(224, 255)), 0, 0, 1]), bytes([127, 0, 0, 1]),
+                   bytes([255, 1, 2, 3])][int(rng.integers(0, 4))]
+            buf[o + 12:o + 16] = np.frombuffer(src, np.uint8); kind[i] = 11   # source check
+            fix_header_crc(buf, o)
     rx = np.array([ipv4_expect(buf, int(net[i]), int(avail[i]), False) for i in range(n)], dtype=np.int64)
     tx = np.array([ipv4_expect(tx_buf, int(net[i]), int(avail[i]), True) for i in range(n)], dtype=np.int64)
     # the unit_socket.c test_crc_check frames, in a buffer of their own semantics
@@ -348,6 +393,13 @@ def unit_socket_frames() -> dict:
     add(b4, False, True, "TCP crc 0x0016 accepted (:512-514); the IP crc is stale after proto=6")
     b5 = bytearray(b4); b5[36:38] = bytes([0x88, 0x99])
     add(b5, False, False, "TCP crc 0x8899 rejected (:515-517)")
+    # the same two TCP frames with the IPv4 header checksum restored, so the batch reaches the
+    # transport check the unit test calls directly
+    for bb, ok, note in ((b4, True, "TCP crc 0x0016 accepted, IP crc restored"),
+                         (b5, False, "TCP crc 0x8899 rejected, IP crc restored")):
+        bc = bytearray(bb); bc[10:12] = b"\0\0"
+        c = O.ref_checksum(bytes(bc[:20])); bc[10], bc[11] = c >> 8, c & 0xFF
+        add(bc, True, ok, note)
     buf = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
     n = len(frames)
     net = np.arange(n, dtype=np.uint64) * 64
@@ -355,7 +407,8 @@ def unit_socket_frames() -> dict:
     rx = np.array([ipv4_expect(buf, int(net[i]), 64, False) for i in range(n)])
     for i in range(n):
         assert (rx[i, 0] == 0) == expect_net_ok[i], (i, rx[i])
-        assert (rx[i, 1] == 0) == expect_l4_ok[i], (i, rx[i])
+        if expect_net_ok[i]:           # a bad header is discarded before the transport check
+            assert (rx[i, 1] == 0) == expect_l4_ok[i], (i, rx[i])
     return dict(buf=buf, net=net, avail=avail, rx_net=rx[:, 0].astype(np.uint16), rx_l4=rx[:, 1].astype(np.uint16),
                 rx_verdict=rx[:, 2].astype(np.uint8), notes=np.array(notes))
 
@@ -370,14 +423,18 @@ def pseudo6(src: bytes, dst: bytes, nxt: int, tl: int) -> bytes:
     return src + dst + tl.to_bytes(4, "big") + bytes([0, 0, 0, nxt])
 
 
-def ipv6_expect(buf: np.ndarray, off: int, avail: int, seed: int, tx: bool):
-    """(out_l4, verdict) for one IPv6 datagram; see oracle_batch_ipv6 / the module doc."""
+def ipv6_expect(buf: np.ndarray, off: int, avail: int, seed: int, tx: bool, nxthdr_dispatch: bool = False):
+    """(out_l4, verdict) for one IPv6 datagram; see oracle_batch_ipv6 / the module doc.  RX
+    dispatches TCP / UDP as pico_transport_crc_check does (stack/pico_socket.c:1919-1958: byte 9
+    of the header read as an IPv4 proto) unless nxthdr_dispatch.  Seed 0 must name TCP / UDP /
+    ICMPv6 directly (the extension-header walk is pinned by make_ref_rx.py)."""
     refd = O.ref_dualbuffer_checksum
     MAL, L4, ACC = 8, 4, 1
     if avail < 40:
         return 0, MAL
     h = buf[off:off + avail].tobytes()
     net_len, proto = (seed & 0xFFFF, (seed >> 16) & 0xFF) if seed else (40, h[6])
+    assert seed or tx or proto in (6, 17, 58), "seed-0 extension headers: see make_ref_rx.py"
     plen = (h[4] << 8) | h[5]
     if net_len < 40 or net_len > avail:
         return 0, MAL
@@ -385,8 +442,16 @@ def ipv6_expect(buf: np.ndarray, off: int, avail: int, seed: int, tx: bool):
     if net_len + tl > avail:
         return 0, MAL
     t = bytearray(h[net_len:net_len + tl])
-    ps = pseudo6(h[8:24], h[24:40], proto, tl)
     if not tx:
+        if proto in (6, 17) and not nxthdr_dispatch:
+            b9 = h[9]
+            if (proto == 17 or b9 == 17) and net_len + 8 > avail:
+                return 0, MAL
+            if b9 == 6 or (b9 == 17 and (h[net_len + 6] or h[net_len + 7])):
+                c = refd(pseudo6(h[8:24], h[24:40], b9, tl), bytes(t))
+                return c, (L4 if c else ACC)
+            return 0, ACC
+        ps = pseudo6(h[8:24], h[24:40], proto, tl)
         if proto == 6:
             c = refd(ps, bytes(t))
             return c, (L4 if c else ACC)
@@ -403,6 +468,7 @@ def ipv6_expect(buf: np.ndarray, off: int, avail: int, seed: int, tx: bool):
             c = refd(ps, bytes(t))
             return c, (L4 if (c and h[net_len] in ND_MLD_TYPES) else ACC)
         return 0, ACC
+    ps = pseudo6(h[8:24], h[24:40], proto, tl)
     xoff, need = {6: (16, 20), 17: (6, 8), 58: (2, 4)}.get(proto, (None, 0))
     if xoff is None:
         return 0, ACC
@@ -449,6 +515,18 @@ def ipv6_cases() -> dict:
     avail = np.concatenate(avs).astype(np.uint32)
     seeds = np.concatenate(seeds_all).astype(np.uint32)
     n = net.size
+    # header byte 9 (source address byte 1) is what pico_transport_crc_check dispatches on
+    # (pico_socket.c:1919-1923): most TCP / UDP datagrams get their own protocol there, some the
+    # other one, the rest keep a random byte (no transport check)
+    for i in range(n):
+        o = int(net[i])
+        proto = (int(seeds[i]) >> 16) if seeds[i] else int(buf[o + 6])
+        if proto in (6, 17):
+            r = rng.random()
+            if r < 0.6:
+                buf[o + 9] = proto
+            elif r < 0.75:
+                buf[o + 9] = 23 - proto
     tx_buf = buf.copy()
     # valid checksums the way the reference TX path writes them
     for i in range(n):
@@ -483,9 +561,11 @@ def ipv6_cases() -> dict:
         else:
             seeds[i] = 20 | (6 << 16); kind[i] = 7                          # net_len < 40
     rx = np.array([ipv6_expect(buf, int(net[i]), int(avail[i]), int(seeds[i]), False) for i in range(n)])
+    rxn = np.array([ipv6_expect(buf, int(net[i]), int(avail[i]), int(seeds[i]), False, True) for i in range(n)])
     tx = np.array([ipv6_expect(tx_buf, int(net[i]), int(avail[i]), int(seeds[i]), True) for i in range(n)])
     return dict(buf=buf, tx_buf=tx_buf, net=net, avail=avail, seed=seeds, kind=kind,
                 rx_l4=rx[:, 0].astype(np.uint16), rx_verdict=rx[:, 1].astype(np.uint8),
+                rx_l4_nx=rxn[:, 0].astype(np.uint16), rx_verdict_nx=rxn[:, 1].astype(np.uint8),
                 tx_l4=tx[:, 0].astype(np.uint16), tx_verdict=tx[:, 1].astype(np.uint8))
 
 

@@ -50,7 +50,8 @@ from picotcp_amd import synth  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(ROOT, "oracle", "_ref", "libref_callers.so")
 RC_TCP4, RC_UDP4, RC_TCP6, RC_UDP6, RC_ICMP6, RC_MLD = range(6)
-MAL = 8
+MAL, NET_BAD, FRAG = 8, 2, 16
+NO_L4 = (MAL, NET_BAD, FRAG)          # verdicts where the stack makes no transport call
 
 
 def load():
@@ -76,8 +77,8 @@ def ipv4(lib, cases) -> tuple[np.ndarray, np.ndarray]:
         o, a = int(cases["net"][i]), int(cases["avail"][i])
         for is_tx, buf, out, verdict in ((False, cases["buf"], rx, cases["rx_verdict"]),
                                          (True, cases["tx_buf"], tx, cases["tx_verdict"])):
-            if verdict[i] & MAL or a < 20:
-                continue                                  # the IP layer discards it
+            if verdict[i] in NO_L4 or a < 20:
+                continue                                  # the IP layer discards it / hands it to reassembly
             h = buf[o:o + a]
             ihl = int(h[0]) & 0xF
             hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
@@ -93,17 +94,21 @@ def ipv4(lib, cases) -> tuple[np.ndarray, np.ndarray]:
     return rx, tx
 
 
-def ipv6(lib, cases) -> tuple[np.ndarray, np.ndarray]:
+def ipv6(lib, cases, nxthdr_dispatch: bool = False) -> tuple[np.ndarray, np.ndarray]:
+    """RX: TCP / UDP checked as pico_transport_crc_check dispatches them -- on byte 9 of the
+    header (stack/pico_socket.c:1919-1923) -- or, with nxthdr_dispatch, by the transport's own
+    protocol; ICMPv6 by pico_icmp6_checksum."""
     n = cases["net"].size
     rx = np.full(n, -1, dtype=np.int32)
     tx = np.full(n, -1, dtype=np.int32)
     which = {6: RC_TCP6, 17: RC_UDP6, 58: RC_ICMP6}
     need = {6: 20, 17: 8, 58: 4}
+    rxv = cases["rx_verdict_nx"] if nxthdr_dispatch else cases["rx_verdict"]
     for i in range(n):
         o, a, seed = int(cases["net"][i]), int(cases["avail"][i]), int(cases["seed"][i])
-        for is_tx, buf, out, verdict in ((False, cases["buf"], rx, cases["rx_verdict"]),
+        for is_tx, buf, out, verdict in ((False, cases["buf"], rx, rxv),
                                          (True, cases["tx_buf"], tx, cases["tx_verdict"])):
-            if verdict[i] & MAL or a < 40:
+            if verdict[i] in NO_L4 or a < 40:
                 continue
             h = buf[o:o + a]
             net_len, proto = (seed & 0xFFFF, (seed >> 16) & 0xFF) if seed else (40, int(h[6]))
@@ -111,6 +116,10 @@ def ipv6(lib, cases) -> tuple[np.ndarray, np.ndarray]:
             if proto not in which:
                 continue
             if not is_tx:
+                if proto in (6, 17) and not nxthdr_dispatch:
+                    proto = int(h[9])                      # net_hdr->proto through the IPv4 cast
+                    if proto not in (6, 17):
+                        continue
                 if proto == 17 and not (h[net_len + 6] or h[net_len + 7]):
                     continue
                 out[i] = call(lib, which[proto], buf, o, a, net_len, tl, False)
@@ -168,6 +177,8 @@ def eth(lib, n: int = 1536):
     checked = 0
     for i in range(n):
         o = int(off[i]) + 14
+        if tv[i] == 16:                                       # IPv4 fragment: its header checksum only
+            rx_buf[o + 10], rx_buf[o + 11] = tn[i] >> 8, tn[i] & 0xFF
         if tv[i] == 1:                                        # IPv4, accepted
             ihl = int(rx_buf[o]) & 0xF
             hl = 20 + (4 * (ihl - 5) if ihl > 5 else 0)
@@ -209,14 +220,22 @@ def eth(lib, n: int = 1536):
             rx_buf[o:o + 6] = np.frombuffer(bytes([0x02, 0x99, 0x88, 0x77, 0x66, 0x55]), np.uint8)
     rn, rl4, rv = O.batch_eth(rx_buf, desc, mac=MAC)
     rn_nomac, rl4_nomac, rv_nomac = O.batch_eth(rx_buf, desc)
+    rn_nx, rl4_nx, rv_nx = O.batch_eth(rx_buf, desc, mac=MAC, nxthdr_dispatch=True)
     for i in range(n):                                        # RX transport values vs the callers
         o, a = int(off[i]) + 14, int(desc["len"][i]) - 14
-        if rv[i] & 8 or a <= 0 or rl4[i] == 0 and not (rv[i] & 4):
+        if (rv[i] & 0x7F) in NO_L4 or a <= 0 or rl4[i] == 0 and not (rv[i] & 4):
             continue
         if rv[i] & 128:
             sd = int(seeds[i])
-            net_len, proto = (sd & 0xFFFF, sd >> 16) if sd else (40, int(rx_buf[o + 6]))
+            if sd:
+                net_len, proto = sd & 0xFFFF, sd >> 16
+            else:                                             # the extension-header walk (pinned separately)
+                k, net_len, proto = O.ipv6_walk(rx_buf[o:o + a])
+                if k != O.WALK_PROTO:
+                    continue
             tlen = (((int(rx_buf[o + 4]) << 8) | int(rx_buf[o + 5])) - (net_len - 40)) & 0xFFFF
+            if proto in (6, 17):
+                proto = int(rx_buf[o + 9])                    # pico_transport_crc_check's byte-9 dispatch
             which = {6: RC_TCP6, 17: RC_UDP6, 58: RC_ICMP6}.get(proto)
             if which is not None:
                 assert call(lib, which, rx_buf, o, a, net_len, tlen, False) == rl4[i], i
@@ -234,7 +253,7 @@ def eth(lib, n: int = 1536):
     return dict(tx_buf=tx_buf, buf=rx_buf, off=off, flen=flen, rx_len=desc["len"].copy(), seed=seeds, kind=kind,
                 mac=np.frombuffer(MAC, np.uint8).copy(), tx_net=tn, tx_l4=tl4, tx_verdict=tv,
                 rx_net=rn, rx_l4=rl4, rx_verdict=rv, rx_net_nomac=rn_nomac, rx_l4_nomac=rl4_nomac,
-                rx_verdict_nomac=rv_nomac)
+                rx_verdict_nomac=rv_nomac, rx_l4_nx=rl4_nx, rx_verdict_nx=rv_nx)
 
 
 def main() -> None:
@@ -245,14 +264,16 @@ def main() -> None:
     c6 = dict(np.load(os.path.join(OUT, "ipv6_cases.npz")))
     v4_rx, v4_tx = ipv4(lib, c4)
     v6_rx, v6_tx = ipv6(lib, c6)
+    v6_rx_nx, _ = ipv6(lib, c6, nxthdr_dispatch=True)
     # the Python restatement behind ipv4_cases / ipv6_cases must agree with the reference callers
     for name, got, exp in (("v4_rx", v4_rx, c4["rx_l4"]), ("v4_tx", v4_tx, c4["tx_l4"]),
-                           ("v6_rx", v6_rx, c6["rx_l4"]), ("v6_tx", v6_tx, c6["tx_l4"])):
+                           ("v6_rx", v6_rx, c6["rx_l4"]), ("v6_tx", v6_tx, c6["tx_l4"]),
+                           ("v6_rx_nx", v6_rx_nx, c6["rx_l4_nx"])):
         m = got >= 0
         bad = np.flatnonzero(got[m] != exp[m].astype(np.int32))
         assert bad.size == 0, (name, bad[:10])
         print(f"{name}: {int(m.sum())} reference caller values, all equal to the restatement")
-    out = dict(v4_rx=v4_rx, v4_tx=v4_tx, v6_rx=v6_rx, v6_tx=v6_tx, **mld(lib))
+    out = dict(v4_rx=v4_rx, v4_tx=v4_tx, v6_rx=v6_rx, v6_tx=v6_tx, v6_rx_nx=v6_rx_nx, **mld(lib))
     np.savez_compressed(os.path.join(OUT, "ref_callers.npz"), **out)
     print("mld:", out["mld_net"].size, "reports")
     np.savez_compressed(os.path.join(OUT, "eth_cases.npz"), **eth(lib))

@@ -85,3 +85,9 @@ def eth_desc(c: dict, rx: bool = True) -> np.ndarray:
     d["len"] = c["rx_len"] if rx else c["flen"]
     d["seed"] = c["seed"]
     return d
+
+
+def ref_rx_cases() -> dict:
+    """Datagrams with the reference's own RX verdicts (make_ref_rx.py)."""
+    z = np.load(os.path.join(GOLDEN, "ref_rx_cases.npz"))
+    return {k: z[k] for k in z.files}

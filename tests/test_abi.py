@@ -50,7 +50,13 @@ def test_reference_symbol_signatures_are_drop_in():
 
 
 def test_abi_version():
-    assert _lib.load().pico_csum_abi_version() == 1
+    assert _lib.load().pico_csum_abi_version() == _lib.ABI_VERSION == 2
+    src = open(HEADER).read()
+    assert re.search(r"#define PICO_CSUM_ABI_VERSION 2\b", src)
+    for name, val in (("F_NXTHDR_DISPATCH", 4), ("V_FRAG", 16), ("V_EXPIRED", 16), ("V_MALFORMED", 8)):
+        m = re.search(rf"#define PICO_CSUM_{name}\s+(0x[0-9a-fA-F]+|[0-9]+)u", src)
+        assert m and int(m.group(1), 0) == val, name
+        assert getattr(_lib, name) == val
 
 
 def test_header_compiles_as_c_and_cpp(tmp_path):
@@ -83,6 +89,13 @@ def test_argument_validation():
                                             None) == -_lib.EINVAL
     assert lib.pico_ipv6_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2004), 4, 0, None, None, None) \
         == -_lib.EINVAL
+    # F_NXTHDR_DISPATCH is an IPv6 / Ethernet RX option
+    assert lib.pico_ipv6_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_TX | _lib.F_NXTHDR_DISPATCH,
+                                            None, None, None) == -_lib.EINVAL
+    assert lib.pico_eth_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_TX | _lib.F_NXTHDR_DISPATCH,
+                                           None, None, None, None, None) == -_lib.EINVAL
+    assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_NXTHDR_DISPATCH, None, None,
+                                            None, None) == -_lib.EINVAL
     # NULL buffers
     assert lib.pico_checksum_batch_uniform_dev(None, 6000, 1500, 1500, 4, 0, vp(0x3000), None) == -_lib.EINVAL
     # frames past base_len
@@ -96,6 +109,7 @@ def test_argument_validation():
 
 def test_launch_override_validation():
     lib = _lib.load()
+    # uniform rings: group 4..64
     assert lib.pico_csum_set_launch_override(12, 2, 1, 16, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 3, 1, 16, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 2, 1, 6, 0, 0) == -_lib.EINVAL
@@ -104,22 +118,14 @@ def test_launch_override_validation():
     assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 1, 4) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 1, 3) == 0
     assert lib.pico_csum_set_launch_override(16, 2, 4, 16, 2, 2) == 0
-    assert lib.pico_csum_set_launch_override(1, 4, 1, 7, 1, 0) == 0
-    assert lib.pico_csum_set_launch_override(1, 4, 8, 7, 1, 0) == 0
-    assert lib.pico_csum_set_launch_override(1, 4, 9, 7, 1, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(1, 4, 0, 7, 1, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 8, 0, 37, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 8, 3, 16, 2, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(2, 8, 2, 16, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 16, 2, 16, 2, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(2, 4, 2, 16, 2, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(4, 16, 1, 16, 2, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(2, 4, 1, 16, 2, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(2, 8, 1, 16, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 8, 4, 16, 2, 0) == 0
-    assert lib.pico_csum_set_launch_override(2, 2, 0, 16, 2, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(3, 8, 0, 16, 1, 0) == 0
-    assert lib.pico_csum_set_launch_override(3, 8, 0, 32, 1, 0) == -_lib.EINVAL
+    # descriptor batches: group 2, fpw only; the flat (1) and adaptive (3) kernels are gone
+    assert lib.pico_csum_set_launch_override(2, 8, 0, 37, 2, 0) == 0
+    assert lib.pico_csum_set_launch_override(2, 0, 0, 64, 0, 0) == 0
+    assert lib.pico_csum_set_launch_override(2, 0, 0, 65, 0, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(2, 0, 0, 0, 0, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(1, 4, 1, 7, 1, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(3, 8, 0, 16, 1, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(0, 0, 0, 0, 0, 0) == 0
 
 

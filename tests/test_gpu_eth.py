@@ -13,7 +13,7 @@ from tests.test_gpu_parity import KERNELS, to_dev, u16, use_kernel
 
 pytestmark = pytest.mark.gpu
 
-SORTED = ["auto"] + [k for k, v in KERNELS.items() if v is not None and v[0] == 2]
+SORTED = list(KERNELS)
 
 
 @pytest.fixture(autouse=True)
@@ -57,9 +57,12 @@ def test_eth_tx_compute_and_write(kernel):
     _, _, rv = O.batch_eth(back, G.eth_desc(c, rx=False))
     acc = (c["tx_verdict"] & 0x7F) == 1
     assert ((rv[acc] & 0x7F) == 1).all()
+    # ... fragments got their header checksum only, and are handed to reassembly on RX ...
+    frag = (c["tx_verdict"] & 0x7F) == 16
+    assert frag.sum() > 10 and ((rv[frag] & 0x7F) == 16).all()
     # ... and only the crc fields changed
     diff = np.flatnonzero(back != c["tx_buf"])
-    assert diff.size <= 4 * int(acc.sum())
+    assert diff.size <= 4 * int(acc.sum()) + 2 * int(frag.sum())
     # the oracle TX on the GPU-written bytes sees the same values again
     on2, ol2, _ = O.batch_eth(back, G.eth_desc(c, rx=False), tx=True)
     np.testing.assert_array_equal(on2, c["tx_net"])

@@ -43,11 +43,11 @@ def test_far_apart_over_2gib(ipv6):
     d_desc = batch.desc_to_device(far, DEV)
     for tx in (False, True):
         fl = batch.F_TX if tx else 0
-        for shape in (None, (2, 8, 64, 1, 2), (2, 8, 64, 0, 2), (2, 8, 64, 2, 2)):
+        for shape in (None, 64, 7):
             if shape is None:
                 batch.set_launch_override(0)
             else:
-                batch.set_launch_override(*shape)
+                batch.set_launch_override(2, fpw=shape)
             msg = f"ipv6={ipv6} tx={tx} shape={shape}"
             if ipv6:
                 wl, wv = O.batch_ipv6(buf, desc, tx=tx)

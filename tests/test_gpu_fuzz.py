@@ -1,7 +1,8 @@
 """Randomized differential tests: every batched kernel vs the oracle on random
 descriptors, seeds, crc fields and fully random IPv4 / IPv6 header bytes (uint16
-length wraps, IHL 0-15, options, truncated buffers, unknown protocols).  Seeded,
-so a failure reproduces.  Run on an MI355X with `-m gpu`."""
+length wraps, IHL 0-15, options, truncated buffers, unknown protocols, fragments,
+extension-header chains).  Seeded, so a failure reproduces.  Run on an MI355X with
+`-m gpu`."""
 from __future__ import annotations
 
 import numpy as np
@@ -30,9 +31,15 @@ def to_dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-# launch shapes exercised for descriptor batches: auto (adaptive), flat, lane groups
-DESC_SHAPES = [None, (3, 8, 16, 0, 1), (2, 8, 64, 2, 2), (2, 8, 6, 2, 1), (2, 8, 64, 4, 2), (2, 8, 5, 4, 1), (2, 8, 64, 1, 2), (2, 8, 5, 1, 1), (2, 4, 33, 0, 1), (1, 1, 1, 0, 1), (1, 4, 64, 0, 2), (1, 2, 7, 2, 1), (4, 8, 16, 1, 1), (64, 2, 4, 1, 2),
-               (16, 8, 12, 1, 1)]
+# descriptor batches: the sorted-rounds kernel, automatic or with forced frames per wave
+DESC_FPW = [None, 64, 33, 6, 5, 1]
+
+
+def use_fpw(f):
+    if f is None:
+        batch.set_launch_override(0)
+    else:
+        batch.set_launch_override(2, fpw=f)
 
 
 @pytest.mark.parametrize("trial", range(6))
@@ -51,11 +58,8 @@ def test_fuzz_raw_descriptors(trial):
     crc = int(rng.choice([-1, 0, 2, 10, 16, 6]))
     want = O.batch_raw(buf, desc, crc_off=crc)
     d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
-    for shape in DESC_SHAPES:
-        if shape is None:
-            batch.set_launch_override(0)
-        else:
-            batch.set_launch_override(*shape)
+    for shape in DESC_FPW:
+        use_fpw(shape)
         got = u16(batch.checksum_batch(d_buf, d_desc, n, crc_off=crc))
         np.testing.assert_array_equal(got, want, err_msg=f"trial={trial} shape={shape} crc={crc}")
 
@@ -102,12 +106,8 @@ def test_fuzz_ipv4(trial, tx):
     desc["seed"] = 0
     wn, wl, wv = O.batch_ipv4(buf, desc, tx=tx)
     d_desc = batch.desc_to_device(desc, DEV)
-    for shape in (None, (2, 8, 64, 2, 2), (2, 8, 3, 2, 1), (2, 8, 64, 4, 2), (2, 8, 3, 4, 1), (2, 8, 64, 1, 2), (2, 8, 3, 1, 1), (1, 1, 5, 0, 1), (1, 8, 64, 0, 2), (4, 8, 16, 1, 1),
-                  (32, 2, 64, 1, 1)):
-        if shape is None:
-            batch.set_launch_override(0)
-        else:
-            batch.set_launch_override(*shape)
+    for shape in (None, 64, 3, 1):
+        use_fpw(shape)
         net, l4, v = batch.ipv4_checksum_batch(to_dev(buf), d_desc, n, flags=batch.F_TX if tx else 0)
         np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg=f"verdict trial={trial} shape={shape}")
         np.testing.assert_array_equal(u16(net), wn, err_msg=f"net trial={trial} shape={shape}")
@@ -122,14 +122,41 @@ def test_fuzz_ipv6(trial, tx):
     buf, desc = random_datagrams(rng, n, ipv6=True)
     wl, wv = O.batch_ipv6(buf, desc, tx=tx)
     d_desc = batch.desc_to_device(desc, DEV)
-    for shape in (None, (2, 8, 64, 2, 2), (2, 8, 7, 2, 1), (2, 8, 64, 4, 2), (2, 8, 7, 4, 1), (2, 8, 64, 1, 2), (2, 8, 7, 1, 1), (1, 1, 3, 0, 1), (1, 8, 64, 0, 2)):
-        if shape is None:
-            batch.set_launch_override(0)
-        else:
-            batch.set_launch_override(*shape)
+    for shape in (None, 64, 7, 1):
+        use_fpw(shape)
         l4, v = batch.ipv6_checksum_batch(to_dev(buf), d_desc, n, flags=batch.F_TX if tx else 0)
         np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg=f"verdict trial={trial} shape={shape}")
         np.testing.assert_array_equal(u16(l4), wl, err_msg=f"l4 trial={trial} shape={shape}")
+    if not tx:                                   # the next-header dispatch on the same bytes
+        wl, wv = O.batch_ipv6(buf, desc, nxthdr_dispatch=True)
+        l4, v = batch.ipv6_checksum_batch(to_dev(buf), d_desc, n, flags=batch.F_NXTHDR_DISPATCH)
+        np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg=f"nx verdict trial={trial}")
+        np.testing.assert_array_equal(u16(l4), wl, err_msg=f"nx l4 trial={trial}")
+
+
+@pytest.mark.parametrize("trial", range(3))
+def test_fuzz_rx_chains(trial):
+    """make_ref_rx.py's generators (the reference-pinned families: fragments, the evil bit,
+    IHL < 5, bad sources; random IPv6 extension-header chains for the kernel's own walk),
+    fresh seeds, against the oracle -- which those fixtures pin to the compiled reference."""
+    from tests.golden import make_ref_rx as M
+    rng = np.random.default_rng(9100 + trial)
+    for gen, fam in ((M.gen_v4, 4), (M.gen_v6, 6)):
+        items = gen(rng, 3000)
+        buf, off, av = M.pack(items, rng)
+        desc = batch.make_desc(off, av)
+        d_desc = batch.desc_to_device(desc, DEV)
+        for shape in (None, 64, 5):
+            use_fpw(shape)
+            if fam == 4:
+                wn, wl, wv = O.batch_ipv4(buf, desc)
+                net, l4, v = batch.ipv4_checksum_batch(to_dev(buf), d_desc, len(items))
+                np.testing.assert_array_equal(u16(net), wn, err_msg=f"v4 net trial={trial} shape={shape}")
+            else:
+                wl, wv = O.batch_ipv6(buf, desc)
+                l4, v = batch.ipv6_checksum_batch(to_dev(buf), d_desc, len(items))
+            np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg=f"v{fam} verdict trial={trial} shape={shape}")
+            np.testing.assert_array_equal(u16(l4), wl, err_msg=f"v{fam} l4 trial={trial} shape={shape}")
 
 
 @pytest.mark.parametrize("trial", range(4))

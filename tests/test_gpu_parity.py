@@ -14,24 +14,17 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
-# descriptor batches also run on the flat work-list kernel (group 1) and the
-# sorted-rounds kernel (group 2)
-DESC_SHAPES = SHAPES + [(1, c) for c in (1, 2, 4, 8)] + [(2, 4), (2, 8)]
-# override per descriptor kernel for the kernel-parametrized tests
-KERNELS = {"auto": None, "adaptive": (3, 8, 16, 0, 1), "flat": (1, 4, 8, 1, 1), "sorted": (2, 8, 64, 4, 2),
-           "sorted_fpw7": (2, 8, 7, 4, 1), "sorted_c4": (2, 4, 13, 0, 1), "sorted_small": (2, 8, 64, 1, 2),
-           "sorted_small_fpw5": (2, 8, 5, 1, 1), "sorted_stream": (2, 8, 64, 2, 2), "sorted_stream_fpw9": (2, 8, 9, 2, 1)}
-
-
-def fpws(g):
-    return (1, 13, 64) if g <= 2 else sorted({64 // g, 64})
+# descriptor batches: the sorted-rounds kernel, automatic or with a forced frames-per-wave
+# (1: a wave per frame; 5 / 7 / 13: ragged waves; 64: full waves whatever the batch size)
+FPWS = (1, 5, 7, 13, 64)
+KERNELS = {"auto": None, **{f"fpw{f}": f for f in FPWS}}
 
 
 def use_kernel(name):
     if KERNELS[name] is None:
         batch.set_launch_override(0)
     else:
-        batch.set_launch_override(*KERNELS[name])
+        batch.set_launch_override(2, fpw=KERNELS[name])
 
 
 def u16(t: torch.Tensor) -> np.ndarray:
@@ -111,21 +104,20 @@ def test_desc_golden(name):
     np.testing.assert_array_equal(got, case["expected"])
 
 
-@pytest.mark.parametrize("g,c", DESC_SHAPES)
-def test_desc_every_shape(g, c):
+@pytest.mark.parametrize("fpw", FPWS)
+def test_desc_every_fpw(fpw):
     case = G.raw_cases()["mixed_align"]
     buf, desc = G.raw_case_inputs(case, lambda b: O.adder(0, b))
     d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc, DEV)
-    for fpw in fpws(g):
-        batch.set_launch_override(g, c, fpw)
-        got = u16(batch.checksum_batch(d_buf, d_desc, desc.size))
-        np.testing.assert_array_equal(got, case["expected"], err_msg=f"g={g} c={c} fpw={fpw}")
+    batch.set_launch_override(2, fpw=fpw)
+    got = u16(batch.checksum_batch(d_buf, d_desc, desc.size))
+    np.testing.assert_array_equal(got, case["expected"], err_msg=f"fpw={fpw}")
 
 
 @pytest.mark.parametrize("kernel", list(KERNELS))
 def test_desc_big_regions(kernel):
-    """Regions over 64K chunks (> 1 MiB) take the flat kernel's whole-wave path; mixed with
-    small ones, odd offsets, seeds and a crc field."""
+    """Regions over 64K chunks (> 1 MiB) in 64-lane rounds, mixed with small ones, odd
+    offsets, seeds and a crc field."""
     rng = np.random.default_rng(44)
     buf = synth.random_bytes(45, 12 << 20)
     offs = [1, 3 << 20, 5, (7 << 20) + 3, 100, 2000, 11 << 20]
@@ -242,22 +234,23 @@ def test_ipv4_golden_rx_tx():
     np.testing.assert_array_equal(v.cpu().numpy(), c["tx_verdict"])
 
 
-@pytest.mark.parametrize("g,c", DESC_SHAPES)
-def test_ipv4_every_shape(g, c):
+@pytest.mark.parametrize("fpw", FPWS)
+def test_ipv4_every_fpw(fpw):
+    """The fixture (valid, corrupted, fragments, the evil bit, IHL < 5, bad sources, options,
+    truncations) with every wave shape, RX and TX."""
     cs = G.ipv4_cases()
     desc = batch.desc_to_device(G.ipv4_desc(cs["net"], cs["avail"]), DEV)
     n = cs["net"].size
     d_buf = to_dev(cs["buf"])
-    for fpw in fpws(g):
-        batch.set_launch_override(g, c, fpw)
-        net, l4, v = batch.ipv4_checksum_batch(d_buf, desc, n)
-        np.testing.assert_array_equal(u16(net), cs["rx_net"], err_msg=f"g={g} c={c} fpw={fpw}")
-        np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"g={g} c={c} fpw={fpw}")
-        np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"g={g} c={c} fpw={fpw}")
-        net, l4, v = batch.ipv4_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
-        np.testing.assert_array_equal(u16(net), cs["tx_net"], err_msg=f"TX g={g} c={c} fpw={fpw}")
-        np.testing.assert_array_equal(u16(l4), cs["tx_l4"], err_msg=f"TX g={g} c={c} fpw={fpw}")
-        np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"], err_msg=f"TX g={g} c={c} fpw={fpw}")
+    batch.set_launch_override(2, fpw=fpw)
+    net, l4, v = batch.ipv4_checksum_batch(d_buf, desc, n)
+    np.testing.assert_array_equal(u16(net), cs["rx_net"], err_msg=f"fpw={fpw}")
+    np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"fpw={fpw}")
+    np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"fpw={fpw}")
+    net, l4, v = batch.ipv4_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
+    np.testing.assert_array_equal(u16(net), cs["tx_net"], err_msg=f"TX fpw={fpw}")
+    np.testing.assert_array_equal(u16(l4), cs["tx_l4"], err_msg=f"TX fpw={fpw}")
+    np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"], err_msg=f"TX fpw={fpw}")
 
 
 def test_ipv4_out_of_bounds_is_malformed():
@@ -337,19 +330,22 @@ def test_host_batch_roundtrip():
 
 # ------------------------------------------------------------------ IPv6 fused
 
-@pytest.mark.parametrize("g,c", [(1, 1), (1, 2), (1, 4), (1, 8), (2, 4), (2, 8)])
-def test_ipv6_golden_rx_tx(g, c):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_ipv6_golden_rx_tx(kernel):
+    """RX with the reference's byte-9 dispatch (default) and the next-header dispatch, TX."""
     cs = G.ipv6_cases()
     desc = batch.desc_to_device(G.ipv6_desc(cs), DEV)
     n = cs["net"].size
-    for fpw in (1, 13, 64):
-        batch.set_launch_override(g, c, fpw, 0, 1)
-        l4, v = batch.ipv6_checksum_batch(to_dev(cs["buf"]), desc, n)
-        np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"], err_msg=f"c={c} fpw={fpw}")
-        np.testing.assert_array_equal(u16(l4), cs["rx_l4"], err_msg=f"c={c} fpw={fpw}")
-        l4, v = batch.ipv6_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
-        np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"], err_msg=f"TX c={c} fpw={fpw}")
-        np.testing.assert_array_equal(u16(l4), cs["tx_l4"], err_msg=f"TX c={c} fpw={fpw}")
+    use_kernel(kernel)
+    l4, v = batch.ipv6_checksum_batch(to_dev(cs["buf"]), desc, n)
+    np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict"])
+    np.testing.assert_array_equal(u16(l4), cs["rx_l4"])
+    l4, v = batch.ipv6_checksum_batch(to_dev(cs["buf"]), desc, n, flags=batch.F_NXTHDR_DISPATCH)
+    np.testing.assert_array_equal(v.cpu().numpy(), cs["rx_verdict_nx"])
+    np.testing.assert_array_equal(u16(l4), cs["rx_l4_nx"])
+    l4, v = batch.ipv6_checksum_batch(to_dev(cs["tx_buf"]), desc, n, flags=batch.F_TX)
+    np.testing.assert_array_equal(v.cpu().numpy(), cs["tx_verdict"])
+    np.testing.assert_array_equal(u16(l4), cs["tx_l4"])
 
 
 @pytest.mark.parametrize("proto,hbh,icmp_type", [(6, False, 0), (17, False, 0), (58, False, 135), (6, True, 0),
@@ -367,17 +363,22 @@ def test_ipv6_tx_write_then_rx_accepts(proto, hbh, icmp_type):
     d_buf, d_desc = to_dev(buf), batch.desc_to_device(desc_h, DEV)
     l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size, flags=batch.F_TX | batch.F_WRITE)
     np.testing.assert_array_equal(u16(l4), want_l4)
-    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size)
+    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size, flags=batch.F_NXTHDR_DISPATCH)
     assert (v.cpu().numpy() == 1).all()
     assert (u16(l4) == 0).all()
-    ol, ov = O.batch_ipv6(d_buf.cpu().numpy(), desc_h)
+    ol, ov = O.batch_ipv6(d_buf.cpu().numpy(), desc_h, nxthdr_dispatch=True)
     assert (ov == 1).all()
+    # the reference's dispatch (byte 9) on the same bytes: whatever it checks, the oracle agrees
+    wl, wv = O.batch_ipv6(d_buf.cpu().numpy(), desc_h)
+    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, lens.size)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    np.testing.assert_array_equal(u16(l4), wl)
 
 
 # ------------------------------------------------------------------ reassembly-size datagrams
 
 @pytest.mark.parametrize("proto", [6, 17])
-@pytest.mark.parametrize("kernel", ["auto", "flat"])
+@pytest.mark.parametrize("kernel", ["auto", "fpw7"])
 def test_ipv4_frag_max_datagrams(proto, kernel):
     """64512 B (PICO_IPV4_FRAG_MAX_SIZE) IPv4 datagrams, as pico_fragments_reassemble hands
     them on: TX compute + write, then RX verify accepts; both against the oracle, with a

@@ -15,7 +15,7 @@ from tests.test_gpu_parity import KERNELS, to_dev, u16, use_kernel
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [k for k in KERNELS if k != "adaptive"]     # the adaptive kernel serves raw batches only
+VARIANTS = list(KERNELS)
 
 
 @pytest.fixture(autouse=True)
@@ -47,6 +47,19 @@ def test_ipv6_transport_vs_reference_callers(kernel, tx):
     buf = to_dev(c["tx_buf" if tx else "buf"])
     d = to_dev(G.ipv6_desc(c).view(np.uint8))
     l4, _ = batch.ipv6_checksum_batch(buf, d, c["net"].size, flags=_lib.F_TX if tx else 0)
+    got = u16(l4).astype(np.int32)
+    m = ref >= 0
+    np.testing.assert_array_equal(got[m], ref[m])
+
+
+@pytest.mark.parametrize("kernel", VARIANTS)
+def test_ipv6_nxthdr_dispatch_vs_reference_callers(kernel):
+    """F_NXTHDR_DISPATCH: the transport's own protocol picks the caller."""
+    rc, c = G.ref_callers(), G.ipv6_cases()
+    ref = rc["v6_rx_nx"]
+    use_kernel(kernel)
+    d = to_dev(G.ipv6_desc(c).view(np.uint8))
+    l4, _ = batch.ipv6_checksum_batch(to_dev(c["buf"]), d, c["net"].size, flags=_lib.F_NXTHDR_DISPATCH)
     got = u16(l4).astype(np.int32)
     m = ref >= 0
     np.testing.assert_array_equal(got[m], ref[m])
