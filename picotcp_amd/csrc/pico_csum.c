@@ -475,6 +475,8 @@ struct pico_csum_ctx {
     int desc_ready;
 };
 
+static void ctx_desc_free(struct pico_csum_ctx *c);
+
 struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes)
 {
     struct pico_csum_ctx *c;
@@ -513,15 +515,8 @@ void pico_csum_ctx_destroy(struct pico_csum_ctx *c)
         if (c->d_out[i]) hipFree(c->d_out[i]);
         if (c->done[i]) hipEventDestroy(c->done[i]);
         if (c->st[i]) hipStreamDestroy(c->st[i]);
-        if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
-        if (c->d_desc[i]) hipFree(c->d_desc[i]);
-        if (c->d_net[i]) hipFree(c->d_net[i]);
-        if (c->d_l4[i]) hipFree(c->d_l4[i]);
-        if (c->d_ver[i]) hipFree(c->d_ver[i]);
-        if (c->h_net[i]) hipHostFree(c->h_net[i]);
-        if (c->h_l4[i]) hipHostFree(c->h_l4[i]);
-        if (c->h_ver[i]) hipHostFree(c->h_ver[i]);
     }
+    ctx_desc_free(c);
     free(c);
 }
 
@@ -586,6 +581,26 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *c, const void *base, 
 
 enum { HB_RAW = 0, HB_IPV4 = 1, HB_IPV6 = 2, HB_ETH = 3 };
 
+static void ctx_desc_free(struct pico_csum_ctx *c)
+{
+    int i;
+    for (i = 0; i < 2; i++) {
+        if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
+        if (c->d_desc[i]) hipFree(c->d_desc[i]);
+        if (c->d_net[i]) hipFree(c->d_net[i]);
+        if (c->d_l4[i]) hipFree(c->d_l4[i]);
+        if (c->d_ver[i]) hipFree(c->d_ver[i]);
+        if (c->h_net[i]) hipHostFree(c->h_net[i]);
+        if (c->h_l4[i]) hipHostFree(c->h_l4[i]);
+        if (c->h_ver[i]) hipHostFree(c->h_ver[i]);
+        c->h_desc[i] = c->d_desc[i] = NULL;
+        c->d_net[i] = c->d_l4[i] = c->h_net[i] = c->h_l4[i] = NULL;
+        c->d_ver[i] = c->h_ver[i] = NULL;
+    }
+    c->desc_ready = 0;
+}
+
+/* on the ctx's device (the caller has made it current); on failure nothing stays allocated */
 static int ctx_desc_alloc(struct pico_csum_ctx *c)
 {
     uint64_t nd = CTX_MAX_DESC(c->staging);
@@ -599,34 +614,53 @@ static int ctx_desc_alloc(struct pico_csum_ctx *c)
             hipMalloc((void **)&c->d_ver[i], nd) != hipSuccess ||
             hipHostMalloc((void **)&c->h_net[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void **)&c->h_l4[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_ver[i], nd, hipHostMallocDefault) != hipSuccess)
+            hipHostMalloc((void **)&c->h_ver[i], nd, hipHostMallocDefault) != hipSuccess) {
+            ctx_desc_free(c);
             return fail(PICO_CSUM_ENOMEM, "ctx descriptor staging (%llu descriptors)", (unsigned long long)nd);
+        }
     }
     c->desc_ready = 1;
     return 0;
 }
 
+static int in_bounds(const struct pico_csum_desc *d, uint64_t base_len)
+{
+    return d->off <= base_len && d->len <= base_len - d->off;
+}
+
 /* One burst: descriptors [i, j) whose bytes span at most the staging buffer go H2D (the span
  * and the descriptors, rebased to it) on stream b, through the device batch, and their results
- * (with F_WRITE also the span, crc fields written) D2H; the next chunk's H2D overlaps this one
- * on the other stream.  A region outside base_len is handed to the kernel as one (offset past
- * the staging bound), so it gets the device API's answer for it. */
+ * D2H; the next chunk's H2D overlaps this one on the other stream.  A region outside base_len is
+ * handed to the kernel as one (offset past the staging bound), so it gets the device API's
+ * answer for it.
+ * F_WRITE copies back only the hull of the chunk's own frames [first frame start, last frame
+ * end) -- never the 16-byte rounding below it, which may hold the previous chunk's last frame --
+ * and a chunk whose hull overlaps the hull of any chunk issued on the other stream (descriptors
+ * not in ascending order) first waits for that stream, so no stale copy can land over a
+ * result.  Every argument is checked before the first copy: an error returns with nothing
+ * queued and no byte of `base` changed; a HIP error mid-burst drains both streams first. */
 static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, uint64_t base_len,
                            const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
                            const uint8_t *mac, uint16_t *out, uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict,
                            const char *what)
 {
     const uint64_t maxd = CTX_MAX_DESC(c ? c->staging : 0);
+    const int write = (flags & PICO_CSUM_F_WRITE) != 0;
+    uint64_t wlo[2] = {UINT64_MAX, UINT64_MAX}, whi[2] = {0, 0};   /* F_WRITE hulls issued per stream */
     uint32_t i = 0;
     int b = 0, rc = 0;
     if (!c || !base || !desc)
         return fail(PICO_CSUM_EINVAL, "%s: NULL argument", what);
     if (n == 0)
         return 0;
-    if ((rc = ctx_desc_alloc(c)) != 0)
-        return rc;
+    for (i = 0; i < n; i++)                     /* before anything is queued */
+        if (in_bounds(&desc[i], base_len) && (desc[i].len > c->staging || (desc[i].off & 15u) + desc[i].len > c->staging))
+            return fail(PICO_CSUM_EINVAL, "%s: frame %u of %u bytes exceeds the staging buffer", what, i, desc[i].len);
+    i = 0;
     if (hipSetDevice(c->device) != hipSuccess)
         return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
+    if ((rc = ctx_desc_alloc(c)) != 0)
+        return rc;
     c->pend_cnt[0] = c->pend_cnt[1] = 0;
     /* results of slot bb's last chunk, from pinned staging to the caller's arrays */
 #define FLUSH(bb)                                                                                  \
@@ -640,50 +674,50 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
             c->pend_cnt[bb] = 0;                                                                   \
         }                                                                                          \
     } while (0)
-    while (i < n && !rc) {
-        uint64_t lo = UINT64_MAX, hi = 0;
+#define TRY(call, msg)                                                                             \
+    if ((e = (call)) != hipSuccess) {                                                              \
+        rc = fail(PICO_CSUM_EIO, "%s: %s: %s", what, msg, hipGetErrorString(e));                   \
+        break;                                                                                     \
+    }
+    while (i < n) {
+        uint64_t lo = UINT64_MAX, hi = 0, hlo = UINT64_MAX;
         uint32_t j = i, k, cnt;
         hipError_t e;
         /* grow the chunk while the span fits the staging buffer */
         while (j < n && (uint64_t)(j - i) < maxd) {
             uint64_t o = desc[j].off, oa, end;
-            if (o > base_len || desc[j].len > base_len - o) {   /* out of bounds: no bytes */
+            if (!in_bounds(&desc[j], base_len)) {      /* out of bounds: no bytes */
                 j++;
                 continue;
             }
             oa = o & ~(uint64_t)15;   /* the span starts on a 16-byte line: frames keep their alignment */
             end = o + desc[j].len;
-            if ((end > hi ? end : hi) - (oa < lo ? oa : lo) > c->staging) {
-                if (j == i)
-                    return fail(PICO_CSUM_EINVAL, "%s: a frame of %u bytes exceeds the staging buffer", what,
-                                desc[j].len);
-                break;
-            }
+            if ((end > hi ? end : hi) - (oa < lo ? oa : lo) > c->staging)
+                break;                /* (j > i: a single frame fits, checked above) */
             if (oa < lo) lo = oa;
+            if (o < hlo) hlo = o;
             if (end > hi) hi = end;
             j++;
         }
         cnt = j - i;
-        if (lo == UINT64_MAX) lo = hi = 0;
+        if (lo == UINT64_MAX) lo = hi = hlo = 0;
         /* the pinned descriptor and result slots are reused: the previous chunk on them must be
          * done, and its results copied out */
-        if (hipEventSynchronize(c->done[b]) != hipSuccess)
-            return fail(PICO_CSUM_EIO, "%s: event synchronize failed", what);
+        TRY(hipEventSynchronize(c->done[b]), "event synchronize")
         FLUSH(b);
         for (k = 0; k < cnt; k++) {
             const struct pico_csum_desc *s = &desc[i + k];
             struct pico_csum_desc *t = &c->h_desc[b][k];
-            int oob = s->off > base_len || s->len > base_len - s->off;
-            t->off = oob ? UINT64_MAX : s->off - lo;
+            t->off = in_bounds(s, base_len) ? s->off - lo : UINT64_MAX;
             t->len = s->len;
             t->seed = s->seed;
         }
-        if (hi > lo && (e = hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice,
-                                           c->st[b])) != hipSuccess)
-            return fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
-        if ((e = hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
-                                hipMemcpyHostToDevice, c->st[b])) != hipSuccess)
-            return fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
+        if (write && hi > hlo && hlo < whi[b ^ 1] && wlo[b ^ 1] < hi)
+            TRY(hipStreamWaitEvent(c->st[b], c->done[b ^ 1], 0), "stream wait")
+        if (hi > lo)
+            TRY(hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice, c->st[b]), "H2D")
+        TRY(hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
+                           hipMemcpyHostToDevice, c->st[b]), "H2D")
         switch (mode) {
         case HB_RAW:
             rc = pico_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, crc_off, flags, c->d_l4[b], NULL,
@@ -704,22 +738,26 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         }
         if (rc)
             break;
-#define D2H(dst, src, bytes)                                                                              \
-        if ((dst) && (e = hipMemcpyAsync((dst), (src), (bytes), hipMemcpyDeviceToHost, c->st[b])) != hipSuccess) \
-            return fail(PICO_CSUM_EIO, "%s: D2H: %s", what, hipGetErrorString(e));
-        D2H(out || out_l4 ? c->h_l4[b] : NULL, c->d_l4[b], (size_t)cnt * 2u)
-        D2H(out_net ? c->h_net[b] : NULL, c->d_net[b], (size_t)cnt * 2u)
-        D2H(verdict ? c->h_ver[b] : NULL, c->d_ver[b], (size_t)cnt)
+        if (out || out_l4)
+            TRY(hipMemcpyAsync(c->h_l4[b], c->d_l4[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]), "D2H")
+        if (out_net)
+            TRY(hipMemcpyAsync(c->h_net[b], c->d_net[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]), "D2H")
+        if (verdict)
+            TRY(hipMemcpyAsync(c->h_ver[b], c->d_ver[b], (size_t)cnt, hipMemcpyDeviceToHost, c->st[b]), "D2H")
         c->pend_first[b] = i;
         c->pend_cnt[b] = cnt;
-        if ((flags & PICO_CSUM_F_WRITE) && hi > lo)
-            D2H((uint8_t *)base + lo, c->d_buf[b], hi - lo)
-#undef D2H
-        if (hipEventRecord(c->done[b], c->st[b]) != hipSuccess)
-            return fail(PICO_CSUM_EIO, "%s: event record failed", what);
+        if (write && hi > hlo) {
+            TRY(hipMemcpyAsync((uint8_t *)base + hlo, (const uint8_t *)c->d_buf[b] + (hlo - lo), hi - hlo,
+                               hipMemcpyDeviceToHost, c->st[b]), "D2H")
+            if (hlo < wlo[b]) wlo[b] = hlo;
+            if (hi > whi[b]) whi[b] = hi;
+        }
+        TRY(hipEventRecord(c->done[b], c->st[b]), "event record")
         i = j;
         b ^= 1;
     }
+#undef TRY
+    /* drain both streams whatever happened: no copy may land after the return */
     if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
         if (!rc) rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
     if (!rc) {

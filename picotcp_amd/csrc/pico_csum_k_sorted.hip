@@ -342,20 +342,21 @@ __device__ __noinline__ int walk_dst(const uint8_t* __restrict__ h, uint32_t ava
 }
 #undef WBYTE
 
-#define WBYTE(k, dst)                                \
-    do {                                             \
-        if ((uint32_t)(k) >= avail) return WALK_BAD; \
-        (dst) = h[(uint32_t)(k)];                    \
+#define WBYTE(k, dst)                                            \
+    do {                                                         \
+        if ((uint32_t)(k) >= avail) return (uint32_t)(WALK_BAD + 1); \
+        (dst) = h[(uint32_t)(k)];                                \
     } while (0)
 
-__device__ __noinline__ __attribute__((unused)) int ipv6_walk(const uint8_t* __restrict__ h, uint32_t avail, uint32_t& net_len_out,
-                                      uint32_t& proto_out) {
+// Returns kind + 1 | net_len << 8 | proto << 24 (one register: no stack slots for outputs).
+__device__ __noinline__ __attribute__((unused)) uint32_t ipv6_walk_packed(const uint8_t* __restrict__ h,
+                                                                           uint32_t avail) {
     const uint32_t plen = ((uint32_t)h[4] << 8) | h[5];
     uint32_t nx = h[6], b, ptr = 40u;
     // sequence check: steps of (uint8)((len + 1) << 3) (0 when len >= 31: the next step reads
     // the same header again), 8 for a fragment header; at most 2 steps per 8 bytes of avail
     for (uint32_t it = 0;; ++it) {
-        if (it > 2u * (avail >> 3) + 8u) return WALK_BAD;
+        if (it > 2u * (avail >> 3) + 8u) return (uint32_t)(WALK_BAD + 1);
         uint32_t optlen;
         if (nx == 0u || nx == 43u || nx == 60u || nx == 50u || nx == 51u) {
             WBYTE(ptr + 1u, b);
@@ -365,7 +366,7 @@ __device__ __noinline__ __attribute__((unused)) int ipv6_walk(const uint8_t* __r
         } else if (nx == 59u || nx == 6u || nx == 17u || nx == 58u) {
             break;
         } else {
-            return WALK_DROP;
+            return (uint32_t)(WALK_DROP + 1);
         }
         WBYTE(ptr, nx);
         ptr += optlen;
@@ -379,17 +380,15 @@ __device__ __noinline__ __attribute__((unused)) int ipv6_walk(const uint8_t* __r
         const uint32_t e = net_len;
         uint32_t cur_optlen;
         if (nx == 6u || nx == 17u || nx == 58u) {
-            if (must_align && (plen & 7u) != 0u) return WALK_DROP;
-            net_len_out = net_len;
-            proto_out = nx;
-            return frag ? WALK_FRAG : WALK_PROTO;
+            if (must_align && (plen & 7u) != 0u) return (uint32_t)(WALK_DROP + 1);
+            return (uint32_t)((frag ? WALK_FRAG : WALK_PROTO) + 1) | (net_len << 8) | (nx << 24);
         } else if (nx == 0u) {                                      // hop-by-hop: only first
-            if (cur_nexthdr != 6u) return WALK_DROP;
+            if (cur_nexthdr != 6u) return (uint32_t)(WALK_DROP + 1);
             WBYTE(e + 1u, b);
             cur_optlen = (b + 1u) << 3;
             const int r = walk_hbh(h, avail, e);
-            if (r == -2) return WALK_BAD;
-            if (r < 0) return WALK_DROP;
+            if (r == -2) return (uint32_t)(WALK_BAD + 1);
+            if (r < 0) return (uint32_t)(WALK_DROP + 1);
             must_align = r != 0;
         } else if (nx == 43u) {                                     // routing
             uint32_t segleft, type;
@@ -398,26 +397,26 @@ __device__ __noinline__ __attribute__((unused)) int ipv6_walk(const uint8_t* __r
             WBYTE(e + 3u, segleft);
             if (segleft != 0u) {
                 WBYTE(e + 2u, type);
-                if (type != 2u) return WALK_DROP;
+                if (type != 2u) return (uint32_t)(WALK_DROP + 1);
             }
         } else if (nx == 44u) {                                     // fragment
             uint32_t om1;
             cur_optlen = 8u;
             WBYTE(e + 3u, om1);
-            if (e + 2u >= avail) return WALK_BAD;                   // om[0] is read too
+            if (e + 2u >= avail) return (uint32_t)(WALK_BAD + 1);                   // om[0] is read too
             frag = true;
-            if ((om1 & 1u) && (plen & 7u) != 0u) return WALK_DROP;
+            if ((om1 & 1u) && (plen & 7u) != 0u) return (uint32_t)(WALK_DROP + 1);
         } else if (nx == 60u) {                                     // destination options
             WBYTE(e + 1u, b);
             cur_optlen = (b + 1u) << 3;
             must_align = true;
             const int r = walk_dst(h, avail, e);
-            if (r == -2) return WALK_BAD;
-            if (r < 0) return WALK_DROP;
+            if (r == -2) return (uint32_t)(WALK_BAD + 1);
+            if (r < 0) return (uint32_t)(WALK_DROP + 1);
         } else {                                                    // ESP, AUTH, none, invalid
-            return WALK_DROP;
+            return (uint32_t)(WALK_DROP + 1);
         }
-        if (net_len + cur_optlen > 0xFFFFu) return WALK_BAD;        // the uint16 would wrap
+        if (net_len + cur_optlen > 0xFFFFu) return (uint32_t)(WALK_BAD + 1);        // the uint16 would wrap
         net_len += cur_optlen;
         WBYTE(e, nx);                                               // exthdr->nxthdr (:805)
         cur_nexthdr = ptr;
@@ -620,9 +619,12 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                     // RX with extension headers and no seed: walk them here, as
                     // pico_ipv6_extension_headers does (ipv6_walk)
                     if (!tx && proto != 6u && proto != 17u && proto != 58u) {
-                        const int k = ipv6_walk(p.base + off, avail, net_len, proto);
+                        const uint32_t w = ipv6_walk_packed(p.base + off, avail);
+                        const int k = (int)(w & 0xFFu) - 1;
                         if (k == WALK_FRAG) post = PV_FRAG;
-                        else walked = k == WALK_PROTO;
+                        walked = k == WALK_PROTO;
+                        net_len = (w >> 8) & 0xFFFFu;
+                        proto = w >> 24;
                     }
                 }
                 tl = (plen - (net_len - 40u)) & 0xFFFFu;                // pico_ipv6.c:790
@@ -705,26 +707,31 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
             }
             return v;
         };
+        // Only the chunks that hold region bytes count: a region can end well before the window
+        // part does (a UDP / ICMPv6 transport shorter than the field the reference reads: ext >
+        // span), so the last counted chunk is the one holding the region's last byte.
+        const bool wreg = k0 != 0u && re > rs;
+        const uint32_t we1 = wreg ? (re - 1u) >> 4 : 0u;
         auto window_sums = [&](auto perm_tag) {
             constexpr bool PERM = decltype(perm_tag)::value;
 #pragma unroll
             for (uint32_t i = 0; i < HW; ++i) {
                 const uint32_t c = add_full<PERM>(hw[i], sl, 0u);
-                p_all += (i >= d && i < d + k0) ? c : 0u;
+                p_all += (wreg && i >= d && i <= we1) ? c : 0u;
             }
-            if (__builtin_amdgcn_ballot_w64(k0 != 0u)) {
-                const uint32_t e0 = k0 ? d : 0u, e1 = k0 ? d + k0 - 1u : 0u;
+            if (__builtin_amdgcn_ballot_w64(wreg)) {
+                const uint32_t e0 = wreg ? d : 0u, e1 = we1;
                 uint4 h0, h1;
-                if (__builtin_amdgcn_ballot_w64(k0 != 0u && !staged) == 0) {
+                if (__builtin_amdgcn_ballot_w64(wreg && !staged) == 0) {
                     h0 = stage[lane * HW + (e0 ^ (lane & (HW - 1)))];
                     h1 = stage[lane * HW + (e1 ^ (lane & (HW - 1)))];
                 } else {
                     h0 = edge_chunk(e0);
                     h1 = edge_chunk(e1);
                 }
-                if (k0) {
+                if (wreg) {
                     p_all -= masked_chunk_sum<PERM>(h0, 16u * e0, 16u * e0, rs, sl);
-                    p_all -= masked_chunk_sum<PERM>(h1, 16u * e1, re, P, sl);
+                    p_all -= masked_chunk_sum<PERM>(h1, 16u * e1, re, 16u * (e1 + 1u), sl);
                 }
             }
         };

@@ -7,7 +7,7 @@ O=$R/gpurun_out
 TAG=${1:-run}
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
     > $O/pytest_gpu_$TAG.log 2>&1
 echo "pytest ok"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1

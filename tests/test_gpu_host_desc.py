@@ -95,3 +95,52 @@ def test_frame_larger_than_staging_is_einval(hb):
     with pytest.raises(_lib.PicoCsumError) as e:
         hb.checksum_batch(buf, d)
     assert e.value.rc == -_lib.EINVAL
+
+
+def _packed_small_frames(n, seed):
+    """Frames packed back to back (no gaps), 8..200 B, so most start off a 16-byte line and
+    chunk boundaries fall inside 16-byte lines shared by two frames."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(8, 200, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+    buf = synth.random_bytes(seed, int(offs[-1]) + int(lens[-1]))
+    return buf, offs, lens, rng
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_write_packed_unaligned_and_shuffled(hb, shuffle):
+    """F_WRITE on a packed burst (crc at offset 6, as a UDP header) spanning many chunks, in
+    ascending order and with the descriptors shuffled: every crc field holds its frame's value
+    and no other byte changes."""
+    buf, offs, lens, rng = _packed_small_frames(40_000, 71 + shuffle)
+    order = rng.permutation(lens.size) if shuffle else np.arange(lens.size)
+    d = batch.make_desc(offs[order], lens[order])
+    orig = buf.copy()
+    want = O.batch_raw(orig, d, crc_off=6)
+    out = hb.checksum_batch(buf, d, crc_off=6, flags=_lib.F_WRITE)
+    np.testing.assert_array_equal(out, want)
+    has = d["len"] >= 8
+    o = d["off"][has].astype(np.int64)
+    exp = orig.copy()
+    exp[o + 6] = (want[has] >> 8).astype(np.uint8)
+    exp[o + 7] = (want[has] & 0xFF).astype(np.uint8)
+    np.testing.assert_array_equal(buf, exp)
+
+
+def test_oversized_frame_mid_burst_with_write_changes_nothing(hb):
+    """A frame larger than the staging buffer in the middle of an F_WRITE burst: -EINVAL before
+    anything is queued -- no byte of the caller's buffer changes, before or after the return."""
+    buf, offs, lens, _ = _packed_small_frames(20_000, 5)
+    big = np.zeros(3 << 20, np.uint8)
+    full = np.concatenate([buf, big])
+    offs = np.concatenate([offs[:10_000], [buf.size], offs[10_000:]]).astype(np.uint64)
+    lens = np.concatenate([lens[:10_000], [2 << 20], lens[10_000:]]).astype(np.uint32)
+    d = batch.make_desc(offs, lens)
+    before = full.copy()
+    with pytest.raises(_lib.PicoCsumError) as e:
+        hb.checksum_batch(full, d, crc_off=6, flags=_lib.F_WRITE)
+    assert e.value.rc == -_lib.EINVAL
+    np.testing.assert_array_equal(full, before)
+    import time
+    time.sleep(0.2)                                  # nothing still in flight lands later
+    np.testing.assert_array_equal(full, before)

@@ -426,3 +426,47 @@ def test_c2_full_size_tx_compute():
     np.testing.assert_array_equal(wb[ip + 11], (want[0] & 0xFF).astype(np.uint8))
     np.testing.assert_array_equal(wb[ip + 20 + 16], (want[1] >> 8).astype(np.uint8))
     np.testing.assert_array_equal(wb[ip + 20 + 17], (want[1] & 0xFF).astype(np.uint8))
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_short_transports_every_alignment(v6):
+    """Transports shorter than the field the reference reads (UDP tl < 8: the crc at 6-7 lies
+    past the region; ICMPv6 tl 1-3), at every start alignment: the region sum must stop at the
+    region's end even when the head window reads further (regression: r03 fuzz)."""
+    rng = np.random.default_rng(606 + v6)
+    parts, offs, avs, pos = [], [], [], 0
+    for a in range(16):
+        for tl in range(0, 12):
+            for proto in ((17, 58, 6) if v6 else (17, 6)):
+                hl = 40 if v6 else 20
+                d = bytearray(rng.integers(0, 256, hl + max(tl, 8) + 8).astype(np.uint8).tobytes())
+                if v6:
+                    d[0], d[4], d[5], d[6], d[9] = 0x60, 0, tl, proto, proto
+                else:
+                    d[0], d[2], d[3], d[6], d[7], d[9] = 0x45, 0, hl + tl, 0x40, 0, proto
+                    d[12] = 10
+                    d[10:12] = b"\0\0"
+                    c = O.checksum(bytes(d[:20]))
+                    d[10], d[11] = c >> 8, c & 0xFF
+                pos += (a - pos) % 16
+                offs.append(pos)
+                avs.append(len(d))
+                parts.append((pos, bytes(d)))
+                pos += len(d)
+    buf = np.zeros(pos + 16, np.uint8)
+    for o, d in parts:
+        buf[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    desc = batch.make_desc(np.array(offs, np.uint64), np.array(avs, np.uint32))
+    d_desc = batch.desc_to_device(desc, DEV)
+    for fpw in (None, 1, 64):
+        use_kernel("auto" if fpw is None else f"fpw{fpw}")
+        if v6:
+            wl, wv = O.batch_ipv6(buf, desc)
+            l4, v = batch.ipv6_checksum_batch(to_dev(buf), d_desc, len(offs))
+        else:
+            wn, wl, wv = O.batch_ipv4(buf, desc)
+            net, l4, v = batch.ipv4_checksum_batch(to_dev(buf), d_desc, len(offs))
+            np.testing.assert_array_equal(u16(net), wn)
+        np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg=f"fpw={fpw}")
+        np.testing.assert_array_equal(u16(l4), wl, err_msg=f"fpw={fpw}")
+    assert (wv == 4).sum() > 100
