@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
@@ -12,6 +12,7 @@ A step = one pass of the hot path over one batch resident in HBM:
   c2eth: the C2 frames through the Ethernet front end (one launch: ethertype dispatch + RX verify)
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
   c3_reasm: 4K x 64512 B datagrams reassembled from 1480 B fragments + TCP check in the same pass
+  c3_reasm6: the same for IPv6 (1448 B fragments behind a fragment header)
   c3: 256K x 9000 B jumbo frames;  c3_64k: 16K x 64 KiB reassembled buffers
   c4: 4M x 1500 B frames sharded over the ranks (strong scaling)
 c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame batches
@@ -77,6 +78,11 @@ CONFIGS = {
                      workload="C3 reassembly (SURVEY 8f row 4): 4K x 64512 B IPv4/TCP datagrams arriving as 1480 B "
                               "fragments (44 per datagram, 14 B Ethernet gap each), gathered into reassembled "
                               "buffers with the TCP pseudo-header check of each datagram in the same pass"),
+    "c3_reasm6": dict(kind="frag", frames=4096, frame_bytes=64512, v6=True,
+                      workload="C3 reassembly, IPv6 (SURVEY 8f row 4): 4K x 64512 B IPv6/TCP datagrams arriving as "
+                               "1448 B fragments (45 per datagram, 40 B header + 8 B fragment header, 14 B Ethernet "
+                               "gap each), each fragment's extension headers walked, gathered into reassembled "
+                               "buffers with the TCP pseudo-header check of each datagram in the same pass"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -161,49 +167,66 @@ def make_c2eth(n, device, seed, keep_host=True):
     return d_buf, d_desc, int(lens.sum()) + 14 * n, (buf, desc) if keep_host else None
 
 
-FRAG = 1480                 # fragment payload (MTU 1500 - 20 B header)
+FRAG = 1480                 # IPv4 fragment payload (MTU 1500 - 20 B header)
+FRAG6 = 1448                # IPv6 fragment payload (MTU 1500 - 40 B header - 8 B fragment header, 8-aligned)
 
 
-def make_frag(n, tl, device, seed):
-    """n IPv4/TCP datagrams of tl transport bytes as in-order 1480 B fragments, each behind a
-    14 B gap, built on the device (vectorized); the TCP checksum made valid with one untimed
-    reassembly pass.  Returns (buffer, fragment descriptors, groups, out, out descriptors,
-    fragment count, payload bytes)."""
-    nf = -(-tl // FRAG)
-    pl = np.full(nf, FRAG, np.int64)
-    pl[-1] = tl - FRAG * (nf - 1)
-    fsz = 14 + 20 + pl                                   # bytes per fragment slot
+def make_frag(n, tl, device, seed, v6=False):
+    """n IPv4/TCP (IPv6/TCP) datagrams of tl transport bytes as in-order 1480 B (1448 B)
+    fragments, each behind a 14 B gap, built on the device (vectorized); the TCP checksum made
+    valid with one untimed reassembly pass.  Returns (buffer, fragment descriptors, groups, out,
+    out descriptors, fragment count, payload bytes)."""
+    fr, hl = (FRAG6, 48) if v6 else (FRAG, 20)
+    nf = -(-tl // fr)
+    pl = np.full(nf, fr, np.int64)
+    pl[-1] = tl - fr * (nf - 1)
+    fsz = 14 + hl + pl                                   # bytes per fragment slot
     per = int(fsz.sum())
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     buf = torch.randint(0, 256, (n * per,), dtype=torch.uint8, device=device, generator=g)
     rel = np.concatenate([[0], np.cumsum(fsz)[:-1]]) + 14          # header offsets in one datagram
     net = (np.arange(n, dtype=np.int64)[:, None] * per + rel[None, :]).reshape(-1)
-    hdr = np.zeros((n, nf, 20), np.uint8)
-    tot = 20 + pl
-    hdr[:, :, 0] = 0x45
-    hdr[:, :, 2], hdr[:, :, 3] = (tot >> 8)[None, :], (tot & 0xFF)[None, :]
-    ident = (np.arange(n) * 7 + seed) & 0xFFFF
-    hdr[:, :, 4], hdr[:, :, 5] = (ident >> 8)[:, None], (ident & 0xFF)[:, None]
-    frag = ((np.arange(nf) * FRAG) >> 3) | np.where(np.arange(nf) < nf - 1, 0x2000, 0)
-    hdr[:, :, 6], hdr[:, :, 7] = (frag >> 8)[None, :], (frag & 0xFF)[None, :]
-    hdr[:, :, 8], hdr[:, :, 9] = 64, 6
-    hdr[:, :, 12:16] = [10, 1, 2, 3]
-    hdr[:, :, 16:20] = [192, 168, 4, 5]
-    idx = torch.from_numpy((net[:, None] + np.arange(20)[None, :]).reshape(-1)).to(device)
+    hdr = np.zeros((n, nf, hl), np.uint8)
+    tot = hl + pl
+    if v6:
+        plen = 8 + pl
+        hdr[:, :, 0] = 0x60
+        hdr[:, :, 4], hdr[:, :, 5] = (plen >> 8)[None, :], (plen & 0xFF)[None, :]
+        hdr[:, :, 6], hdr[:, :, 7] = 44, 64
+        hdr[:, :, 8:24] = [0x20, 6, 0x0d, 0xb8, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 1]   # byte 9 = 6 (TCP)
+        hdr[:, :, 24:40] = [0x20, 1, 0x0d, 0xb8, 0, 0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 2]
+        om = np.arange(nf) * fr | np.where(np.arange(nf) < nf - 1, 1, 0)
+        hdr[:, :, 40], hdr[:, :, 42], hdr[:, :, 43] = 6, (om >> 8)[None, :], (om & 0xFF)[None, :]
+        ident = np.arange(n, dtype=np.int64) * 7 + seed
+        for k in range(4):
+            hdr[:, :, 44 + k] = ((ident >> (24 - 8 * k)) & 0xFF)[:, None]
+    else:
+        hdr[:, :, 0] = 0x45
+        hdr[:, :, 2], hdr[:, :, 3] = (tot >> 8)[None, :], (tot & 0xFF)[None, :]
+        ident = (np.arange(n) * 7 + seed) & 0xFFFF
+        hdr[:, :, 4], hdr[:, :, 5] = (ident >> 8)[:, None], (ident & 0xFF)[:, None]
+        frag = ((np.arange(nf) * fr) >> 3) | np.where(np.arange(nf) < nf - 1, 0x2000, 0)
+        hdr[:, :, 6], hdr[:, :, 7] = (frag >> 8)[None, :], (frag & 0xFF)[None, :]
+        hdr[:, :, 8], hdr[:, :, 9] = 64, 6
+        hdr[:, :, 12:16] = [10, 1, 2, 3]
+        hdr[:, :, 16:20] = [192, 168, 4, 5]
+    idx = torch.from_numpy((net[:, None] + np.arange(hl)[None, :]).reshape(-1)).to(device)
     buf[idx] = torch.from_numpy(hdr.reshape(-1)).to(device)
-    crc = torch.from_numpy(np.stack([net[::nf] + 20 + 16, net[::nf] + 20 + 17], 1).reshape(-1)).to(device)
+    crc = torch.from_numpy(np.stack([net[::nf] + hl + 16, net[::nf] + hl + 17], 1).reshape(-1)).to(device)
     buf[crc] = 0                                         # TCP crc of each datagram (first fragment)
     desc = batch.make_desc(net.astype(np.uint64), np.repeat(tot[None, :], n, 0).reshape(-1))
     grp = np.stack([np.arange(n) * nf, np.full(n, nf)], 1).astype(np.uint32).reshape(-1)
-    cap = (20 + tl + 15) // 16 * 16 + 16
-    # each reassembled datagram at 12 mod 16, so that its transport (behind the 20 B header) is
-    # 16-byte aligned: the gather then stores whole 16-byte units wherever a fragment's place is
-    od = batch.make_desc(np.arange(n, dtype=np.uint64) * cap + np.uint64(12), np.full(n, cap - 12))
+    H = 40 if v6 else 20
+    cap = (H + tl + 15) // 16 * 16 + 16
+    # each reassembled datagram at (16 - H % 16) mod 16, so that its transport (behind the H B
+    # header) is 16-byte aligned: the gather then stores whole 16-byte units
+    od = batch.make_desc(np.arange(n, dtype=np.uint64) * cap + np.uint64(8 if v6 else 12), np.full(n, cap - 12))
     d_desc, d_od = batch.desc_to_device(desc, device), batch.desc_to_device(od, device)
     d_grp = torch.from_numpy(grp.view(np.int32)).to(device)
     out = torch.empty(n * cap, dtype=torch.uint8, device=device)
-    _, l4, _ = batch.ipv4_reassemble_batch(buf, d_desc, n * nf, d_grp, out, d_od)
+    fn = batch.ipv6_reassemble_batch if v6 else batch.ipv4_reassemble_batch
+    _, l4, _ = fn(buf, d_desc, n * nf, d_grp, out, d_od)
     c = l4.view(torch.int16).to(torch.int32) & 0xFFFF                # value to store: short_be(c)
     buf[crc[0::2]] = (c >> 8).to(torch.uint8)
     buf[crc[1::2]] = (c & 0xFF).to(torch.uint8)
@@ -288,11 +311,12 @@ def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float):
                       f"{'TX' if tx else 'RX'} restatement, gcc -O3, 1 thread, {reps} passes"}
 
 
-def cpu_baseline_frag(st, target_s: float):
+def cpu_baseline_frag(st, target_s: float, v6: bool = False):
     """The oracle's reassembly restatement (memcpy gather + pico_checksum of the reassembled
     transport, as pico_fragments_reassemble + pico_transport_crc_check do) on 1 host core
     over the first 256 datagrams of the batch."""
     from oracle import oracle as O
+    fn = O.ipv6_reassemble if v6 else O.ipv4_reassemble
     b, d, gr, o, od, nfr, payload = st
     n = gr.numel() // 2
     k = min(n, 256)
@@ -305,15 +329,16 @@ def cpu_baseline_frag(st, target_s: float):
     outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
     nbytes = payload // n * k
     t0 = time.perf_counter()
-    O.ipv4_reassemble(host, desc, grp, outh, odh)
+    fn(host, desc, grp, outh, odh)
     reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))
     t0 = time.perf_counter()
     for _ in range(reps):
-        O.ipv4_reassemble(host, desc, grp, outh, odh)
+        fn(host, desc, grp, outh, odh)
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload), oracle reassembly restatement "
-                      f"(sort, memcpy gather, pico_checksum of the transport), gcc -O3, 1 thread, {reps} passes"}
+            "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload), oracle {'IPv6' if v6 else 'IPv4'} "
+                      f"reassembly restatement (sort, memcpy gather, pico_checksum of the transport), gcc -O3, "
+                      f"1 thread, {reps} passes"}
 
 
 def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
@@ -342,16 +367,19 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
         hi = int(desc["off"][-1]) + int(desc["len"][-1])
         odh = od.cpu().numpy().view(batch.DESC_DTYPE)[:k]
         outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
-        wl, wl4, wv = O.ipv4_reassemble(b[:hi].cpu().numpy(), desc, grp, outh, odh)
+        v6 = bool(cfg.get("v6"))
+        H = 40 if v6 else 20
+        wl, wl4, wv = (O.ipv6_reassemble if v6 else O.ipv4_reassemble)(b[:hi].cpu().numpy(), desc, grp, outh, odh)
         gl, gl4, gv = (x.cpu().numpy()[:k] for x in out)
         gout = o[:outh.size].cpu().numpy()
         bad = int(((gl.view(np.uint32) != wl) | (gl4.view(np.uint16) != wl4) | (gv != wv)).sum())
         for g in range(k):
             if wl[g]:
                 a = int(odh["off"][g])
-                bad += int(not np.array_equal(gout[a:a + 20 + int(wl[g])], outh[a:a + 20 + int(wl[g])]))
+                bad += int(not np.array_equal(gout[a:a + H + int(wl[g])], outh[a:a + H + int(wl[g])]))
         frames = k
-        what = "first 256 datagrams: lengths, checksums, verdicts and reassembled bytes vs oracle_ipv4_reassemble"
+        what = (f"first 256 datagrams: lengths, checksums, verdicts and reassembled bytes vs "
+                f"oracle_ipv{6 if v6 else 4}_reassemble")
     else:
         b, d = slot[0], slot[1]
         hbuf, hdesc = host
@@ -568,18 +596,23 @@ def main():
     elif cfg["kind"] == "frag":
         n, ln = cfg["frames"], cfg["frame_bytes"]
         rot = a.rotate or max(2, rotation(2 * n * ln))
-        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i) for i in range(rot)]
+        v6 = bool(cfg.get("v6"))
+        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6) for i in range(rot)]
         res = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 
         def step(i):
             b, d, gr, o, od, nfr, _ = sets[i % rot]
-            batch.ipv4_reassemble_batch(b, d, nfr, gr, o, od, results=res[i % rot])
+            if v6:
+                batch.ipv6_reassemble_batch(b, d, nfr, gr, o, od, results=res[i % rot])
+            else:
+                batch.ipv4_reassemble_batch(b, d, nfr, gr, o, od, results=res[i % rot])
         frame_bytes = sets[0][6]
         nfr = sets[0][5]
-        # payload read + written, fragment headers (20 B) + descriptors (16 B) read, 2 x 4 B group,
-        # 20 B header written, (4+2+1) B results
-        algo_bytes = 2 * frame_bytes + 36 * nfr + 8 * n + 20 * n + 7 * n
+        # payload read + written, fragment headers (20 B / 48 B) + descriptors (16 B) read,
+        # 2 x 4 B group, 20 B / 40 B header written, (4+2+1) B results
+        hl, H = (48, 40) if v6 else (20, 20)
+        algo_bytes = 2 * frame_bytes + (hl + 16) * nfr + 8 * n + H * n + 7 * n
     else:
         n = cfg["frames"]
         ln = 0
@@ -704,7 +737,7 @@ def main():
             out["e2e_host_to_host"] = e2e_rate_desc(sets[0][3])
     elif rank == 0 and world == 1 and cfg["kind"] == "frag":
         if not a.no_cpu:
-            out["cpu_baseline"] = cpu_baseline_frag(sets[0], a.cpu_seconds / 2)
+            out["cpu_baseline"] = cpu_baseline_frag(sets[0], a.cpu_seconds / 2, bool(cfg.get("v6")))
         out["roofline"]["copy_ceiling"] = copy_ceiling(sets[0][6], dev)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -258,6 +258,27 @@ int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const 
                                    uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
                                    uint16_t *d_out_transport, uint8_t *d_verdict, void *stream);
 
+/* IPv6 fragment reassembly fused with the transport check of the reassembled datagram
+ * (pico_ipv6_process_frag / pico_fragments_check_complete /
+ * pico_fragments_reassemble, modules/pico_fragments.c:73-83,216-239,304-358,432-498).  Arguments
+ * as pico_ipv4_reassemble_batch_dev, with d_frag[] -> each fragment's IPv6 header (desc.len =
+ * bytes available; desc.seed reserved, 0): the kernel walks each fragment's extension headers as
+ * pico_ipv6_extension_headers does (pico_ipv6.c:659-809) -- the transport must lie behind a
+ * fragment header -- for net_len, the fragment field (offset = frag & 0xFFF8, more = frag & 1,
+ * pico_fragments.c:35-36) and the transport protocol; transport_len = payload_len - (net_len - 40)
+ * (pico_ipv6.c:790).  The output is the first fragment's 40-byte fixed header (its extension
+ * headers are not copied, :334-338) followed by every payload (out_desc.off = 8 mod 16 puts the
+ * transport on a 16-byte line).  The check of the reassembled datagram follows the module the
+ * completing fragment hands it to (its transport protocol): TCP / UDP through
+ * pico_transport_crc_check with the reference's byte-9 dispatch on the copied header
+ * (PICO_CSUM_F_NXTHDR_DISPATCH: by the module instead), ICMPv6 through pico_icmp6_checksum (a
+ * verdict for the ND / MLD types only).  Verdicts and the unspecified-bytes rule as for IPv4
+ * (40 + len > 65535 and a fragment that does not walk to a fragment header are MALFORMED). */
+int pico_ipv6_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
+                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
+                                   uint16_t *d_out_transport, uint8_t *d_verdict, uint32_t flags, void *stream);
+
 /* ---------------------------------------------------------------- layer 3 */
 
 struct pico_csum_ctx;   /* device, two streams, double-buffered staging */

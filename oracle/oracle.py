@@ -71,6 +71,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_batch_eth.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]
         L.oracle_ipv4_reassemble.restype = None
         L.oracle_ipv4_reassemble.argtypes = [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
+        L.oracle_ipv6_reassemble.restype = None
+        L.oracle_ipv6_reassemble.argtypes = [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32]
+        L.oracle_ipv6_walk_frag.restype = ctypes.c_int
+        L.oracle_ipv6_walk_frag.argtypes = [_vp, _u32, _vp, _vp, _vp]
         L.oracle_batch_ipv4_forward.restype = None
         L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
@@ -176,6 +180,27 @@ def ipv4_reassemble(base: np.ndarray, desc: np.ndarray, groups: np.ndarray, out:
     lib().oracle_ipv4_reassemble(_p(base), _p(desc), desc.shape[0], _p(grp), ng, _p(out), _p(od), _p(ol), _p(l4),
                                  _p(v))
     return ol, l4, v
+
+
+def ipv6_reassemble(base: np.ndarray, desc: np.ndarray, groups: np.ndarray, out: np.ndarray, out_desc: np.ndarray,
+                    nxthdr_dispatch: bool = False):
+    """oracle_ipv6_reassemble: writes into `out` (uint8, writable); returns (out_len, out_l4, verdict)."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    od = np.ascontiguousarray(out_desc, dtype=DESC_DTYPE)
+    grp = np.ascontiguousarray(groups, dtype=np.uint32).reshape(-1)
+    ng = grp.size // 2
+    ol, l4, v = np.zeros(ng, np.uint32), np.zeros(ng, np.uint16), np.zeros(ng, np.uint8)
+    lib().oracle_ipv6_reassemble(_p(base), _p(desc), desc.shape[0], _p(grp), ng, _p(out), _p(od), _p(ol), _p(l4),
+                                 _p(v), ORACLE_NXTHDR_DISPATCH if nxthdr_dispatch else 0)
+    return ol, l4, v
+
+
+def ipv6_walk_frag(dgram) -> tuple:
+    """oracle_ipv6_walk_frag: (kind, net_len, proto, frag field)."""
+    a = _buf(dgram)
+    nl, pr, om = ctypes.c_uint32(0), ctypes.c_uint8(0), ctypes.c_uint16(0)
+    k = lib().oracle_ipv6_walk_frag(_p(a), a.size, ctypes.byref(nl), ctypes.byref(pr), ctypes.byref(om))
+    return k, nl.value, pr.value, om.value
 
 
 def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:

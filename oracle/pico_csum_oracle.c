@@ -356,6 +356,14 @@ static int walk_destopt(const uint8_t *h, uint32_t avail, uint32_t e)
  */
 int oracle_ipv6_walk(const uint8_t *h, uint32_t avail, uint32_t *net_len_out, uint8_t *proto_out)
 {
+    uint16_t om;
+    return oracle_ipv6_walk_frag(h, avail, net_len_out, proto_out, &om);
+}
+
+/* oracle_ipv6_walk, also returning f->frag (the last fragment header's offset / M field, :754) */
+int oracle_ipv6_walk_frag(const uint8_t *h, uint32_t avail, uint32_t *net_len_out, uint8_t *proto_out,
+                          uint16_t *frag_out)
+{
     uint32_t plen, ptr, iter, cur_nexthdr;
     uint16_t net_len;
     uint8_t nx, b;
@@ -425,7 +433,7 @@ int oracle_ipv6_walk(const uint8_t *h, uint32_t avail, uint32_t *net_len_out, ui
             net_len = (uint16_t)(net_len + 8u);
             WALK_BYTE(e + 2, om0);
             WALK_BYTE(e + 3, om1);
-            (void)om0;                                        /* f->frag = om0 << 8 | om1: M = bit 0 */
+            *frag_out = (uint16_t)((om0 << 8) + om1);         /* f->frag, :754 (M = bit 0) */
             frag = 1;
             if ((om1 & 1u) && (plen % 8u) != 0) return ORACLE_WALK_DROP;
             break;
@@ -629,44 +637,59 @@ void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint3
 }
 
 /*
- * IPv4 fragment reassembly with the transport check of the reassembled datagram
- * (SURVEY.md 8f row 4).  Fragments arrive as pico_ipv4_process_in hands them to
- * pico_ipv4_process_frag (modules/pico_ipv4.c:381-450: f->transport_len = tot - net_len,
- * f->frag = short_be(hdr->frag)); group g = fragments grp[2g] .. grp[2g] + grp[2g+1] - 1 of
- * one datagram (src, dst, id matched by the stack, pico_fragments.c:499-568), in arrival
- * order.  Per group:
- *   tree order     pico_ipv4_frag_compare (pico_fragments.c:129-139): by offset
- *                  IP4_FRAG_OFF = (frag & 0x1FFF) << 3; pico_tree_insert rejects a second
- *                  fragment with the same offset, so the earlier arrival is kept
+ * Fragment reassembly with the transport check of the reassembled datagram,
+ * IPv4 and IPv6.  Group g = fragments grp[2g] .. grp[2g] + grp[2g+1] - 1 of one datagram (src,
+ * dst, id matched by the stack, pico_fragments.c:104-178, 432-568), in arrival order.
+ * Per fragment:
+ *   IPv4  as pico_ipv4_process_in hands it on (modules/pico_ipv4.c:381-450): net_len = 20 +
+ *         4 (IHL - 5), f->transport_len = (uint16)(tot - net_len), f->frag = short_be(hdr->frag);
+ *         offset IP4_FRAG_OFF = (frag & 0x1FFF) << 3, more = frag & 0x2000 (pico_fragments.c:46-49)
+ *   IPv6  as pico_ipv6_extension_headers hands it on (modules/pico_ipv6.c:707-809, the walk of
+ *         oracle_ipv6_walk): the transport must be reached behind a fragment header (else the
+ *         reference never reassembles it: MALFORMED); net_len = the walk's, f->transport_len =
+ *         (uint16)(payload_len - (net_len - 40)) (:790), f->frag = that header's offset / M
+ *         field; offset IP6_FRAG_OFF = frag & 0xFFF8, more = frag & 1 (pico_fragments.c:35-36);
+ *         the module it goes to (pico_ipv6_process_frag's proto) = the walk's transport protocol
+ * Per group:
+ *   tree order     by offset (pico_ipv4/6_frag_compare, pico_fragments.c:73-83, 129-139);
+ *                  pico_tree_insert rejects a repeated offset: the earlier arrival is kept
  *   completeness   pico_fragments_check_complete (:216-239): offsets contiguous from 0
- *                  (offset == sum of the previous transport_len), up to the first
- *                  fragment without PICO_IPV4_MOREFRAG; len = that sum
- *   gather         pico_fragments_reassemble (:304-358): PICO_SIZE_IP4HDR (20) header
- *                  bytes of the first fragment, then every fragment's transport bytes
- *   transport      pico_transport_crc_check (stack/pico_socket.c:1916-1968) with
- *                  net_hdr->proto of the copied header: TCP always, UDP when its crc != 0;
- *                  pseudo header from the copied header, transport_len = len
- * out_len[g] = len (0 when not reassembled), out_l4[g] = the checksum (0 = valid; 0 when
- * none), verdict[g] = ACCEPT / L4_BAD, or MALFORMED when not reassembled: incomplete, a
- * fragment behind the completing one (the reference's copy loop, :339-345, would write
- * past its 20 + len byte buffer), 20 + len > 65535 (its (uint16_t) allocation size wraps),
- * a fragment whose header or transport lies past desc.len, an empty group or one of more
- * than 512 fragments (the API's limit), or an output
- * region (out_desc[g].len) shorter than 20 + len or not 4-byte aligned (the API's contract).
+ *                  (offset == sum of the previous transport_len), up to the first fragment
+ *                  without "more"; len = that sum.  The set completes at the arrival of the last
+ *                  of those fragments, whose protocol pico_fragments_reassemble hands on.
+ *   gather         pico_fragments_reassemble (:304-358): the first fragment's PICO_SIZE_IP4HDR
+ *                  (20) / PICO_SIZE_IP6HDR (40) bytes, then every fragment's transport bytes
+ *   transport      IPv4: pico_transport_crc_check (stack/pico_socket.c:1916-1968) with
+ *                  net_hdr->proto of the copied header: TCP always, UDP when its crc != 0 (and
+ *                  the datagram holds the 8-byte UDP header), pseudo header from the copied
+ *                  header, transport_len = len.
+ *                  IPv6: the module of the completing fragment -- TCP / UDP: the same check,
+ *                  dispatched on byte 9 of the copied header as the reference does (with
+ *                  ORACLE_NXTHDR_DISPATCH: on the module), pseudo header = struct
+ *                  pico_ipv6_pseudo_hdr of the copied header; ICMPv6: pico_icmp6_checksum, a
+ *                  verdict only for the ND / MLD types (pico_icmp6_process_in); others: none.
+ * out_len[g] = len (0 when not reassembled), out_l4[g] = the checksum (0 = valid; 0 when none),
+ * verdict[g] = ACCEPT / L4_BAD, or MALFORMED when not reassembled: incomplete, a fragment behind
+ * the completing one (the reference's copy loop, :339-345, would write past its HDR + len byte
+ * buffer), HDR + len > 65535 (its (uint16_t) allocation size wraps), a fragment whose header or
+ * transport lies past desc.len, an empty group or one of more than 512 fragments (the API's
+ * limit), or an output region (out_desc[g].len) shorter than HDR + len or not 4-byte aligned
+ * (the API's contract).
  */
-void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
-                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
-                            uint8_t *verdict)
+static void oracle_reassemble(int v6, const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd,
+                              const uint32_t *grp, uint32_t ng, uint8_t *out, const struct pico_csum_desc *od,
+                              uint32_t *out_len, uint16_t *out_l4, uint8_t *verdict, uint32_t flags)
 {
+    const uint32_t HDR = v6 ? 40u : 20u;
     uint32_t g;
     for (g = 0; g < ng; g++) {
-        uint32_t first = grp[2 * g], cnt = grp[2 * g + 1], i, k, m = 0, len = 0, bad = 0, e = 0, done = 0;
+        uint32_t first = grp[2 * g], cnt = grp[2 * g + 1], i, k, m = 0, len = 0, bad = 0, e = 0, done = 0, comp = 0;
         uint32_t na = cnt && cnt <= 512 ? cnt : 1;
         uint32_t *ord = (uint32_t *)malloc(sizeof(uint32_t) * na);
         uint32_t *foff = (uint32_t *)malloc(sizeof(uint32_t) * na);
         uint32_t *tl = (uint32_t *)malloc(sizeof(uint32_t) * na);
         uint32_t *hlen = (uint32_t *)malloc(sizeof(uint32_t) * na);
-        uint8_t *mf = (uint8_t *)malloc(na);
+        uint8_t *mf = (uint8_t *)malloc(na), *pr = (uint8_t *)malloc(na);
         out_len[g] = 0;
         out_l4[g] = 0;
         verdict[g] = PICO_CSUM_V_MALFORMED;
@@ -675,14 +698,30 @@ void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
         for (i = 0; i < cnt && !bad; i++) {
             const struct pico_csum_desc *f = &d[first + i];
             const uint8_t *h = base + f->off;
-            uint32_t ihl, frag;
-            if (f->len < 20) { bad = 1; break; }
-            ihl = h[0] & 0x0Fu;
-            hlen[i] = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-            tl[i] = (uint16_t)(((h[2] << 8) | h[3]) - hlen[i]);
-            frag = (uint32_t)((h[6] << 8) | h[7]);
-            foff[i] = (frag & 0x1FFFu) << 3;
-            mf[i] = (frag & 0x2000u) != 0;
+            if (!v6) {
+                uint32_t ihl, frag;
+                if (f->len < 20) { bad = 1; break; }
+                ihl = h[0] & 0x0Fu;
+                hlen[i] = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                tl[i] = (uint16_t)(((h[2] << 8) | h[3]) - hlen[i]);
+                frag = (uint32_t)((h[6] << 8) | h[7]);
+                foff[i] = (frag & 0x1FFFu) << 3;
+                mf[i] = (frag & 0x2000u) != 0;
+                pr[i] = h[9];
+            } else {
+                uint32_t nl = 0;
+                uint8_t proto = 0;
+                uint16_t om = 0;
+                if (f->len < 40 || oracle_ipv6_walk_frag(h, f->len, &nl, &proto, &om) != ORACLE_WALK_FRAG) {
+                    bad = 1;
+                    break;
+                }
+                hlen[i] = nl;
+                tl[i] = (uint16_t)((((uint32_t)h[4] << 8) | h[5]) - (nl - 40u));
+                foff[i] = om & 0xFFF8u;
+                mf[i] = om & 1u;
+                pr[i] = proto;
+            }
             if (hlen[i] + tl[i] > f->len) bad = 1;
         }
         /* tree: insertion by offset, a repeated offset keeps the earlier arrival */
@@ -700,14 +739,14 @@ void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
         for (k = 0; k < m && !bad; k++) {
             if (foff[ord[k]] != len) break;
             len += tl[ord[k]];
+            if (ord[k] > comp) comp = ord[k];                /* the set completes at its last arrival */
             if (!mf[ord[k]]) { e = k; done = 1; break; }
         }
-        if (!bad && done && e + 1 == m && 20u + len <= 0xFFFFu && od[g].len >= 20u + len && (od[g].off & 3u) == 0) {
+        if (!bad && done && e + 1 == m && HDR + len <= 0xFFFFu && od[g].len >= HDR + len && (od[g].off & 3u) == 0) {
             uint8_t *dst = out + od[g].off;
             const uint8_t *h0 = base + d[first + ord[0]].off;
-            uint32_t at = 20, s;
-            uint8_t proto = h0[9];
-            memcpy(dst, h0, 20);
+            uint32_t at = HDR, s;
+            memcpy(dst, h0, HDR);
             for (k = 0; k < m; k++) {
                 const uint8_t *src = base + d[first + ord[k]].off + hlen[ord[k]];
                 memcpy(dst + at, src, tl[ord[k]]);
@@ -715,14 +754,47 @@ void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
             }
             out_len[g] = len;
             verdict[g] = PICO_CSUM_V_ACCEPT;
-            if (proto == 6 || (proto == 17 && len >= 8 && (dst[20 + 6] || dst[20 + 7]))) {
-                s = oracle_ipv4_pseudo_sum(dst + 12, dst + 16, proto, (uint16_t)len);
-                out_l4[g] = oracle_checksum_finalize(oracle_checksum_adder(s, dst + 20, len));
-                if (out_l4[g]) verdict[g] = PICO_CSUM_V_L4_BAD;
+            if (!v6) {
+                uint8_t proto = h0[9];
+                if (proto == 6 || (proto == 17 && len >= 8 && (dst[20 + 6] || dst[20 + 7]))) {
+                    s = oracle_ipv4_pseudo_sum(dst + 12, dst + 16, proto, (uint16_t)len);
+                    out_l4[g] = oracle_checksum_finalize(oracle_checksum_adder(s, dst + 20, len));
+                    if (out_l4[g]) verdict[g] = PICO_CSUM_V_L4_BAD;
+                }
+            } else {
+                uint8_t module = pr[comp], cp = module;
+                int check = 0;
+                if (module == 6 || module == 17) {
+                    if (!(flags & ORACLE_NXTHDR_DISPATCH))
+                        cp = dst[9];                          /* pico_socket.c:1923 through the IPv4 cast */
+                    check = cp == 6 || (cp == 17 && len >= 8 && (dst[40 + 6] || dst[40 + 7]));
+                } else if (module == 58 && len >= 1) {
+                    check = 1;
+                }
+                if (check) {
+                    s = oracle_ipv6_pseudo_sum(dst + 8, dst + 24, cp, len);
+                    out_l4[g] = oracle_checksum_finalize(oracle_checksum_adder(s, dst + 40, len));
+                    if (out_l4[g] && (module != 58 || icmp6_checked_type(dst[40])))
+                        verdict[g] = PICO_CSUM_V_L4_BAD;
+                }
             }
         }
-        free(ord); free(foff); free(tl); free(hlen); free(mf);
+        free(ord); free(foff); free(tl); free(hlen); free(mf); free(pr);
     }
+}
+
+void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
+                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
+                            uint8_t *verdict)
+{
+    oracle_reassemble(0, base, d, nd, grp, ng, out, od, out_len, out_l4, verdict, 0);
+}
+
+void oracle_ipv6_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
+                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
+                            uint8_t *verdict, uint32_t flags)
+{
+    oracle_reassemble(1, base, d, nd, grp, ng, out, od, out_len, out_l4, verdict, flags);
 }
 
 /* modules/pico_ipv4.c:1547-1556 (pico_ipv4_forward): hdr->ttl = (uint8_t)(hdr->ttl - 1);

@@ -34,6 +34,7 @@ struct pico_csum_desc {
 #define ORACLE_WALK_FRAG  2   /* transport reached behind a fragment header: handed to reassembly */
 #define ORACLE_WALK_BAD  -1   /* the reference would read past the frame, or never terminates */
 int oracle_ipv6_walk(const uint8_t *h, uint32_t avail, uint32_t *net_len, uint8_t *proto);
+int oracle_ipv6_walk_frag(const uint8_t *h, uint32_t avail, uint32_t *net_len, uint8_t *proto, uint16_t *frag);
 
 typedef uint16_t (*oracle_checksum_fn)(void *buf, uint32_t len);
 
@@ -56,6 +57,9 @@ void oracle_batch_eth(const uint8_t *base, const struct pico_csum_desc *d, uint3
 void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
                             uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
                             uint8_t *verdict);
+void oracle_ipv6_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
+                            uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
+                            uint8_t *verdict, uint32_t flags);
 void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
                          uint32_t n, uint16_t *out, uint32_t nthreads);

@@ -24,7 +24,14 @@
  *   protocol), 2 handed to pico_ipv6_process_frag; for 1 with TCP / UDP, bit 4 = the transport
  *   check (pico_transport_crc_check, with f->transport_hdr / transport_len as the walk set them)
  *   passed.
- * Callers (tests/golden/make_ref_rx.py) only pass datagrams whose reference reads stay inside
+ * rr_reasm(v6, base, offs, lens, n, out, cap, &len, &module, &check): the n fragments of one
+ *   datagram, in arrival order, through pico_ipv4_process_in / pico_ipv6_extension_headers with
+ *   the REAL pico_ipv4/6_process_frag (tree, completeness, pico_fragments_reassemble), the trees
+ *   reset first; returns 1 when pico_fragments_reassemble handed a datagram to
+ *   pico_transport_receive (its net_len + transport_len bytes copied to out, len =
+ *   transport_len, module = the protocol it was handed with, check = pico_transport_crc_check
+ *   on it for TCP / UDP, else -1), 0 when none was reassembled.
+ * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py) only pass datagrams whose reference reads stay inside
  * avail and whose walk terminates (the oracle restatement decides which; the others are
  * restatement-only and documented so).
  */
@@ -46,6 +53,7 @@ int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
 int rr_ipv6_ext_headers(struct pico_frame *f);
 int rr_transport_crc_check(struct pico_frame *f);
+void rr_frag_reset(void);
 
 void __real_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto);
 void __real_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_frame *f, uint8_t proto);
@@ -58,6 +66,8 @@ int rr_init(void);
 int rr_ipv4_link(uint32_t addr);
 int rr_ipv4_rx(const uint8_t *d, uint32_t avail);
 int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
+int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
+             uint32_t cap, uint32_t *out_len, uint32_t *module, int *check);
 
 static struct pico_device *g_dev;
 static int g_frag, g_deliv_proto;
@@ -223,4 +233,55 @@ int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *pr
         pico_frame_discard(f);
     }
     return r;
+}
+
+int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
+             uint32_t cap, uint32_t *out_len, uint32_t *module, int *check)
+{
+    uint32_t i;
+    struct pico_frame *full, *q;
+    if (!g_dev)
+        return -1;
+    rr_frag_reset();
+    if (g_deliv) {
+        pico_frame_discard(g_deliv);
+        g_deliv = NULL;
+    }
+    g_forward = 1;
+    for (i = 0; i < n; i++) {
+        struct pico_frame *f = mk(base + offs[i], lens[i]);
+        if (!f)
+            break;
+        if (v6) {
+            if (rr_ipv6_ext_headers(f) > 0 && f != g_deliv)   /* not a fragment: not ours to keep */
+                pico_frame_discard(f);
+            else if (f != g_deliv)
+                pico_frame_discard(f);                       /* handed on as a copy, or dropped */
+        } else {
+            rr_ipv4_process_in(f);                           /* discards f itself */
+            while ((q = pico_dequeue(pico_proto_udp.q_in)) != NULL)
+                pico_frame_discard(q);
+            while ((q = pico_dequeue(pico_proto_icmp4.q_in)) != NULL)
+                pico_frame_discard(q);
+        }
+    }
+    g_forward = 0;
+    full = g_deliv;
+    g_deliv = NULL;
+    rr_frag_reset();
+    if (!full)
+        return 0;
+    *out_len = full->transport_len;
+    *module = (uint32_t)g_deliv_proto;
+    if ((uint32_t)full->net_len + full->transport_len <= cap)
+        memcpy(out, full->net_hdr, (size_t)full->net_len + full->transport_len);
+    if (g_deliv_proto == 6 || g_deliv_proto == 17) {
+        *check = rr_transport_crc_check(full);               /* discards full when it fails */
+        if (*check)
+            pico_frame_discard(full);
+    } else {
+        *check = -1;
+        pico_frame_discard(full);
+    }
+    return 1;
 }

@@ -30,6 +30,7 @@ EXPORTED = (
     "pico_eth_checksum_batch_dev",
     "pico_ipv4_forward_batch_dev",
     "pico_ipv4_reassemble_batch_dev",
+    "pico_ipv6_reassemble_batch_dev",
     "pico_csum_ctx_create",
     "pico_csum_ctx_destroy",
     "pico_checksum_batch_uniform_host",
@@ -94,6 +95,7 @@ def load() -> ctypes.CDLL:
     sig("pico_eth_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp)
     sig("pico_ipv4_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, vp)
+    sig("pico_ipv6_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, u32, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)
     sig("pico_csum_ctx_destroy", None, vp)
     sig("pico_checksum_batch_uniform_host", ctypes.c_int, vp, vp, u64, u32, u32, u32, vp)

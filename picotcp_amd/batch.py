@@ -226,6 +226,17 @@ def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: i
     (first, count) pairs per datagram (int32 tensor of 2*n), out = uint8 device buffer the
     datagrams are written into at out_desc[g].off.  Returns (out_len int32[n], out_transport
     int16[n], verdict uint8[n])."""
+    return _reassemble(False, base, frag_desc, n_frag, groups, out, out_desc, 0, stream, results)
+
+
+def ipv6_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: int, groups: torch.Tensor,
+                          out: torch.Tensor, out_desc: torch.Tensor, flags: int = 0, stream=None, results=None):
+    """IPv6 reassembly gather + transport check (pico_fragments.c:432-498, 304-358): as
+    ipv4_reassemble_batch, descriptors at each fragment's IPv6 header; flags F_NXTHDR_DISPATCH."""
+    return _reassemble(True, base, frag_desc, n_frag, groups, out, out_desc, flags, stream, results)
+
+
+def _reassemble(v6, base, frag_desc, n_frag, groups, out, out_desc, flags, stream, results):
     for t, nm in ((base, "base"), (frag_desc, "frag_desc"), (groups, "groups"), (out, "out"), (out_desc, "out_desc")):
         _require_device(t, nm)
         if t.device != base.device:
@@ -245,10 +256,16 @@ def ipv4_reassemble_batch(base: torch.Tensor, frag_desc: torch.Tensor, n_frag: i
     for t, nm, sz in ((ol, "out_len", 4), (l4, "out_transport", 2), (v, "verdict", 1)):
         _check_out(t, n, nm, dev, sz)
     lib = _lib.load()
-    _lib.check("pico_ipv4_reassemble_batch_dev",
-               lib.pico_ipv4_reassemble_batch_dev(_ptr(base), base.numel(), _ptr(frag_desc), n_frag, _ptr(groups), n,
-                                                  _ptr(out), out.numel(), _ptr(out_desc), _ptr(ol), _ptr(l4), _ptr(v),
-                                                  _stream_handle(stream)))
+    if v6:
+        _lib.check("pico_ipv6_reassemble_batch_dev",
+                   lib.pico_ipv6_reassemble_batch_dev(_ptr(base), base.numel(), _ptr(frag_desc), n_frag, _ptr(groups),
+                                                      n, _ptr(out), out.numel(), _ptr(out_desc), _ptr(ol), _ptr(l4),
+                                                      _ptr(v), flags, _stream_handle(stream)))
+    else:
+        _lib.check("pico_ipv4_reassemble_batch_dev",
+                   lib.pico_ipv4_reassemble_batch_dev(_ptr(base), base.numel(), _ptr(frag_desc), n_frag, _ptr(groups),
+                                                      n, _ptr(out), out.numel(), _ptr(out_desc), _ptr(ol), _ptr(l4),
+                                                      _ptr(v), _stream_handle(stream)))
     return ol, l4, v
 
 

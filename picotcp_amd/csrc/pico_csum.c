@@ -35,10 +35,9 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
                                   void *stream);
-int pico_csum_launch_ipv4_reassemble(const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
-                                     const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len,
-                                     const void *out_desc, uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict,
-                                     void *stream);
+int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
+                                const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len, const void *out_desc,
+                                uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict, uint32_t flags, void *stream);
 
 /* ------------------------------------------------------------------ errors */
 
@@ -424,10 +423,10 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
                          "pico_ipv4_forward_batch_dev");
 }
 
-int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
-                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
-                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
-                                   uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
+static int reassemble_dev(int v6, const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                          uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out, uint64_t out_len,
+                          const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len, uint16_t *d_out_transport,
+                          uint8_t *d_verdict, uint32_t flags, void *stream, const char *what)
 {
     int rc;
     if (n_dgram == 0)
@@ -438,12 +437,32 @@ int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const 
         return fail(PICO_CSUM_EINVAL, "descriptor arrays must be 16-byte aligned");
     if (((uintptr_t)d_groups & 3u) != 0 || ((uintptr_t)d_out & 3u) != 0)
         return fail(PICO_CSUM_EINVAL, "d_groups and d_out must be 4-byte aligned");
+    if (flags & ~(v6 ? PICO_CSUM_F_NXTHDR_DISPATCH : 0u))
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
     if ((rc = need_device()) != 0)
         return rc;
-    return launch_status(pico_csum_launch_ipv4_reassemble(d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out,
-                                                          out_len, d_out_desc, d_out_len, d_out_transport, d_verdict,
-                                                          stream),
-                         "pico_ipv4_reassemble_batch_dev");
+    return launch_status(pico_csum_launch_reassemble(v6, d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out,
+                                                     out_len, d_out_desc, d_out_len, d_out_transport, d_verdict,
+                                                     flags, stream),
+                         what);
+}
+
+int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
+                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
+                                   uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
+{
+    return reassemble_dev(0, d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out, out_len, d_out_desc,
+                          d_out_len, d_out_transport, d_verdict, 0, stream, "pico_ipv4_reassemble_batch_dev");
+}
+
+int pico_ipv6_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
+                                   uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
+                                   uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
+                                   uint16_t *d_out_transport, uint8_t *d_verdict, uint32_t flags, void *stream)
+{
+    return reassemble_dev(1, d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out, out_len, d_out_desc,
+                          d_out_len, d_out_transport, d_verdict, flags, stream, "pico_ipv6_reassemble_batch_dev");
 }
 
 /* ------------------------------------------------------------------ layer 3 */

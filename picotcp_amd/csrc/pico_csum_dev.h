@@ -293,6 +293,152 @@ __device__ __forceinline__ uint32_t masked_chunk_sum(const uint4 v, uint32_t ch,
     return dot2_add(d, dot2_add(c, dot2_add(b, dot2_add(a, 0u))));
 }
 
+// ---------------------------------------------------------------- IPv6 extension headers
+//
+// pico_ipv6_extension_headers (modules/pico_ipv6.c:707-809) with the sequence check before it
+// (pico_ipv6_check_headers_sequence, :659-694), for an RX datagram whose descriptor carries no
+// seed and whose next header is not TCP / UDP / ICMPv6 (sorted kernel), and for every IPv6
+// fragment (reassembly kernel) -- one lane walks its own datagram with byte loads (L2 hits: the
+// header was just fetched).  Reads stay inside avail; where the reference would read past its buffer, or loop
+// forever (a zero-length step: (uint8)((len + 1) << 3) wraps for len >= 31, an option length
+// of 254), or let its uint16 f->net_len wrap, the datagram is WALK_BAD (MALFORMED).
+//   WALK_DROP   the reference discards it (invalid / misplaced header, an option or routing
+//               type that discards, M with a payload length not a multiple of 8, ESP / AUTH /
+//               no next header)
+//   WALK_PROTO  the transport is reached: net_len, proto
+//   WALK_FRAG   the transport is reached behind a fragment header: pico_ipv6_process_frag
+constexpr int WALK_BAD = -1, WALK_DROP = 0, WALK_PROTO = 1, WALK_FRAG = 2;
+
+#define WBYTE(k, dst)                          \
+    do {                                       \
+        if ((uint32_t)(k) >= avail) return -2; \
+        (dst) = h[(uint32_t)(k)];              \
+    } while (0)
+
+// pico_ipv6_process_hopbyhop (:525-582): must_align 1 / 0, -1 discard, -2 bad
+__device__ __noinline__ int walk_hbh(const uint8_t* __restrict__ h, uint32_t avail, uint32_t e) {
+    uint32_t b1, type, olen;
+    WBYTE(e + 1, b1);
+    uint32_t len = (((b1 + 1u) << 3) - 2u) & 0xFFu, opt = e + 2u;
+    int must_align = 1;
+    while (len) {
+        WBYTE(opt, type);
+        if (type == 0u) { ++opt; --len; continue; }                 // Pad1
+        WBYTE(opt + 1u, olen);
+        const uint32_t optlen = (olen + 2u) & 0xFFu;
+        if (type == 5u) { if (olen == 2u) must_align = 0; }         // router alert (MLD)
+        else if (type != 1u && (type & 0xC0u) != 0u) return -1;     // action: discard
+        if (optlen == 0u) return -2;                                // the reference loops forever
+        opt += optlen;
+        len = (len - optlen) & 0xFFu;
+    }
+    return must_align;
+}
+
+// pico_ipv6_process_destopt (:610-657): 0 pass, -1 discard, -2 bad; every option advances opt[1] + 2
+__device__ __noinline__ int walk_dst(const uint8_t* __restrict__ h, uint32_t avail, uint32_t e) {
+    uint32_t b1, type, olen;
+    WBYTE(e + 1, b1);
+    uint32_t len = (((b1 + 1u) << 3) - 2u) & 0xFFu, opt = e + 2u;
+    while (len) {
+        WBYTE(opt, type);
+        WBYTE(opt + 1u, olen);
+        const uint32_t optlen = (olen + 2u) & 0xFFu;
+        if (type != 0u && type != 1u && type != 201u && (type & 0xC0u) != 0u) return -1;
+        if (optlen == 0u) return -2;
+        opt += optlen;
+        len = (len - optlen) & 0xFFu;
+    }
+    return 0;
+}
+#undef WBYTE
+
+#define WBYTE(k, dst)                                            \
+    do {                                                         \
+        if ((uint32_t)(k) >= avail) return (uint64_t)(WALK_BAD + 1); \
+        (dst) = h[(uint32_t)(k)];                                \
+    } while (0)
+
+// Returns kind + 1 | net_len << 8 | proto << 24 | f->frag << 32 (the last fragment header's
+// offset / M field, :754) -- registers only, no stack slots for outputs.
+__device__ __noinline__ __attribute__((unused)) uint64_t ipv6_walk_packed(const uint8_t* __restrict__ h,
+                                                                           uint32_t avail) {
+    const uint32_t plen = ((uint32_t)h[4] << 8) | h[5];
+    uint32_t nx = h[6], b, ptr = 40u;
+    // sequence check: steps of (uint8)((len + 1) << 3) (0 when len >= 31: the next step reads
+    // the same header again), 8 for a fragment header; at most 2 steps per 8 bytes of avail
+    for (uint32_t it = 0;; ++it) {
+        if (it > 2u * (avail >> 3) + 8u) return (uint64_t)(WALK_BAD + 1);
+        uint32_t optlen;
+        if (nx == 0u || nx == 43u || nx == 60u || nx == 50u || nx == 51u) {
+            WBYTE(ptr + 1u, b);
+            optlen = ((b + 1u) << 3) & 0xFFu;
+        } else if (nx == 44u) {
+            optlen = 8u;
+        } else if (nx == 59u || nx == 6u || nx == 17u || nx == 58u) {
+            break;
+        } else {
+            return (uint64_t)(WALK_DROP + 1);
+        }
+        WBYTE(ptr, nx);
+        ptr += optlen;
+    }
+    // the walk: f->net_len (uint16) moves by >= 8 bytes a step
+    uint32_t net_len = 40u, cur_nexthdr = 6u;
+    bool must_align = false, frag = false;
+    uint32_t om = 0;
+    nx = h[6];
+    ptr = 40u;
+    for (;;) {
+        const uint32_t e = net_len;
+        uint32_t cur_optlen;
+        if (nx == 6u || nx == 17u || nx == 58u) {
+            if (must_align && (plen & 7u) != 0u) return (uint64_t)(WALK_DROP + 1);
+            return ((uint64_t)om << 32) | (uint32_t)((frag ? WALK_FRAG : WALK_PROTO) + 1) | (net_len << 8) | (nx << 24);
+        } else if (nx == 0u) {                                      // hop-by-hop: only first
+            if (cur_nexthdr != 6u) return (uint64_t)(WALK_DROP + 1);
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            const int r = walk_hbh(h, avail, e);
+            if (r == -2) return (uint64_t)(WALK_BAD + 1);
+            if (r < 0) return (uint64_t)(WALK_DROP + 1);
+            must_align = r != 0;
+        } else if (nx == 43u) {                                     // routing
+            uint32_t segleft, type;
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            WBYTE(e + 3u, segleft);
+            if (segleft != 0u) {
+                WBYTE(e + 2u, type);
+                if (type != 2u) return (uint64_t)(WALK_DROP + 1);
+            }
+        } else if (nx == 44u) {                                     // fragment
+            uint32_t om0, om1;
+            cur_optlen = 8u;
+            WBYTE(e + 3u, om1);
+            WBYTE(e + 2u, om0);
+            om = (om0 << 8) | om1;
+            frag = true;
+            if ((om1 & 1u) && (plen & 7u) != 0u) return (uint64_t)(WALK_DROP + 1);
+        } else if (nx == 60u) {                                     // destination options
+            WBYTE(e + 1u, b);
+            cur_optlen = (b + 1u) << 3;
+            must_align = true;
+            const int r = walk_dst(h, avail, e);
+            if (r == -2) return (uint64_t)(WALK_BAD + 1);
+            if (r < 0) return (uint64_t)(WALK_DROP + 1);
+        } else {                                                    // ESP, AUTH, none, invalid
+            return (uint64_t)(WALK_DROP + 1);
+        }
+        if (net_len + cur_optlen > 0xFFFFu) return (uint64_t)(WALK_BAD + 1);        // the uint16 would wrap
+        net_len += cur_optlen;
+        WBYTE(e, nx);                                               // exthdr->nxthdr (:805)
+        cur_nexthdr = ptr;
+        ptr += cur_optlen;
+    }
+}
+#undef WBYTE
+
 struct FlatArgs {
     uint8_t* base;
     uint64_t base_len;

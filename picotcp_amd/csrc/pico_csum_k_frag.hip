@@ -1,17 +1,21 @@
-// pico_csum_k_frag.hip -- IPv4 fragment reassembly gather fused with the transport check of
-// the reassembled datagram, and its launcher.
+// pico_csum_k_frag.hip -- IPv4 and IPv6 fragment reassembly gather fused with the transport
+// check of the reassembled datagram, and its launcher.
 // Helpers, argument conventions and the arithmetic contract: pico_csum_dev.h.
 //
-// Reference: pico_ipv4_process_frag / pico_fragments_check_complete /
-// pico_fragments_reassemble (modules/pico_fragments.c:129-139, 216-239, 304-358, 499-568),
-// then pico_transport_crc_check (stack/pico_socket.c:1916-1968) on the reassembled frame.
+// Reference: pico_ipv4_process_frag / pico_ipv6_process_frag / pico_fragments_check_complete /
+// pico_fragments_reassemble (modules/pico_fragments.c:73-139, 216-239, 304-358, 432-568), then
+// pico_transport_crc_check (stack/pico_socket.c:1916-1968) -- or, for ICMPv6,
+// pico_icmp6_checksum -- on the reassembled frame.  IPv6 fragments are walked on device
+// (ipv6_walk_packed, pico_csum_dev.h: pico_ipv6_extension_headers) for net_len, the fragment
+// field and the transport protocol.
 // The reference copies every fragment into a fresh frame (memcpy, :334-345) and then sums
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
 // One workgroup (4 waves) per datagram (its fragments are a contiguous descriptor range, in
 // arrival order):
-//   1. all 256 threads parse the fragment headers (IHL, total length, MF, offset) into LDS and
+//   1. all 256 threads parse the fragment headers (IPv4: IHL, total length, MF, offset; IPv6: the
+//      extension-header walk, payload length, M, offset, protocol) into LDS and
 //      mark repeated offsets (pico_tree_insert rejects a repeated key: the earliest arrival
 //      of each offset is kept);
 //   2. the gather starts at once: a kept fragment's place in the transport is its own offset
@@ -19,7 +23,7 @@
 //      ordering.  Waves 1-3 gather fragments 1, 2, 3 mod 4 while wave 0 checks completeness
 //      (rank by offset among the kept fragments, LDS broadcast reads; a wave prefix scan of
 //      the sorted transport lengths against the offsets, up to the first fragment without MF,
-//      which must be the last in tree order), copies the first fragment's 20 header bytes,
+//      which must be the last in tree order), copies the first fragment's 20 (IPv6: 40) header bytes,
 //      then gathers fragments 0 mod 4;
 //   3. gather: a fragment's payload in 16-byte units, 2 x 64 units per wave per step, every
 //      load issued before any is used: two aligned 16-byte loads through a buffer window over
@@ -37,6 +41,7 @@ constexpr uint32_t FRAG_MAX = 512;     // fragments per datagram handled on devi
 
 struct FragArgs {
     const uint8_t* base;
+    uint32_t flags;                     // IPv6: F_NXD
     uint64_t base_len;
     const pico_csum_desc_dev* frag;
     const uint32_t* grp;                // 2 per datagram: first descriptor, count
@@ -51,17 +56,20 @@ struct FragArgs {
 };
 
 struct FragLds {
-    uint32_t key[FRAG_MAX];   // offset | MF << 16 | header length << 17 | dup << 24
+    uint32_t key[FRAG_MAX];   // offset | MF << 16 | dup << 24
     uint32_t tl[FRAG_MAX];    // transport length
     uint16_t sidx[FRAG_MAX];  // tree position -> fragment
     uint64_t src[FRAG_MAX];   // fragment -> payload address (no descriptor re-read in the gather)
+    uint8_t pr[FRAG_MAX];     // IPv6: the walk's transport protocol (the module it is handed to)
     uint32_t len, bad, proto, pseudo, first0;
-    uint32_t acc[4], w1[4];
+    uint32_t acc[4], w0[4], w1[4];
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*p; }
 
-__global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
+template <bool V6>
+__global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
+    constexpr uint32_t HDR = V6 ? 40u : 20u;          // PICO_SIZE_IP6HDR / PICO_SIZE_IP4HDR
     __shared__ FragLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t g = blockIdx.x;
@@ -69,32 +77,43 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
     const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
-                      (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < 20u;
+                      (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < HDR;
     if (tid == 0) {
         L.bad = bad0 ? 1u : 0u;
         L.first0 = NONE;
     }
     __syncthreads();
 
-    // ---- 1. parse (pico_ipv4_process_in: net_len, transport_len = tot - net_len, frag)
+    // ---- 1. parse.  IPv4 as pico_ipv4_process_in hands a fragment on (net_len, transport_len =
+    //         tot - net_len, frag); IPv6 as pico_ipv6_extension_headers does (the walk must reach
+    //         the transport behind a fragment header; transport_len = payload_len - (net_len - 40))
     if (!bad0) {
         for (uint32_t j = tid; j < cnt; j += 256u) {
             const pico_csum_desc_dev d = p.frag[first + j];
-            uint32_t key = 0, tl = 0;
-            if (d.len < 20u || d.off > p.base_len || d.len > p.base_len - d.off) {
+            uint32_t key = 0, tl = 0, hl = 0;
+            if (d.len < HDR || d.off > p.base_len || d.len > p.base_len - d.off) {
                 L.bad = 1u;
-            } else {
+            } else if constexpr (!V6) {
                 const uint8_t* h = p.base + d.off;
                 const uint32_t ihl = ld_u8(h) & 0x0Fu;
-                const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+                hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
                 tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
                 const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
-                key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u) | (hl << 17);
+                key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u);
                 if (hl + tl > d.len) L.bad = 1u;
+            } else {
+                const uint8_t* h = p.base + d.off;
+                const uint64_t w = ipv6_walk_packed(h, d.len);
+                const uint32_t om = (uint32_t)(w >> 32);
+                hl = ((uint32_t)w >> 8) & 0xFFFFu;
+                tl = ((((ld_u8(h + 4) << 8) | ld_u8(h + 5))) - (hl - 40u)) & 0xFFFFu;
+                key = (om & 0xFFF8u) | ((om & 1u) << 16);
+                L.pr[j] = (uint8_t)((uint32_t)w >> 24);
+                if ((int)(w & 0xFFu) - 1 != WALK_FRAG || hl + tl > d.len) L.bad = 1u;
             }
             L.key[j] = key;
             L.tl[j] = tl;
-            L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + (key >> 17);
+            L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + hl;
         }
     }
     __syncthreads();
@@ -109,8 +128,8 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
         }
     }
     __syncthreads();
-    uint8_t* t = p.out + od.off + 20;
-    const uint32_t cap = od.len - 20u;                  // transport bytes the output region holds
+    uint8_t* t = p.out + od.off + HDR;
+    const uint32_t cap = od.len - HDR;                  // transport bytes the output region holds
 
     // ---- 2. wave 0: completeness (pico_fragments_check_complete) and the header
     if (wv == 0 && !bad) {
@@ -147,18 +166,33 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
             }
             carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         }
-        const bool b = gap || e == NONE || e + 1u != m || 20u + len > 0xFFFFu || len > cap;
-        // the first fragment's PICO_SIZE_IP4HDR bytes (pico_fragments.c:332-333) and the pseudo
-        // header (struct pico_ipv4_pseudo_hdr as LE words: src, dst, proto << 8, bswap16(len))
+        const bool b = gap || e == NONE || e + 1u != m || HDR + len > 0xFFFFu || len > cap;
+        // the first fragment's PICO_SIZE_IP4HDR / PICO_SIZE_IP6HDR bytes (pico_fragments.c:332-338)
+        // and the pseudo header's address part: IPv4 struct pico_ipv4_pseudo_hdr as LE words (src,
+        // dst, proto << 8, bswap16(len)); IPv6 struct pico_ipv6_pseudo_hdr (src, dst, long_be(len);
+        // the next-header word is added in phase 4, once the checked protocol is known)
         uint32_t proto = 0, pseudo = 0;
         if (!b) {
-            const uint8_t* h0 = reinterpret_cast<const uint8_t*>(L.src[L.first0]) - ((L.key[L.first0] >> 17) & 0x7Fu);
-            const uint32_t hb = lane < 20u ? ld_u8(h0 + lane) : 0u;
-            if (lane < 20u) t[(int)lane - 20] = (uint8_t)hb;
-            proto = (uint32_t)__shfl((int)hb, 9);
-            const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
-            pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) + (proto << 8) +
-                     (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+            const uint8_t* h0 = p.base + p.frag[first + L.first0].off;
+            const uint32_t hb = lane < HDR ? ld_u8(h0 + lane) : 0u;
+            if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hb;
+            if constexpr (!V6) {
+                proto = (uint32_t)__shfl((int)hb, 9);
+                const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) + (proto << 8) +
+                         (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+            } else {
+                // the module: the walk's protocol of the chain fragment that arrived last (the
+                // arrival that completes the set hands its protocol on, pico_fragments.c:492);
+                // byte 9 of the copied header rides in bits 8-15 (the reference's TCP / UDP dispatch)
+                uint32_t last = 0;
+                for (uint32_t i = lane; i <= e; i += 64u) last = max(last, (uint32_t)L.sidx[i] + 1u);
+                last = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_max(last), 63) - 1u;
+                proto = (uint32_t)L.pr[last] | ((uint32_t)__shfl((int)hb, 9) << 8);
+                const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                pseudo = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(pw), 63) +
+                         (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+            }
         }
         if (lane == 0) {
             L.len = b ? 0u : len;
@@ -170,7 +204,7 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
 
     // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order),
     //         each kept fragment at its own offset
-    uint32_t acc = 0, w1 = 0;
+    uint32_t acc = 0, w0 = 0, w1 = 0;
     if (!bad) {
         const bool t8 = ((reinterpret_cast<uintptr_t>(t)) & 7u) == 0;   // workgroup-uniform
         struct Frag {
@@ -232,31 +266,55 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
                         for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = x[w];
                     }
                     acc = dot2_add(x[3], dot2_add(x[2], dot2_add(x[1], dot2_add(x[0], acc))));   // even offset
-                    if (f.at + b0 == 0u) w1 = x[1];         // transport bytes 4..7 (UDP crc: 6, 7)
+                    if (f.at + b0 == 0u) {                  // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
+                        w0 = x[0];
+                        w1 = x[1];
+                    }
                 }
             }
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
+        w0 = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(w0), 63);
         w1 = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(w1), 63);
         if (lane == 0) {
             L.acc[wv] = acc;
+            L.w0[wv] = w0;
             L.w1[wv] = w1;
         }
     }
     __syncthreads();
     bad = L.bad != 0;
 
-    // ---- 4. pico_transport_crc_check on the reassembled frame
+    // ---- 4. pico_transport_crc_check on the reassembled frame (ICMPv6: pico_icmp6_process_in)
     if (tid == 0) {
         uint32_t l4 = 0, v = V_MALFORMED;
         const uint32_t len = L.len, proto = L.proto;
         if (!bad) {
             const uint32_t s = L.acc[0] + L.acc[1] + L.acc[2] + L.acc[3];
+            const uint32_t word0 = L.w0[0] | L.w0[1] | L.w0[2] | L.w0[3];
             const uint32_t word1 = L.w1[0] | L.w1[1] | L.w1[2] | L.w1[3];
             v = V_ACCEPT;
-            if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
-                l4 = finalize(L.pseudo + s);
-                if (l4) v = V_L4_BAD;
+            if constexpr (!V6) {
+                if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
+                    l4 = finalize(L.pseudo + s);
+                    if (l4) v = V_L4_BAD;
+                }
+            } else {
+                const uint32_t module = proto & 0xFFu, b9 = proto >> 8;
+                uint32_t cp = module;
+                bool check = false;
+                if (module == 6u || module == 17u) {
+                    if (!(p.flags & F_NXD)) cp = b9;          // pico_socket.c:1923 through the IPv4 cast
+                    check = cp == 6u || (cp == 17u && len >= 8u && (word1 >> 16) != 0u);
+                } else if (module == 58u && len >= 1u) {
+                    check = true;
+                }
+                if (check) {
+                    l4 = finalize(L.pseudo + (cp << 8) + s);
+                    const uint32_t type = word0 & 0xFFu;
+                    const bool checked = module != 58u || (type >= 130u && type <= 137u) || type == 143u;
+                    if (l4 && checked) v = V_L4_BAD;
+                }
             }
         }
         if (p.o_len) p.o_len[g] = bad ? 0u : len;
@@ -269,16 +327,17 @@ __global__ __launch_bounds__(256) void ipv4_reassemble_kernel(FragArgs p) {
 
 extern "C" {
 
-int pico_csum_launch_ipv4_reassemble(const void* base, uint64_t base_len, const void* frag, uint32_t n_frag,
-                                     const uint32_t* groups, uint32_t n_dgram, void* out, uint64_t out_len,
-                                     const void* out_desc, uint32_t* o_len, uint16_t* o_l4, uint8_t* verdict,
-                                     void* stream) {
+// v6: 0 IPv4, 1 IPv6; flags: F_NXD (IPv6)
+int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, const void* frag, uint32_t n_frag,
+                                const uint32_t* groups, uint32_t n_dgram, void* out, uint64_t out_len, const void* out_desc,
+                                uint32_t* o_len, uint16_t* o_l4, uint8_t* verdict, uint32_t flags, void* stream) {
     if (n_dgram == 0) return (int)hipSuccess;
-    FragArgs a{static_cast<const uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(frag), groups,
-               n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
+    FragArgs a{static_cast<const uint8_t*>(base), flags, base_len, static_cast<const pico_csum_desc_dev*>(frag),
+               groups, n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
                static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict};
     const dim3 grid(n_dgram), block(256);
-    hipLaunchKernelGGL(ipv4_reassemble_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    if (v6) hipLaunchKernelGGL(reassemble_kernel<true>, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    else hipLaunchKernelGGL(reassemble_kernel<false>, grid, block, 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
 

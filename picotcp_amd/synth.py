@@ -330,3 +330,77 @@ def ipv4_fragments(lengths, seed: int = 21, proto: int = 17, frag_payload: int =
         buf[int(off[j]):int(off[j]) + pieces[j].size] = pieces[j]
     flen = np.array([p.size for p in pieces], dtype=np.uint32)
     return buf, off, flen, np.array(groups, dtype=np.uint32).reshape(-1, 2)
+
+
+def ipv6_fragments(lengths, seed: int = 23, proto: int = 6, frag_payload: int = 1448, shuffle: bool = True,
+                   valid: bool = True, hbh: bool = False, b9_proto: bool = True):
+    """IPv6 datagrams of the given TRANSPORT lengths, each split into fragments of
+    `frag_payload` bytes (a multiple of 8; the last one shorter) as pico_ipv6_frag_send / an
+    MTU-1500 path produces them: every fragment an IPv6 frame (14-byte Ethernet gap, 40-byte
+    header, an optional 8-byte hop-by-hop header (PadN) when `hbh`, the 8-byte fragment header:
+    next header = proto, offset | M, a per-datagram id; payload length = the rest), same src /
+    dst.  With `valid` the transport carries a correct TCP / UDP / ICMPv6 checksum over the whole
+    datagram; `b9_proto` puts proto into header byte 9 (the source address's second byte, which
+    pico_transport_crc_check dispatches on).  Fragments of a datagram are placed (and listed) in
+    a seeded arrival order when `shuffle`.
+    Returns (buffer, frag offsets uint64 (-> IPv6 header), frag bytes uint32, groups uint32[n, 2])."""
+    lengths = np.asarray(lengths, dtype=np.uint32)
+    assert frag_payload % 8 == 0 and frag_payload > 0
+    rng = np.random.default_rng(seed)
+    pieces, groups = [], []
+    for g, L in enumerate(lengths.tolist()):
+        t = random_bytes(seed * 1000003 + g, L)
+        src = bytearray(random_bytes(seed * 7 + g, 16).tobytes())
+        dst = bytes(random_bytes(seed * 11 + g, 16).tobytes())
+        if b9_proto:
+            src[1] = proto
+        src = bytes(src)
+        x = {6: 16, 17: 6, 58: 2}.get(proto)
+        if proto == 6 and L >= 20:
+            t[12], t[13], t[16], t[17] = 0x50, 0x18, 0, 0
+        if proto == 17 and L >= 8:
+            t[4], t[5], t[6], t[7] = (L >> 8) & 0xFF, L & 0xFF, 0, 0
+        if proto == 58 and L >= 4:
+            t[0], t[2], t[3] = 128, 0, 0
+        if valid and x is not None and L >= x + 2:
+            ph = np.frombuffer(src + dst + L.to_bytes(4, "big") + bytes([0, 0, 0, proto]), np.uint8)
+            c = _finalize(_ones_sum(t, _ones_sum(ph)))
+            t[x], t[x + 1] = c >> 8, c & 0xFF
+        ident = int(rng.integers(1, 1 << 32))
+        offs = list(range(0, max(L, 1), frag_payload)) if L else [0]
+        frs = []
+        for o in offs:
+            pl = min(frag_payload, L - o)
+            ext = 16 if hbh else 8
+            h = np.zeros(40 + ext, np.uint8)
+            h[0] = 0x60
+            plen = ext + pl
+            h[4], h[5] = plen >> 8, plen & 0xFF
+            h[6], h[7] = (0 if hbh else 44), 64
+            h[8:24] = np.frombuffer(src, np.uint8)
+            h[24:40] = np.frombuffer(dst, np.uint8)
+            f = 40
+            if hbh:
+                h[40:48] = [44, 0, 1, 4, 0, 0, 0, 0]
+                f = 48
+            om = o | (1 if o + pl < L else 0)
+            h[f:f + 8] = [proto, 0, om >> 8, om & 0xFF, ident >> 24, (ident >> 16) & 0xFF, (ident >> 8) & 0xFF,
+                          ident & 0xFF]
+            frs.append(np.concatenate([h, t[o:o + pl]]))
+        if shuffle:
+            frs = [frs[i] for i in rng.permutation(len(frs))]
+        groups.append((len(pieces), len(frs)))
+        pieces.extend(frs)
+    n = len(pieces)
+    place = rng.permutation(n) if shuffle else np.arange(n)
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for j in place.tolist():
+        pos += 14
+        off[j] = pos
+        pos += pieces[j].size
+    buf = random_bytes(seed ^ 0xF6A6, pos + 16)
+    for j in range(n):
+        buf[int(off[j]):int(off[j]) + pieces[j].size] = pieces[j]
+    flen = np.array([p.size for p in pieces], dtype=np.uint32)
+    return buf, off, flen, np.array(groups, dtype=np.uint32).reshape(-1, 2)

@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Golden reassembly results from the reference's own compiled fragment path.
+
+Run here (where /root/reference exists):
+    make -C oracle all refrx && python tests/golden/make_ref_reasm.py
+
+oracle/_ref/libref_rx.so (see make_ref_rx.py) feeds the fragments of one datagram, in arrival
+order, through the reference's own RX entry points -- pico_ipv4_process_in
+(modules/pico_ipv4.c:381-470) or pico_ipv6_extension_headers (modules/pico_ipv6.c:707-809) --
+into modules/pico_fragments.c (pico_ipv4_process_frag / pico_ipv6_process_frag :432-498,
+pico_fragments_check_complete :304-358, pico_fragments_reassemble :216-239) and observes the
+datagram it hands to the transport (rr_reasm in oracle/ref_rx_driver.c): its bytes, transport
+length, the protocol module it goes to, and pico_transport_crc_check's result on it for TCP /
+UDP (stack/pico_socket.c:1916-1968, the byte-9 dispatch included).
+
+Groups (seeded, per family): TCP / UDP / ICMP(v6) datagrams of 8..2400 transport bytes cut into
+8 / 64 / 512 / MTU-sized fragments, shuffled; some groups lose a fragment (a hole), repeat one (the
+reference keeps the earlier arrival), carry a flipped payload bit, or (IPv6) a hop-by-hop header
+before the fragment header, a header byte 9 that is not the transport's, or an ND / MLD ICMPv6
+type (the types pico_icmp6_checksum's verdict applies to).  All fragments of every group lie in
+one buffer at random alignments; every group has its own output region (off = 0 / 4 / 8 / 12
+mod 16).
+
+Expected values: the oracle's (oracle/pico_csum_oracle.c), asserted here equal to the
+reference's wherever the reference produces them -- pinned_bytes: the datagram bytes and length
+(every complete group); pinned_verdict: the TCP / UDP verdict (ICMP verdicts are the oracle's
+checksum, itself pinned by ref_callers.npz).  An incomplete group is MALFORMED (the reference
+hands nothing on) and pinned as such.
+
+Output (data only): ref_reasm_cases.npz, per family p in (v4, v6):
+  p_buf, p_frag_off, p_frag_len, p_groups (n, 2), p_out_off, p_out_cap, p_out_size,
+  p_exp_out (the oracle's output buffer), p_len, p_l4, p_verdict, [v6_verdict_nx],
+  p_pinned_bytes, p_pinned_verdict
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+from picotcp_amd import synth  # noqa: E402
+
+REF_RX = os.path.join(ROOT, "oracle", "_ref", "libref_rx.so")
+N_GROUPS = 300
+
+
+def ref_lib():
+    R = ctypes.CDLL(REF_RX)
+    R.rr_init.restype = ctypes.c_int
+    R.rr_ipv4_link.argtypes = [ctypes.c_uint32]
+    R.rr_reasm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    if R.rr_init() != 0:
+        raise RuntimeError("rr_init failed")
+    return R
+
+
+def _fix_v4_crc(b: np.ndarray) -> None:
+    b[10] = b[11] = 0
+    c = O.checksum(b[:20])
+    b[10], b[11] = c >> 8, c & 0xFF
+
+
+def _icmp6_retype(frag: np.ndarray, t0: int, new_type: int, keep_valid: bool) -> None:
+    """Set the ICMPv6 type of the offset-0 fragment (transport at t0); keep the checksum valid
+    (RFC 1624 incremental update) or not."""
+    old = int(frag[t0])
+    frag[t0] = new_type
+    if keep_valid:
+        hc = (int(frag[t0 + 2]) << 8) | int(frag[t0 + 3])
+        m, m2 = (old << 8) | int(frag[t0 + 1]), (new_type << 8) | int(frag[t0 + 1])
+        s = (~hc & 0xFFFF) + (~m & 0xFFFF) + m2
+        while s >> 16:
+            s = (s & 0xFFFF) + (s >> 16)
+        hc2 = ~s & 0xFFFF
+        frag[t0 + 2], frag[t0 + 3] = hc2 >> 8, hc2 & 0xFF
+
+
+def gen_groups(rng, v6: bool, n: int):
+    """n groups: a list of (list of fragment byte arrays in arrival order, hbh)."""
+    out = []
+    for it in range(n):
+        proto = int(rng.choice([6, 17, 58] if v6 else [6, 17, 1]))
+        L = int(rng.integers(8, 2400)) if rng.random() < (0.25 if v6 else 0.5) else int(rng.integers(1, 300)) * 8
+        # (IPv6: pico_ipv6_extension_headers drops a last fragment whose payload length is not a
+        # multiple of 8 -- must_align, modules/pico_ipv6.c:778-788 -- so most lengths are aligned)
+        fp = int(rng.choice([8, 64, 512, 1448 if v6 else 1480]))
+        hbh = bool(v6 and rng.random() < 0.3)
+        seed = int(rng.integers(1, 1 << 30))
+        if v6:
+            buf, off, flen, _ = synth.ipv6_fragments(np.array([L]), seed=seed, proto=proto, frag_payload=fp,
+                                                     shuffle=True, hbh=hbh, b9_proto=bool(rng.random() < 0.8))
+        else:
+            buf, off, flen, _ = synth.ipv4_fragments(np.array([L]), seed=seed, proto=proto, frag_payload=fp,
+                                                     shuffle=True)
+        frs = [buf[int(o):int(o) + int(f)].copy() for o, f in zip(off, flen)]
+        hl = (56 if hbh else 48) if v6 else 20
+        if v6 and proto == 58 and L >= 4 and rng.random() < 0.5:
+            f0 = next(f for f in frs if ((int(f[hl - 6]) << 8) | int(f[hl - 5])) & 0xFFF8 == 0)
+            _icmp6_retype(f0, hl, int(rng.choice([130, 133, 135, 136, 143, 1])), rng.random() < 0.6)
+        if not v6:
+            for f in frs:
+                _fix_v4_crc(f)
+        idx = list(range(len(frs)))
+        r = rng.random()
+        if r < 0.15 and len(idx) > 1:
+            idx.pop(int(rng.integers(0, len(idx))))                                  # a hole
+        elif r < 0.3 and (v6 or len(idx) > 1):
+            # (an unfragmented IPv4 datagram -- offset 0, MF clear -- is delivered by
+            # pico_ipv4_process_in itself, not reassembled: a batch never holds one twice)
+            idx.insert(int(rng.integers(0, len(idx) + 1)), idx[int(rng.integers(0, len(idx)))])   # a repeat
+        elif r < 0.35:
+            idx.pop(int(rng.integers(0, len(idx))))                                  # maybe nothing left
+        frs = [frs[i].copy() for i in idx]
+        if frs and rng.random() < 0.1:
+            f = frs[int(rng.integers(0, len(frs)))]
+            if f.size > hl:
+                f[int(rng.integers(hl, f.size))] ^= 1 << int(rng.integers(8))          # a payload bit
+        out.append(frs)
+    return out
+
+
+def pack(groups, rng, v6: bool):
+    """Every fragment into one buffer at random alignments; output regions."""
+    frags = [f for g in groups for f in g]
+    offs, pos = [], 0
+    for f in frags:
+        pos += int(rng.integers(0, 16))
+        offs.append(pos)
+        pos += f.size
+    buf = rng.integers(0, 256, pos + 16).astype(np.uint8)
+    for f, o in zip(frags, offs):
+        buf[o:o + f.size] = f
+    gi, first = [], 0
+    for g in groups:
+        gi.append((first, len(g)))
+        first += len(g)
+    H = 40 if v6 else 20
+    ooff, ocap, pos = [], [], 0
+    for g in groups:
+        pos = (pos + 15) & ~15
+        pos += int(rng.choice([0, 4, 8, 12]))
+        cap = H + sum(f.size for f in g) + 8
+        ooff.append(pos)
+        ocap.append(cap)
+        pos += cap
+    return (buf, np.array(offs, np.uint64), np.array([f.size for f in frags], np.uint32),
+            np.array(gi, np.uint32).reshape(-1, 2), np.array(ooff, np.uint64), np.array(ocap, np.uint32), pos + 16)
+
+
+def family(R, rng, v6: bool) -> dict:
+    groups = gen_groups(rng, v6, N_GROUPS)
+    buf, foff, flen, grp, ooff, ocap, osize = pack(groups, rng, v6)
+    desc = np.zeros(foff.size, O.DESC_DTYPE)
+    desc["off"], desc["len"] = foff, flen
+    od = np.zeros(ooff.size, O.DESC_DTYPE)
+    od["off"], od["len"] = ooff, ocap
+    out = np.zeros(osize, np.uint8)
+    if v6:
+        ol, l4, v = O.ipv6_reassemble(buf, desc, grp, out, od)
+        _, _, vnx = O.ipv6_reassemble(buf, desc, grp, np.zeros(osize, np.uint8), od, nxthdr_dispatch=True)
+    else:
+        ol, l4, v = O.ipv4_reassemble(buf, desc, grp, out, od)
+    H = 40 if v6 else 20
+    pb, pv = np.zeros(len(groups), bool), np.zeros(len(groups), bool)
+    for g, (first, cnt) in enumerate(grp.tolist()):
+        offs = np.ascontiguousarray(foff[first:first + cnt])
+        lens = np.ascontiguousarray(flen[first:first + cnt])
+        if not v6 and cnt:
+            o = int(offs[0])
+            R.rr_ipv4_link(int.from_bytes(bytes(buf[o + 16:o + 20]), "little"))
+        cap = 70000
+        rout = np.zeros(cap, np.uint8)
+        rl, rm, rc = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+        ok = R.rr_reasm(int(v6), buf.ctypes.data, offs.ctypes.data if cnt else None,
+                        lens.ctypes.data if cnt else None, cnt, rout.ctypes.data, cap,
+                        ctypes.byref(rl), ctypes.byref(rm), ctypes.byref(rc))
+        if not ok:
+            assert v[g] == 8, (v6, g, int(v[g]))
+            pb[g] = pv[g] = True
+            continue
+        o = int(ooff[g])
+        assert ol[g] == rl.value, (v6, g, int(ol[g]), rl.value)
+        assert np.array_equal(out[o:o + H + rl.value], rout[:H + rl.value]), (v6, g)
+        pb[g] = True
+        if rm.value in (6, 17) and rc.value >= 0:
+            assert v[g] == (1 if rc.value else 4), (v6, g, int(v[g]), rc.value)
+            pv[g] = True
+    d = {"buf": buf, "frag_off": foff, "frag_len": flen, "groups": grp, "out_off": ooff, "out_cap": ocap,
+         "out_size": np.array([osize], np.uint64), "exp_out": out, "len": ol, "l4": l4, "verdict": v,
+         "pinned_bytes": pb, "pinned_verdict": pv}
+    if v6:
+        d["verdict_nx"] = vnx
+    print("v6" if v6 else "v4", "groups", len(groups), "fragments", foff.size, "pinned bytes", int(pb.sum()),
+          "pinned verdicts", int(pv.sum()), "verdicts",
+          dict(zip(*[x.tolist() for x in np.unique(v, return_counts=True)])))
+    return d
+
+
+def main() -> None:
+    if not os.path.exists(REF_RX):
+        sys.exit(f"{REF_RX} missing: run `make -C oracle refrx` first")
+    R = ref_lib()
+    rng = np.random.default_rng(20261018)
+    arrays = {}
+    for v6 in (False, True):
+        for k, a in family(R, rng, v6).items():
+            arrays[("v6_" if v6 else "v4_") + k] = a
+    np.savez_compressed(os.path.join(HERE, "ref_reasm_cases.npz"), **arrays)
+
+
+if __name__ == "__main__":
+    main()

@@ -91,3 +91,9 @@ def ref_rx_cases() -> dict:
     """Datagrams with the reference's own RX verdicts (make_ref_rx.py)."""
     z = np.load(os.path.join(GOLDEN, "ref_rx_cases.npz"))
     return {k: z[k] for k in z.files}
+
+
+def ref_reasm_cases() -> dict:
+    """Fragment groups with the reference's own reassembly results (make_ref_reasm.py)."""
+    z = np.load(os.path.join(GOLDEN, "ref_reasm_cases.npz"))
+    return {k: z[k] for k in z.files}

@@ -96,6 +96,12 @@ def test_argument_validation():
                                            None, None, None, None, None) == -_lib.EINVAL
     assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_NXTHDR_DISPATCH, None, None,
                                             None, None) == -_lib.EINVAL
+    # reassembly: flags (IPv6: F_NXTHDR_DISPATCH only), alignment, NULL buffers
+    ra = (vp(0x1000), 1 << 20, vp(0x2000), 4, vp(0x3000), 2, vp(0x4000), 1 << 20, vp(0x5000), None, None, None)
+    assert lib.pico_ipv6_reassemble_batch_dev(*ra, _lib.F_TX, None) == -_lib.EINVAL
+    assert lib.pico_ipv6_reassemble_batch_dev(*ra[:6], vp(0x4002), *ra[7:], 0, None) == -_lib.EINVAL
+    assert lib.pico_ipv4_reassemble_batch_dev(*ra[:8], vp(0x5008), None, None, None, None) == -_lib.EINVAL
+    assert lib.pico_ipv4_reassemble_batch_dev(None, *ra[1:], None) == -_lib.EINVAL
     # NULL buffers
     assert lib.pico_checksum_batch_uniform_dev(None, 6000, 1500, 1500, 4, 0, vp(0x3000), None) == -_lib.EINVAL
     # frames past base_len

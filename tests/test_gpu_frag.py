@@ -1,7 +1,9 @@
-"""GPU: IPv4 reassembly gather + transport check (pico_ipv4_reassemble_batch_dev) against the
-oracle on seeded fragment sets -- out-of-order arrival, repeated offsets, holes, overlaps,
-fragments behind the completing one, odd tails, UDP crc 0, TCP / UDP / other protocols,
-64512-byte datagrams -- bit-exact on the outputs and on every reassembled byte."""
+"""GPU: IPv4 / IPv6 reassembly gather + transport check (pico_ipv4_reassemble_batch_dev,
+pico_ipv6_reassemble_batch_dev) against the oracle on seeded fragment sets -- out-of-order
+arrival, repeated offsets, holes, overlaps, fragments behind the completing one, odd tails, UDP
+crc 0, TCP / UDP / ICMP / other protocols, hop-by-hop headers before the fragment header, both
+IPv6 dispatches, 64512-byte datagrams -- and against the reference-pinned fixture
+(tests/golden/ref_reasm_cases.npz) -- bit-exact on the outputs and on every reassembled byte."""
 from __future__ import annotations
 
 import numpy as np
@@ -17,30 +19,37 @@ from tests.test_gpu_parity import to_dev
 pytestmark = pytest.mark.gpu
 
 
-def gpu_reassemble(buf, d, grp, od, out_size):
+def gpu_reassemble(buf, d, grp, od, out_size, v6=False, nx=False):
     out = torch.zeros(out_size, dtype=torch.uint8, device="cuda:0")
-    ol, l4, v = batch.ipv4_reassemble_batch(to_dev(buf), to_dev(d.view(np.uint8)), d.size,
-                                            to_dev(np.ascontiguousarray(grp, np.uint32).reshape(-1).view(np.int32)),
-                                            out, to_dev(od.view(np.uint8)))
+    args = (to_dev(buf), to_dev(d.view(np.uint8)), d.size,
+            to_dev(np.ascontiguousarray(grp, np.uint32).reshape(-1).view(np.int32)), out, to_dev(od.view(np.uint8)))
+    if v6:
+        ol, l4, v = batch.ipv6_reassemble_batch(*args, flags=batch.F_NXTHDR_DISPATCH if nx else 0)
+    else:
+        ol, l4, v = batch.ipv4_reassemble_batch(*args)
     torch.cuda.synchronize()
     return ol.cpu().numpy().view(np.uint32), l4.cpu().numpy().view(np.uint16), v.cpu().numpy(), out.cpu().numpy()
 
 
-def check(buf, d, grp, od, out_size):
+def check(buf, d, grp, od, out_size, v6=False, nx=False):
     out_o = np.zeros(out_size, np.uint8)
-    wl, w4, wv = O.ipv4_reassemble(buf, d, grp, out_o, od)
-    gl, g4, gv, out_g = gpu_reassemble(buf, d, grp, od, out_size)
+    if v6:
+        wl, w4, wv = O.ipv6_reassemble(buf, d, grp, out_o, od, nxthdr_dispatch=nx)
+    else:
+        wl, w4, wv = O.ipv4_reassemble(buf, d, grp, out_o, od)
+    gl, g4, gv, out_g = gpu_reassemble(buf, d, grp, od, out_size, v6, nx)
+    np.testing.assert_array_equal(gv, wv)
     np.testing.assert_array_equal(gl, wl)
     np.testing.assert_array_equal(g4, w4)
-    np.testing.assert_array_equal(gv, wv)
-    for g in np.flatnonzero(wl):                        # every reassembled byte
-        o, n = int(od["off"][g]), 20 + int(wl[g])
+    H = 40 if v6 else 20
+    for g in np.flatnonzero(wv != 8):                   # every reassembled byte
+        o, n = int(od["off"][g]), H + int(wl[g])
         np.testing.assert_array_equal(out_g[o:o + n], out_o[o:o + n], err_msg=f"datagram {g}")
     return wl, wv
 
 
-def layout(lens, align=16, shift=0):
-    cap = np.array([(20 + int(x) + align - 1) // align * align for x in lens], np.uint64) + np.uint64(align)
+def layout(lens, align=16, shift=0, hdr=20):
+    cap = np.array([(hdr + int(x) + align - 1) // align * align for x in lens], np.uint64) + np.uint64(align)
     off = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.uint64) + np.uint64(shift)
     return G.ipv4_desc(off, (cap - np.uint64(align)).astype(np.uint32)), int(cap.sum()) + shift + 16
 
@@ -102,4 +111,55 @@ def test_reassembly_limits():
     od["off"][1] += 2                                    # not 4-byte aligned
     d["len"][int(grp[2, 0])] -= 1                        # a payload past desc.len
     wl, wv = check(buf, d, grp, od, size)
+    assert (wv == 8).all()
+
+
+@pytest.mark.parametrize("shift", [8, 4])
+@pytest.mark.parametrize("proto", [6, 17, 58])
+@pytest.mark.parametrize("payload,hbh", [(1448, False), (8, False), (512, True), (64000, True)])
+@pytest.mark.parametrize("nx", [False, True])
+def test_ipv6_reassembly_vs_oracle(proto, payload, hbh, shift, nx):
+    rng = np.random.default_rng(proto * 100 + payload % 97 + hbh)
+    lens = (rng.integers(1, 1500, 30) * 8).tolist() + rng.integers(0, 9000, 10).tolist() + [
+        65488, 65480, 65496, 1, 8, 9, 1448, 1449, 2896, 2904]
+    if payload == 8:
+        lens = [x for x in lens if x <= 4000]           # <= 512 fragments per datagram
+    buf, off, flen, grp = synth.ipv6_fragments(lens, seed=proto + payload, proto=proto, frag_payload=payload,
+                                               hbh=hbh, b9_proto=bool(rng.random() < 0.5))
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=shift, hdr=40)          # 8: transports on 16-byte lines
+    wl, wv = check(buf, d, grp, od, size, v6=True, nx=nx)
+    assert (wv != 8).sum() >= len(lens) // 2
+
+
+@pytest.mark.parametrize("fam,nx", [("v4", False), ("v6", False), ("v6", True)])
+def test_reference_fixture(fam, nx):
+    """The reference-pinned groups (make_ref_reasm.py): verdicts, lengths, transports, bytes."""
+    c = G.ref_reasm_cases()
+    p = fam + "_"
+    d = G.ipv4_desc(c[p + "frag_off"], c[p + "frag_len"])
+    od = G.ipv4_desc(c[p + "out_off"], c[p + "out_cap"])
+    gl, g4, gv, out_g = gpu_reassemble(c[p + "buf"], d, c[p + "groups"], od, int(c[p + "out_size"][0]),
+                                       fam == "v6", nx)
+    np.testing.assert_array_equal(gv, c[p + ("verdict_nx" if nx else "verdict")])
+    np.testing.assert_array_equal(gl, c[p + "len"])
+    np.testing.assert_array_equal(g4, c[p + "l4"])
+    H = 40 if fam == "v6" else 20
+    for g in np.flatnonzero(gv != 8):
+        o, n = int(c[p + "out_off"][g]), H + int(gl[g])
+        np.testing.assert_array_equal(out_g[o:o + n], c[p + "exp_out"][o:o + n], err_msg=f"datagram {g}")
+
+
+def test_ipv6_reassembly_limits():
+    """Output region too small or misaligned, a truncated fragment, a datagram over 65535 bytes,
+    and a fragment that does not walk to a fragment header: not reassembled."""
+    buf, off, flen, grp = synth.ipv6_fragments([3000, 3000, 3000, 65496, 3000], seed=5, proto=17)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout([3000, 3000, 3000, 65496, 3000], hdr=40)
+    od["len"][0] = 3000                                  # < 40 + 3000
+    od["off"][1] += 2                                    # not 4-byte aligned
+    d["len"][int(grp[2, 0])] -= 1                        # a payload past desc.len
+    f4 = int(off[int(grp[4, 0])])
+    buf[f4 + 6] = 17                                     # no fragment header: UDP straight away
+    wl, wv = check(buf, d, grp, od, size, v6=True)
     assert (wv == 8).all()
