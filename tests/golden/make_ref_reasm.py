@@ -29,7 +29,7 @@ hands nothing on) and pinned as such.
 
 Output (data only): ref_reasm_cases.npz, per family p in (v4, v6):
   p_buf, p_frag_off, p_frag_len, p_groups (n, 2), p_out_off, p_out_cap, p_out_size,
-  p_exp_out (the oracle's output buffer), p_len, p_l4, p_verdict, [v6_verdict_nx],
+  p_exp_out (the oracle's output buffer), p_len, p_l4, p_verdict, [v6_verdict_nx, v6_l4_nx],
   p_pinned_bytes, p_pinned_verdict
 """
 from __future__ import annotations
@@ -165,7 +165,7 @@ def family(R, rng, v6: bool) -> dict:
     out = np.zeros(osize, np.uint8)
     if v6:
         ol, l4, v = O.ipv6_reassemble(buf, desc, grp, out, od)
-        _, _, vnx = O.ipv6_reassemble(buf, desc, grp, np.zeros(osize, np.uint8), od, nxthdr_dispatch=True)
+        _, l4nx, vnx = O.ipv6_reassemble(buf, desc, grp, np.zeros(osize, np.uint8), od, nxthdr_dispatch=True)
     else:
         ol, l4, v = O.ipv4_reassemble(buf, desc, grp, out, od)
     H = 40 if v6 else 20
@@ -197,7 +197,7 @@ def family(R, rng, v6: bool) -> dict:
          "out_size": np.array([osize], np.uint64), "exp_out": out, "len": ol, "l4": l4, "verdict": v,
          "pinned_bytes": pb, "pinned_verdict": pv}
     if v6:
-        d["verdict_nx"] = vnx
+        d["verdict_nx"], d["l4_nx"] = vnx, l4nx
     print("v6" if v6 else "v4", "groups", len(groups), "fragments", foff.size, "pinned bytes", int(pb.sum()),
           "pinned verdicts", int(pv.sum()), "verdicts",
           dict(zip(*[x.tolist() for x in np.unique(v, return_counts=True)])))

@@ -143,7 +143,7 @@ def test_reference_fixture(fam, nx):
                                        fam == "v6", nx)
     np.testing.assert_array_equal(gv, c[p + ("verdict_nx" if nx else "verdict")])
     np.testing.assert_array_equal(gl, c[p + "len"])
-    np.testing.assert_array_equal(g4, c[p + "l4"])
+    np.testing.assert_array_equal(g4, c[p + ("l4_nx" if nx else "l4")])
     H = 40 if fam == "v6" else 20
     for g in np.flatnonzero(gv != 8):
         o, n = int(c[p + "out_off"][g]), H + int(gl[g])

@@ -49,8 +49,9 @@ def test_oracle_matches_reference_fixture(fam):
     assert c[p + "pinned_bytes"].all() and c[p + "pinned_verdict"].mean() > 0.6
     assert set(np.unique(v).tolist()) == {1, 4, 8}
     if fam == "v6":
-        _, _, vnx, _ = _run(c, fam, nx=True)
+        _, l4nx, vnx, _ = _run(c, fam, nx=True)
         np.testing.assert_array_equal(vnx, c["v6_verdict_nx"])
+        np.testing.assert_array_equal(l4nx, c["v6_l4_nx"])
         assert (vnx != v).any()                        # the byte-9 dispatch matters on these groups
 
 
