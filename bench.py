@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2tx_nw|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
   c1 (default, the metric's config): 256K x 1500 B frames, raw pico_checksum per frame
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
   c2tx: the same datagrams, fused TX (checksums computed and written in place)
+  c2tx_nw: fused TX computed and returned only (F_TX without F_WRITE: the driver's header write-out)
   c2v6: 256K IMIX+20 B IPv6/TCP datagrams, fused IPv6 pseudo-header RX verify
   c2eth: the C2 frames through the Ethernet front end (one launch: ethertype dispatch + RX verify)
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
@@ -67,6 +68,10 @@ CONFIGS = {
     "c2tx": dict(kind="ipv4", frames=262144, tx=True,
                  workload="C2 compute mode: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams, fused TX: IPv4 "
                           "header and TCP checksums computed with the crc fields read as zero and written in place"),
+    "c2tx_nw": dict(kind="ipv4", frames=262144, tx=True, write=False,
+                    workload="C2 compute-only TX: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams, IPv4 header "
+                             "and TCP checksums computed with the crc fields read as zero and returned (F_TX "
+                             "without F_WRITE: the driver writes them with its headers)"),
     "c3_frag": dict(kind="ipv4", frames=16384, frame_bytes=64512,
                     workload="C3 reassembled: 16K x 64512 B (PICO_IPV4_FRAG_MAX_SIZE) IPv4/TCP datagrams, fused "
                              "IPv4 header + TCP pseudo-header RX verify"),
@@ -401,12 +406,12 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
         for g_, w_ in zip(got, want):
             miss |= g_ != w_
         frames, bad = int(hdesc.size), int(miss.sum())
-        if tx:                                      # the in-place writes: oracle RX on them accepts
+        if tx and cfg.get("write", True):           # the in-place writes: oracle RX on them accepts
             rx = O.batch_ipv4(now, hdesc) if kind == "ipv4" else None
             if rx is not None:
                 bad += int(((want[2] == 1) & (rx[2] != 1)).sum())
         what = f"every datagram vs the oracle's fused {kind} {'TX' if tx else 'RX'} restatement" + \
-            (" (+ RX of the written bytes)" if tx and kind == "ipv4" else "")
+            (" (+ RX of the written bytes)" if tx and kind == "ipv4" and cfg.get("write", True) else "")
     return {"frames": frames, "mismatches": bad, "checker": what, "seconds": round(time.perf_counter() - t0, 2)}
 
 
@@ -570,7 +575,8 @@ def main():
         ln = cfg.get("frame_bytes", 0)
         rot = a.rotate or rotation(n * ((ln or IMIX_MEAN) + 14))
         sets = [make_c2(n, dev, 500 + 13 * rank + i, ln, keep_host=i == 0) for i in range(rot)]
-        fl = batch.F_TX | batch.F_WRITE if cfg.get("tx") else 0
+        wr = cfg.get("tx") and cfg.get("write", True)
+        fl = (batch.F_TX | (batch.F_WRITE if wr else 0)) if cfg.get("tx") else 0
         outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                  torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 
@@ -579,7 +585,7 @@ def main():
             batch.ipv4_checksum_batch(b, d, n, flags=fl, out=outs[i % rot])
         frame_bytes = sets[0][2]
         # datagrams + descriptors + (2+2+1) B results (+ the two 2-byte crc fields written in place on TX)
-        algo_bytes = frame_bytes + 16 * n + 5 * n + (4 * n if cfg.get("tx") else 0)
+        algo_bytes = frame_bytes + 16 * n + 5 * n + (4 * n if wr else 0)
     elif cfg["kind"] == "eth":
         n = cfg["frames"]
         ln = 0

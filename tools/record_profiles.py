@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
-"""Copy one GPU round's rocprofv3 summaries + bench lines into profiles/<round>/ and
-refresh profiles/pmc_traffic.json (the `traffic` figure bench.py reports).
+"""Copy one GPU round's bench lines, rocprofv3 kernel statistics and PMC passes into
+profiles/<round>/ and refresh profiles/pmc_traffic.json (the `traffic` figure bench.py reports).
 
-  python tools/record_profiles.py <tag> <round-dir>      e.g.  r01c r01
+  python tools/record_profiles.py <tag> <round-dir>        e.g.  r03g r03
+
+Inputs (gpurun_out/, written by scripts/gpu_round.sh and scripts/gpu_pmc_round.sh):
+  bench_<cfg>_<tag>.json, prof_<cfg>_<tag>/run_kernel_stats.csv,
+  pmc_{fetch,write}_<cfg>_<tag>/run_counter_collection.csv, pmc_sq{a,b}_<cfg>_<tag>/...
+Outputs: profiles/<round>/bench_<cfg>.json, <cfg>_kernel_stats.csv, pmc_summary.json,
+summary.txt (bench kernel average vs the trace's, traffic / algorithmic, SQ ratios).
 """
 import csv
 import json
@@ -11,44 +17,115 @@ import shutil
 import statistics
 import sys
 
-tag, rnd = sys.argv[1], sys.argv[2]
-src = "gpurun_out"
-dst = os.path.join("profiles", rnd)
-os.makedirs(dst, exist_ok=True)
-for cfg in ("c1", "c2", "c2v6"):
-    d = os.path.join(src, f"prof_{cfg}_{tag}")
-    if os.path.isdir(d):
-        shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{cfg}_kernel_stats.csv"))
-for cfg in ("c1", "c2", "c2tx", "c2v6", "c3", "c3_64k", "c3_frag"):
-    f = os.path.join(src, f"bench_{cfg}_{tag}.json")
-    if os.path.exists(f):
-        shutil.copy(f, os.path.join(dst, f"bench_{cfg}.json"))
-path = os.path.join("profiles", "pmc_traffic.json")
-rec = json.load(open(path)) if os.path.exists(path) else {}
-for cfg in ("c1", "c2", "c2v6"):
-    r = {}
-    for kind, c in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        f = os.path.join(src, f"pmc_{kind}_{cfg}_{tag}", "run_counter_collection.csv")
-        if not os.path.exists(f):
-            break
-        rows = list(csv.DictReader(open(f)))
-        # the timed kernel = the checksum kernel with the most dispatches
-        names = {}
-        for x in rows:
-            if "csum" in x["Kernel_Name"]:
-                names[x["Kernel_Name"]] = names.get(x["Kernel_Name"], 0) + 1
-        kern = max(names, key=names.get)
-        r[c + "_kB_median"] = statistics.median(float(x["Counter_Value"]) for x in rows if x["Kernel_Name"] == kern)
-        r["kernel"] = kern
-    else:
-        r["hbm_read_bytes_per_launch"] = int(r["FETCH_SIZE_kB_median"] * 1024 * 2)
-        r["hbm_write_bytes_per_launch"] = int(r["WRITE_SIZE_kB_median"] * 1024)
-        r["hbm_bytes_per_launch"] = r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"]
-        r["round"] = rnd
-        rec[cfg] = r
-rec["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                  "`bench.py --config <c> --steps 20`; median over the timed checksum kernel's dispatches; "
-                  "FETCH_SIZE (kB) x1024 x2 (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md "
-                  "HBM section), WRITE_SIZE (kB) x1024")
-json.dump(rec, open(path, "w"), indent=1)
-print(json.dumps({k: v for k, v in rec.items() if k != "_method"}, indent=1))
+CFGS = ("c1", "c2", "c2tx", "c2tx_nw", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3", "c3_64k", "c3_frag", "c4")
+
+
+def timed_kernel_rows(path):
+    """Rows of the timed kernel (the checksum kernel with the most dispatches)."""
+    rows = list(csv.DictReader(open(path)))
+    names = {}
+    for x in rows:
+        if "csum" in x["Kernel_Name"] or "reassemble" in x["Kernel_Name"]:
+            names[x["Kernel_Name"]] = names.get(x["Kernel_Name"], 0) + 1
+    kern = max(names, key=names.get)
+    return kern, [x for x in rows if x["Kernel_Name"] == kern]
+
+
+def counter_medians(path):
+    kern, rows = timed_kernel_rows(path)
+    by = {}
+    for x in rows:
+        by.setdefault(x["Counter_Name"], []).append(float(x["Counter_Value"]))
+    return kern, {k: statistics.median(v) for k, v in by.items()}
+
+
+def main() -> None:
+    tag, rnd = sys.argv[1], sys.argv[2]
+    src = "gpurun_out"
+    dst = os.path.join("profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    path = os.path.join("profiles", "pmc_traffic.json")
+    rec = json.load(open(path)) if os.path.exists(path) else {}
+    summary, pmc = [], {}
+    for cfg in CFGS:
+        bench = None
+        f = os.path.join(src, f"bench_{cfg}_{tag}.json")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(dst, f"bench_{cfg}.json"))
+            bench = json.loads(open(f).read().strip().splitlines()[-1])
+        d = os.path.join(src, f"prof_{cfg}_{tag}")
+        trace_us = None
+        if os.path.isdir(d):
+            shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{cfg}_kernel_stats.csv"))
+            rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
+            rows = [r for r in rows if "csum" in r["Name"] or "reassemble" in r["Name"]]
+            tr = os.path.join(d, "run_kernel_trace.csv")
+            if rows and os.path.exists(tr) and bench:
+                # the timed region: the last `steps` dispatches of the timed kernel (the stats file's
+                # average also holds the setup and verification launches of the same kernel)
+                top = max(rows, key=lambda r: int(r["Calls"]))["Name"]
+                ts = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]))
+                            for x in csv.DictReader(open(tr)) if x["Kernel_Name"] == top)
+                last = ts[-bench["steps"]:]
+                trace_us = sum(e - b for b, e in last) / len(last) / 1e3
+                open(os.path.join(dst, f"{cfg}_timed.txt"), "w").write(
+                    f"{top}\nlast {len(last)} dispatches of {len(ts)} in run_kernel_trace.csv: mean {trace_us:.3f} us "
+                    f"(bench.py HIP events, same run type: {bench['roofline']['kernel_avg_us']} us)\n")
+        r = {}
+        for kind, c in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+            f = os.path.join(src, f"pmc_{kind}_{cfg}_{tag}", "run_counter_collection.csv")
+            if os.path.exists(f):
+                kern, med = counter_medians(f)
+                r[c + "_kB_median"] = med[c]
+                r["kernel"] = kern
+        if "FETCH_SIZE_kB_median" in r and "WRITE_SIZE_kB_median" in r:
+            r["hbm_read_bytes_per_launch"] = int(r["FETCH_SIZE_kB_median"] * 1024 * 2)
+            r["hbm_write_bytes_per_launch"] = int(r["WRITE_SIZE_kB_median"] * 1024)
+            r["hbm_bytes_per_launch"] = r["hbm_read_bytes_per_launch"] + r["hbm_write_bytes_per_launch"]
+            if bench:
+                algo = bench["roofline"]["algorithmic_bytes_per_launch"]
+                r["algorithmic_bytes_per_launch"] = algo
+                r["traffic_over_algorithmic"] = round(r["hbm_bytes_per_launch"] / algo, 3)
+            r["round"] = rnd
+            rec[cfg] = r
+        sq = {}
+        for p in ("sqa", "sqb"):
+            f = os.path.join(src, f"pmc_{p}_{cfg}_{tag}", "run_counter_collection.csv")
+            if os.path.exists(f):
+                sq.update(counter_medians(f)[1])
+        if sq:
+            waves = sq.get("SQ_WAVES", 0) or 1
+            wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
+            sq["VALU_insts_per_wave"] = round(sq.get("SQ_INSTS_VALU", 0) / waves, 1)
+            sq["wait_any_frac"] = round(sq.get("SQ_WAIT_ANY", 0) / wc, 3)
+            sq["wait_inst_any_frac"] = round(sq.get("SQ_WAIT_INST_ANY", 0) / wc, 3)
+            sq["active_inst_any_frac"] = round(sq.get("SQ_ACTIVE_INST_ANY", 0) / wc, 3)
+            pmc[cfg] = sq
+        if bench:
+            line = (f"{cfg:10s} value {bench['value']:9.2f} {bench['unit']}  kernel {bench['roofline']['kernel_avg_us']:8.2f} us"
+                    f" (trace {trace_us:8.2f} us)" if trace_us else
+                    f"{cfg:10s} value {bench['value']:9.2f} {bench['unit']}  kernel {bench['roofline']['kernel_avg_us']:8.2f} us")
+            line += f"  frac {bench['roofline']['frac']:.4f}"
+            if cfg in rec and rec[cfg].get("round") == rnd:
+                line += (f"  traffic/algorithmic {rec[cfg]['traffic_over_algorithmic']}"
+                         f"  write {rec[cfg]['hbm_write_bytes_per_launch'] / 1e6:.2f} MB")
+            if bench.get("verified"):
+                line += f"  verified {bench['verified']['frames']} frames, {bench['verified']['mismatches']} mismatches"
+            summary.append(line)
+    rec["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                      "`bench.py --config <c> --steps 20 --warmup 2`; median over the timed kernel's dispatches; "
+                      "FETCH_SIZE (kB) x1024 x2 (calibrated to 128 B per 128-B line touched, tools/fetch_calib.py), "
+                      "WRITE_SIZE (kB) x1024")
+    json.dump(rec, open(path, "w"), indent=1)
+    if pmc:
+        json.dump(pmc, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+        for cfg, sq in pmc.items():
+            summary.append(f"{cfg:10s} SQ: VALU insts/wave {sq['VALU_insts_per_wave']}, wait_any {sq['wait_any_frac']}, "
+                           f"wait_inst_any {sq['wait_inst_any_frac']}, active_inst_any {sq['active_inst_any_frac']}, "
+                           f"waves {int(sq.get('SQ_WAVES', 0))}")
+    open(os.path.join(dst, "summary.txt"), "w").write("\n".join(summary) + "\n")
+    print("\n".join(summary))
+
+
+if __name__ == "__main__":
+    main()
