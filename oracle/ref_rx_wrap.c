@@ -1,10 +1,10 @@
 /*
  * ref_rx_wrap.c -- TEST INFRASTRUCTURE ONLY.
  *
- * One of four translation units that compile an UNMODIFIED reference source file together
+ * One of five translation units that compile an UNMODIFIED reference source file together
  * with a few exported accessors for its static functions (the technique of the reference's
  * own module tests, test/unit/modunit_*.c, which #include the module they test).  Built by
- * oracle/Makefile (`make refrx`) four times, once per REF_RX_UNIT:
+ * oracle/Makefile (`make refrx`) five times, once per REF_RX_UNIT:
  *   1: modules/pico_ipv4.c   rr_ipv4_process_in  = pico_ipv4_process_in   (:381-470)
  *                            rr_ipv4_crc_check   = pico_ipv4_crc_check    (:243-257)
  *   2: modules/pico_ipv6.c   rr_ipv6_ext_headers = pico_ipv6_extension_headers (:707-809)
@@ -44,6 +44,10 @@ void rr_frag_reset(void)
     ipv4_fragments_timer = ipv6_fragments_timer = 0;
     ipv4_cur_frag_id = ipv6_cur_frag_id = 0;
 }
+#elif REF_RX_UNIT == 5
+#include "pico_ethernet.c"
+int32_t rr_ethernet_receive(struct pico_frame *f);
+int32_t rr_ethernet_receive(struct pico_frame *f) { return pico_ethernet_receive(f); }
 #else
-#error "REF_RX_UNIT must be 1, 2, 3 or 4"
+#error "REF_RX_UNIT must be 1, 2, 3, 4 or 5"
 #endif

@@ -97,3 +97,9 @@ def ref_reasm_cases() -> dict:
     """Fragment groups with the reference's own reassembly results (make_ref_reasm.py)."""
     z = np.load(os.path.join(GOLDEN, "ref_reasm_cases.npz"))
     return {k: z[k] for k in z.files}
+
+
+def ref_eth_cases() -> dict:
+    """An Ethernet burst with the reference's own L2 + IP verdicts (make_ref_eth.py)."""
+    z = np.load(os.path.join(GOLDEN, "ref_eth_cases.npz"))
+    return {k: z[k] for k in z.files}

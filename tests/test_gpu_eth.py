@@ -119,3 +119,19 @@ def test_eth_random_bursts_vs_oracle(seed):
         np.testing.assert_array_equal(u16(on), wn)
         np.testing.assert_array_equal(u16(ol), wl)
         np.testing.assert_array_equal(u8(v), wv)
+
+
+@pytest.mark.parametrize("kernel", SORTED)
+def test_eth_reference_fixture(kernel):
+    """The burst whose L2 and IP verdicts come from the reference's own compiled receive path
+    (tests/golden/make_ref_eth.py), every kernel variant."""
+    c = G.ref_eth_cases()
+    d = np.zeros(c["off"].size, batch.DESC_DTYPE)
+    d["off"], d["len"] = c["off"], c["avail"]
+    use_kernel(kernel)
+    net, l4, v = batch.eth_checksum_batch(to_dev(c["buf"]), batch.desc_to_device(d, "cuda:0"), d.size,
+                                          mac=bytes(c["mac"]))
+    np.testing.assert_array_equal(v.cpu().numpy(), c["verdict"])
+    np.testing.assert_array_equal(u16(net), c["net"])
+    np.testing.assert_array_equal(u16(l4), c["l4"])
+
