@@ -25,13 +25,15 @@
 //      the sorted transport lengths against the offsets, up to the first fragment without MF,
 //      which must be the last in tree order), copies the first fragment's 20 (IPv6: 40) header bytes,
 //      then gathers fragments 0 mod 4;
-//   3. gather: a fragment's payload in 16-byte units, 2 x 64 units per wave per step, every
-//      load issued before any is used: two aligned 16-byte loads through a buffer window over
-//      the payload (out-of-range slots read zeros, no branches) and a shift by the payload's
-//      alignment (wave-uniform per fragment: dword select + alignbyte); stores are 16-, 8- or
-//      4-byte at the unit's place in the transport (which starts 4-byte aligned, offsets being
-//      multiples of 8), only where the fragment fits the output region; v_dot2 sums on the
-//      fly (every unit is a whole number of checksum words); a workgroup reduction at the end.
+//   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
+//      16-byte units, 3 x 64 units per wave per step (two 1480-byte payloads), every load issued
+//      before any is used: two aligned 16-byte loads through one buffer window over both
+//      payloads (out-of-range slots read zeros, no branches) and a shift by the unit's payload
+//      alignment (dword select + alignbyte); stores are 16-, 8- or 4-byte at the unit's place in
+//      the transport (which starts 4-byte aligned, offsets being multiples of 8), only where the
+//      fragment fits the output region; v_dot2 sums on the fly (every unit is a whole number of
+//      checksum words); a workgroup reduction at the end.  (One fragment per step, 2 x 64
+//      units: c3_reasm 154.6 -> 148.9 us, c3_reasm6 171.9 -> 162.0 us, profiles/r03/ab_frag2.txt.)
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
@@ -202,76 +204,101 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
         }
     }
 
-    // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order),
-    //         each kept fragment at its own offset
+    // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order, two
+    //         at a time), each kept fragment at its own offset
     uint32_t acc = 0, w0 = 0, w1 = 0;
     if (!bad) {
-        const bool t8 = ((reinterpret_cast<uintptr_t>(t)) & 7u) == 0;   // workgroup-uniform
-        struct Frag {
-            Window win;
-            uint32_t s, tl, at, nu;
-            bool o16;
-        };
-        constexpr int U = 2;                   // 64-unit slots per fragment per step
-        for (uint32_t j = wv; j < cnt; j += 4u) {
+        const uint64_t tb = reinterpret_cast<uintptr_t>(t);
+        // a kept fragment the output region can hold (else its datagram is not reassembled:
+        // past the region's end, or larger than it); wave-uniform
+        auto gathered = [&](uint32_t j) {
             const uint32_t kj = L.key[j];
-            Frag f;
-            f.tl = L.tl[j];
-            f.at = kj & 0xFFFFu;
-            // a repeated offset is not gathered; nor a fragment the output region cannot hold
-            // (its datagram is then not reassembled: past its end, or larger than the region)
-            if ((kj >> 24) != 0 || f.at + f.tl > cap) continue;            // wave-uniform
+            return (kj >> 24) == 0 && (kj & 0xFFFFu) + L.tl[j] <= cap;
+        };
+        constexpr int U = 3;                   // 64-unit slots per step: two 1480 B payloads
+        uint32_t j = wv;
+        while (true) {
+            while (j < cnt && !gathered(j)) j += 4u;
+            if (j >= cnt) break;
+            uint32_t j2 = j + 4u;
+            while (j2 < cnt && !gathered(j2)) j2 += 4u;
+            // fragment A = j and (if any) B = j2: units [0, na) are A's, [na, na + nb) B's, read
+            // through one buffer window over both payloads' 16-byte lines when they lie within
+            // 1 GiB of each other (else B waits for the next step)
             const uint64_t sa = L.src[j];
-            // a buffer window over the payload's 16-byte lines: every slot loads unconditionally,
-            // slots past the payload read zeros (no branch, so no vmcnt(0) between the loads)
-            f.win = make_window(sa & ~15ull, ((uint32_t)(sa & 15u) + f.tl + 15u) & ~15u);
-            f.s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sa & 15u));
-            f.o16 = ((reinterpret_cast<uintptr_t>(t) + f.at) & 15u) == 0;
-            f.nu = (f.tl + 15u) >> 4;
-            const uint32_t q = f.s >> 2, sb = f.s & 3u;
-            for (uint32_t u0 = 0; u0 < f.nu; u0 += 64u * U) {
+            const uint32_t ta = L.tl[j], na = (ta + 15u) >> 4, ata = L.key[j] & 0xFFFFu;
+            uint64_t sb2 = sa;
+            uint32_t tb2 = 0, nb = 0, atb = 0;
+            if (j2 < cnt) {
+                sb2 = L.src[j2];
+                tb2 = L.tl[j2];
+                const uint64_t lo = min(sa, sb2) & ~15ull, hi = max(sa + ta, sb2 + tb2) + 16u;
+                if (hi - lo < (1ull << 30)) {
+                    nb = (tb2 + 15u) >> 4;
+                    atb = L.key[j2] & 0xFFFFu;
+                } else {
+                    j2 = j;                      // B next step
+                }
+            } else {
+                j2 = j;
+            }
+            const uint64_t wlo = (nb ? min(sa, sb2) : sa) & ~15ull;
+            const uint64_t whi = nb ? max(sa + ta, sb2 + tb2) : sa + ta;
+            const Window win = make_window(wlo, (uint32_t)(((whi + 15u) & ~15ull) - wlo + 16u));
+            const uint32_t va = (uint32_t)(sa - wlo), vb = (uint32_t)(sb2 - wlo);
+            const uint32_t nt = na + nb;
+            for (uint32_t u0 = 0; u0 < nt; u0 += 64u * U) {
                 uint4 c0[U], c1[U];
 #pragma unroll
                 for (int k = 0; k < U; ++k) {               // every load of the step first
-                    const uint32_t u = u0 + 64u * k + lane;
-                    c0[k] = load_win<true>(f.win, u < f.nu ? 16u * u : WIN_OOB);
-                    c1[k] = load_win<true>(f.win, u < f.nu && f.s ? 16u * u + 16u : WIN_OOB);
+                    const uint32_t x = u0 + 64u * k + lane;
+                    const bool inb = x >= na;
+                    const uint32_t u = inb ? x - na : x, v = inb ? vb : va;
+                    const bool ok = x < nt, sh = ((inb ? sb2 : sa) & 15u) != 0;
+                    c0[k] = load_win<true>(win, ok ? v - (v & 15u) + 16u * u : WIN_OOB);
+                    c1[k] = load_win<true>(win, ok && sh ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
                 }
 #pragma unroll
                 for (int k = 0; k < U; ++k) {
-                    const uint32_t u = u0 + 64u * k + lane;
-                    if (u >= f.nu) continue;
+                    const uint32_t x = u0 + 64u * k + lane;
+                    if (x >= nt) continue;
+                    const bool inb = x >= na;
+                    const uint32_t u = inb ? x - na : x;
+                    const uint32_t s = (uint32_t)((inb ? sb2 : sa) & 15u), q = s >> 2, sbb = s & 3u;
+                    const uint32_t tl = inb ? tb2 : ta, at = inb ? atb : ata;
                     const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-                    uint32_t x[4];
+                    uint32_t xw[4];
 #pragma unroll
                     for (int w = 0; w < 4; ++w)             // bytes [s, s + 16) of the 32 loaded
-                        x[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
-                                                          sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sb);
-                    const uint32_t b0 = 16u * u, nb = min(16u, f.tl - b0);
-                    uint8_t* o = t + f.at + b0;
-                    if (nb < 16u) {                         // the fragment's last, partial unit
+                        xw[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
+                                                           sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sbb);
+                    const uint32_t b0 = 16u * u, nbytes = min(16u, tl - b0);
+                    uint8_t* o = t + at + b0;
+                    const uint32_t oa = (uint32_t)((tb + at + b0) & 15u);
+                    if (nbytes < 16u) {                     // the fragment's last, partial unit
 #pragma unroll
                         for (int w = 0; w < 4; ++w) {
                             const uint32_t lo = 4u * w;
-                            x[w] = nb <= lo ? 0u : nb >= lo + 4u ? x[w] : x[w] & ((1u << (8u * (nb - lo))) - 1u);
+                            xw[w] = nbytes <= lo ? 0u : nbytes >= lo + 4u ? xw[w] : xw[w] & ((1u << (8u * (nbytes - lo))) - 1u);
                         }
-                        for (uint32_t qq = 0; qq < nb; ++qq) o[qq] = (uint8_t)(x[qq >> 2] >> (8u * (qq & 3u)));
-                    } else if (f.o16) {
-                        *reinterpret_cast<uint4*>(o) = make_uint4(x[0], x[1], x[2], x[3]);
-                    } else if (t8) {
-                        reinterpret_cast<uint2*>(o)[0] = make_uint2(x[0], x[1]);
-                        reinterpret_cast<uint2*>(o)[1] = make_uint2(x[2], x[3]);
+                        for (uint32_t qq = 0; qq < nbytes; ++qq) o[qq] = (uint8_t)(xw[qq >> 2] >> (8u * (qq & 3u)));
+                    } else if (oa == 0u) {
+                        *reinterpret_cast<uint4*>(o) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+                    } else if ((oa & 7u) == 0u) {
+                        reinterpret_cast<uint2*>(o)[0] = make_uint2(xw[0], xw[1]);
+                        reinterpret_cast<uint2*>(o)[1] = make_uint2(xw[2], xw[3]);
                     } else {
 #pragma unroll
-                        for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = x[w];
+                        for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = xw[w];
                     }
-                    acc = dot2_add(x[3], dot2_add(x[2], dot2_add(x[1], dot2_add(x[0], acc))));   // even offset
-                    if (f.at + b0 == 0u) {                  // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
-                        w0 = x[0];
-                        w1 = x[1];
+                    acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));   // even offset
+                    if (at + b0 == 0u) {                    // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
+                        w0 = xw[0];
+                        w1 = xw[1];
                     }
                 }
             }
+            j = (j2 == j ? j : j2) + 4u;
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
         w0 = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(w0), 63);
