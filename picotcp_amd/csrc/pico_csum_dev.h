@@ -361,7 +361,7 @@ __device__ __noinline__ int walk_dst(const uint8_t* __restrict__ h, uint32_t ava
 
 // Returns kind + 1 | net_len << 8 | proto << 24 | f->frag << 32 (the last fragment header's
 // offset / M field, :754) -- registers only, no stack slots for outputs.
-__device__ __noinline__ __attribute__((unused)) uint64_t ipv6_walk_packed(const uint8_t* __restrict__ h,
+__device__ __forceinline__ uint64_t ipv6_walk_packed(const uint8_t* __restrict__ h,
                                                                            uint32_t avail) {
     const uint32_t plen = ((uint32_t)h[4] << 8) | h[5];
     uint32_t nx = h[6], b, ptr = 40u;
