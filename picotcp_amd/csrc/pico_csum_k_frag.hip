@@ -26,19 +26,44 @@
 //      which must be the last in tree order), copies the first fragment's 20 (IPv6: 40) header bytes,
 //      then gathers fragments 0 mod 4;
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
-//      16-byte units, 3 x 64 units per wave per step (two 1480-byte payloads), every load issued
-//      before any is used: two aligned 16-byte loads through one buffer window over both
-//      payloads (out-of-range slots read zeros, no branches) and a shift by the unit's payload
-//      alignment (dword select + alignbyte); stores are 16-, 8- or 4-byte at the unit's place in
-//      the transport (which starts 4-byte aligned, offsets being multiples of 8), only where the
-//      fragment fits the output region; v_dot2 sums on the fly (every unit is a whole number of
-//      checksum words); a workgroup reduction at the end.  (One fragment per step, 2 x 64
-//      units: c3_reasm 154.6 -> 148.9 us, c3_reasm6 171.9 -> 162.0 us, profiles/r03/ab_frag2.txt.)
+//      16-byte units, 3 x 64 units per wave per step (two 1480-byte payloads): two aligned
+//      16-byte loads per unit through one buffer window over both payloads (out-of-range slots
+//      read zeros, no branches) and a shift by the unit's payload alignment (dword select +
+//      alignbyte); v_dot2 sums on the fly (every unit is a whole number of checksum words); a
+//      workgroup reduction at the end.  Software-pipelined over two register sets: the next
+//      step's loads are issued before this step's stores, and the stores are a fixed sequence
+//      per unit (one 16-byte store if the unit is whole and 16-byte aligned in the output, else
+//      dwords, then the bytes of a last partial dword; the others at an out-of-range offset), so
+//      the loads are waited on with the stores still in flight.  The fragments' metadata is
+//      held in registers across two lanes' worth of indices (no LDS reads in the loop).
+//      Measured (profiles/r03): one fragment per step 154.6 / 171.9 us (c3_reasm / c3_reasm6),
+//      pairs 148.9 / 162.0 us (ab_frag2.txt), pipelined 144.8 / 153.4 us (ab_frag_pipe.txt);
+//      without the stores 89.5 / 97.6 us, without the gather 18.2 / 26.2 us (ab_frag_ablate.txt,
+//      FRAG_AB measurement builds).
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
 namespace {
 
+// min / max of two device addresses (< 2^63) from the sign of their difference: scalar ALU only
+// (a 64-bit compare is a vector instruction, whose temporaries inside the pipelined gather get
+// waited on)
+__device__ __forceinline__ uint64_t min64s(uint64_t a, uint64_t b) {
+    return ((a - b) >> 63) ? a : b;
+}
+__device__ __forceinline__ uint64_t max64s(uint64_t a, uint64_t b) {
+    return ((a - b) >> 63) ? b : a;
+}
+
+// sel4 as three selects (the nested form compiles to branches inside the pipelined gather)
+__device__ __forceinline__ uint32_t sel4s(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t lo = (q & 1u) ? b : a, hi = (q & 1u) ? d : c;
+    return (q & 2u) ? hi : lo;
+}
+
+#ifndef FRAG_AB
+#define FRAG_AB 0       // measurement builds only: 1 = no gather stores, 2 = no gather
+#endif
 constexpr uint32_t FRAG_MAX = 512;     // fragments per datagram handled on device
 
 struct FragArgs {
@@ -205,100 +230,182 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
     }
 
     // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order, two
-    //         at a time), each kept fragment at its own offset
+    //         at a time), each kept fragment at its own offset.  Software-pipelined: a step's
+    //         loads are issued before the previous step is stored, and every load and store of a
+    //         step is issued unconditionally (buffer operations, out-of-range offsets do nothing),
+    //         so the in-order vmcnt the loads are waited on never includes the stores before them.
     uint32_t acc = 0, w0 = 0, w1 = 0;
     if (!bad) {
         const uint64_t tb = reinterpret_cast<uintptr_t>(t);
+        const Window ow = make_window(tb, cap);           // the transport part of the output region
         // a kept fragment the output region can hold (else its datagram is not reassembled:
         // past the region's end, or larger than it); wave-uniform
-        auto gathered = [&](uint32_t j) {
-            const uint32_t kj = L.key[j];
-            return (kj >> 24) == 0 && (kj & 0xFFFFu) + L.tl[j] <= cap;
+        auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+        // this wave's fragments (j = w + 4 i, i < 128) held in two lanes' registers, read once: the
+        // loop below reads no LDS (an LDS read there would wait on the loads issued ahead of it)
+        const uint32_t w = uni(wv);
+        uint32_t ck[2], ct[2], cl[2], ch[2];
+        uint64_t gm[2];                       // bit i: fragment i is gathered
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t j = w + 4u * (lane + 64u * h);
+            const bool in = j < cnt;
+            ck[h] = in ? L.key[j] : 0u;
+            ct[h] = in ? L.tl[j] : 0u;
+            const uint64_t x = in ? L.src[j] : 0ull;
+            cl[h] = (uint32_t)x;
+            ch[h] = (uint32_t)(x >> 32);
+            // kept, and inside the output region (else the datagram is not reassembled: past the
+            // region's end, or larger than it)
+            gm[h] = __builtin_amdgcn_ballot_w64(in && (ck[h] >> 24) == 0 && (ck[h] & 0xFFFFu) + ct[h] <= cap);
+        }
+        auto field = [](const uint32_t (&c)[2], uint32_t i) {
+            return (uint32_t)(i < 64u ? __builtin_amdgcn_readlane((int)c[0], (int)i)
+                                      : __builtin_amdgcn_readlane((int)c[1], (int)(i - 64u)));
         };
+        auto next_gathered = [&](uint32_t i) {        // first gathered i' >= i, else 128
+            if (i < 64u) {
+                const uint64_t m = gm[0] & (~0ull << i);
+                if (m) return (uint32_t)__builtin_ctzll(m);
+                i = 64u;
+            }
+            const uint64_t m = i < 128u ? gm[1] & (~0ull << (i - 64u)) : 0ull;
+            return m ? 64u + (uint32_t)__builtin_ctzll(m) : 128u;
+        };
+        auto src_of = [&](uint32_t i) { return ((uint64_t)field(ch, i) << 32) | field(cl, i); };
         constexpr int U = 3;                   // 64-unit slots per step: two 1480 B payloads
-        uint32_t j = wv;
-        while (true) {
-            while (j < cnt && !gathered(j)) j += 4u;
-            if (j >= cnt) break;
-            uint32_t j2 = j + 4u;
-            while (j2 < cnt && !gathered(j2)) j2 += 4u;
-            // fragment A = j and (if any) B = j2: units [0, na) are A's, [na, na + nb) B's, read
-            // through one buffer window over both payloads' 16-byte lines when they lie within
-            // 1 GiB of each other (else B waits for the next step)
-            const uint64_t sa = L.src[j];
-            const uint32_t ta = L.tl[j], na = (ta + 15u) >> 4, ata = L.key[j] & 0xFFFFu;
-            uint64_t sb2 = sa;
-            uint32_t tb2 = 0, nb = 0, atb = 0;
-            if (j2 < cnt) {
-                sb2 = L.src[j2];
-                tb2 = L.tl[j2];
-                const uint64_t lo = min(sa, sb2) & ~15ull, hi = max(sa + ta, sb2 + tb2) + 16u;
+        struct Step {                          // plain scalars (a buffer resource inside a copied
+            uint64_t wlo;                      // struct ends up in an LDS-promoted alloca)
+            uint32_t wsz, i, i2, va, vb, na, nt, ta, tb, ata, atb, sa, sb, u0, valid;
+        };
+        // fragment A = i and (if any) B = i2: units [0, na) are A's, [na, nt) B's, read through
+        // one buffer window over both payloads' 16-byte lines when they lie within 1 GiB of each
+        // other (else B waits for the next step)
+        auto make_pair = [&](uint32_t i0) {
+            Step st;
+            const uint32_t i = next_gathered(i0);
+            st.valid = i < 128u;
+            st.u0 = 0;
+            st.i = st.i2 = i;
+            st.wlo = tb;
+            st.wsz = 0;
+            st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.sa = st.sb = 0;
+            if (!st.valid) return st;
+            const uint32_t i2 = next_gathered(i + 1u);
+            const uint64_t sa = src_of(i);
+            st.ta = field(ct, i);
+            st.na = (st.ta + 15u) >> 4;
+            st.ata = field(ck, i) & 0xFFFFu;
+            uint64_t sb = sa;
+            st.tb = st.atb = 0;
+            uint32_t nb = 0;
+            if (i2 < 128u) {
+                sb = src_of(i2);
+                const uint32_t tb2 = field(ct, i2);
+                const uint64_t lo = min64s(sa, sb) & ~15ull, hi = max64s(sa + st.ta, sb + tb2) + 16u;
                 if (hi - lo < (1ull << 30)) {
                     nb = (tb2 + 15u) >> 4;
-                    atb = L.key[j2] & 0xFFFFu;
+                    st.tb = tb2;
+                    st.atb = field(ck, i2) & 0xFFFFu;
+                    st.i2 = i2;
                 } else {
-                    j2 = j;                      // B next step
-                }
-            } else {
-                j2 = j;
-            }
-            const uint64_t wlo = (nb ? min(sa, sb2) : sa) & ~15ull;
-            const uint64_t whi = nb ? max(sa + ta, sb2 + tb2) : sa + ta;
-            const Window win = make_window(wlo, (uint32_t)(((whi + 15u) & ~15ull) - wlo + 16u));
-            const uint32_t va = (uint32_t)(sa - wlo), vb = (uint32_t)(sb2 - wlo);
-            const uint32_t nt = na + nb;
-            for (uint32_t u0 = 0; u0 < nt; u0 += 64u * U) {
-                uint4 c0[U], c1[U];
-#pragma unroll
-                for (int k = 0; k < U; ++k) {               // every load of the step first
-                    const uint32_t x = u0 + 64u * k + lane;
-                    const bool inb = x >= na;
-                    const uint32_t u = inb ? x - na : x, v = inb ? vb : va;
-                    const bool ok = x < nt, sh = ((inb ? sb2 : sa) & 15u) != 0;
-                    c0[k] = load_win<true>(win, ok ? v - (v & 15u) + 16u * u : WIN_OOB);
-                    c1[k] = load_win<true>(win, ok && sh ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
-                }
-#pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    const uint32_t x = u0 + 64u * k + lane;
-                    if (x >= nt) continue;
-                    const bool inb = x >= na;
-                    const uint32_t u = inb ? x - na : x;
-                    const uint32_t s = (uint32_t)((inb ? sb2 : sa) & 15u), q = s >> 2, sbb = s & 3u;
-                    const uint32_t tl = inb ? tb2 : ta, at = inb ? atb : ata;
-                    const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-                    uint32_t xw[4];
-#pragma unroll
-                    for (int w = 0; w < 4; ++w)             // bytes [s, s + 16) of the 32 loaded
-                        xw[w] = __builtin_amdgcn_alignbyte(sel4(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
-                                                           sel4(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sbb);
-                    const uint32_t b0 = 16u * u, nbytes = min(16u, tl - b0);
-                    uint8_t* o = t + at + b0;
-                    const uint32_t oa = (uint32_t)((tb + at + b0) & 15u);
-                    if (nbytes < 16u) {                     // the fragment's last, partial unit
-#pragma unroll
-                        for (int w = 0; w < 4; ++w) {
-                            const uint32_t lo = 4u * w;
-                            xw[w] = nbytes <= lo ? 0u : nbytes >= lo + 4u ? xw[w] : xw[w] & ((1u << (8u * (nbytes - lo))) - 1u);
-                        }
-                        for (uint32_t qq = 0; qq < nbytes; ++qq) o[qq] = (uint8_t)(xw[qq >> 2] >> (8u * (qq & 3u)));
-                    } else if (oa == 0u) {
-                        *reinterpret_cast<uint4*>(o) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
-                    } else if ((oa & 7u) == 0u) {
-                        reinterpret_cast<uint2*>(o)[0] = make_uint2(xw[0], xw[1]);
-                        reinterpret_cast<uint2*>(o)[1] = make_uint2(xw[2], xw[3]);
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < 4; ++w) reinterpret_cast<uint32_t*>(o)[w] = xw[w];
-                    }
-                    acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));   // even offset
-                    if (at + b0 == 0u) {                    // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
-                        w0 = xw[0];
-                        w1 = xw[1];
-                    }
+                    sb = sa;
                 }
             }
-            j = (j2 == j ? j : j2) + 4u;
+            const uint64_t wlo = (nb ? min64s(sa, sb) : sa) & ~15ull;
+            const uint64_t whi = nb ? max64s(sa + st.ta, sb + st.tb) : sa + st.ta;
+            st.wlo = wlo;
+            st.wsz = (uint32_t)(((whi + 15u) & ~15ull) - wlo + 16u);
+            st.va = (uint32_t)(sa - wlo);
+            st.vb = (uint32_t)(sb - wlo);
+            st.sa = (uint32_t)(sa & 15u);
+            st.sb = (uint32_t)(sb & 15u);
+            st.nt = st.na + nb;
+            return st;
+        };
+        auto next_step = [&](const Step& c) {
+            Step n = c;
+            if (c.u0 + 64u * U < c.nt) n.u0 += 64u * U;
+            else n = make_pair((c.i2 == c.i ? c.i : c.i2) + 1u);
+            return n;
+        };
+        auto issue = [&](const Step& st, uint4 (&c0)[U], uint4 (&c1)[U]) {
+            const Window win = make_window(st.wlo, st.wsz);   // empty for an invalid step
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t x = st.u0 + 64u * k + lane;
+                const bool inb = x >= st.na;
+                const uint32_t u = inb ? x - st.na : x, v = inb ? st.vb : st.va;
+                const bool ok = st.valid && x < st.nt, sh = (inb ? st.sb : st.sa) != 0u;
+                c0[k] = load_win<true>(win, ok ? v - (v & 15u) + 16u * u : WIN_OOB);
+                c1[k] = load_win<true>(win, ok && sh ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
+            }
+        };
+        auto process = [&](const Step& st, const uint4 (&c0)[U], const uint4 (&c1)[U]) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint32_t x = st.u0 + 64u * k + lane;
+                const bool ok = x < st.nt;
+                const bool inb = x >= st.na;
+                const uint32_t u = inb ? x - st.na : x;
+                const uint32_t s = inb ? st.sb : st.sa, q = s >> 2, sbb = s & 3u;
+                const uint32_t tl = inb ? st.tb : st.ta, at = inb ? st.atb : st.ata;
+                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+                uint32_t xw[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)                 // bytes [s, s + 16) of the 32 loaded
+                    xw[w] = __builtin_amdgcn_alignbyte(sel4s(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
+                                                       sel4s(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sbb);
+                const uint32_t b0 = 16u * u, nbytes = ok ? min(16u, tl - b0) : 0u, ob = at + b0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {               // bytes past the fragment read as zero
+                    const uint32_t kb = min((uint32_t)max((int)nbytes - 4 * w, 0), 4u);
+                    xw[w] &= (uint32_t)(0xFFFFFFFFull >> (32u - 8u * kb));
+                }
+                // stores: one 16-byte store for a whole, 16-byte aligned unit, else dwords, then the
+                // last partial dword's bytes -- 8 store instructions per slot, out-of-range ones void
+                const uint32_t so = FRAG_AB == 1 ? ob | WIN_OOB : ob;   // (measurement builds: no stores)
+                const bool whole = nbytes == 16u, a16 = whole && ((tb + ob) & 15u) == 0u;
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
+                                                       (int)(a16 ? so : WIN_OOB), 0, 0);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    __builtin_amdgcn_raw_buffer_store_b32(xw[w], ow.rsrc,
+                                                          (int)(!a16 && 4u * w + 4u <= nbytes ? so + 4u * w : WIN_OOB),
+                                                          0, 0);
+                const uint32_t pw = nbytes >> 2, nr = nbytes & 3u;
+                const uint32_t tw = sel4s(pw & 3u, xw[0], xw[1], xw[2], xw[3]);
+#pragma unroll
+                for (uint32_t i = 0; i < 3; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * i)), ow.rsrc,
+                                                         (int)(i < nr ? so + 4u * pw + i : WIN_OOB), 0, 0);
+                acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));   // even offset
+                if (ok && ob == 0u) {                       // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
+                    w0 = xw[0];
+                    w1 = xw[1];
+                }
+            }
+        };
+        uint4 a0[U], a1[U], b0[U], b1[U];
+        Step cur = make_pair(0u);
+#if FRAG_AB == 2
+        cur.valid = 0;
+#endif
+        if (cur.valid) {
+            issue(cur, a0, a1);
+            for (;;) {                         // two steps per trip, alternating register sets
+                const Step n1 = next_step(cur);
+                issue(n1, b0, b1);
+                __builtin_amdgcn_sched_barrier(0);   // the next step's loads stay ahead of these stores
+                process(cur, a0, a1);
+                if (!n1.valid) break;
+                const Step n2 = next_step(n1);
+                issue(n2, a0, a1);
+                __builtin_amdgcn_sched_barrier(0);
+                process(n1, b0, b1);
+                if (!n2.valid) break;
+                cur = n2;
+            }
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
         w0 = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(w0), 63);
