@@ -12,9 +12,9 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// One workgroup (4 waves) per datagram (its fragments are a contiguous descriptor range, in
-// arrival order):
-//   1. all 256 threads parse the fragment headers (IPv4: IHL, total length, MF, offset; IPv6: the
+// One workgroup (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are
+// a contiguous descriptor range, in arrival order):
+//   1. all threads parse the fragment headers (IPv4: IHL, total length, MF, offset; IPv6: the
 //      extension-header walk, payload length, M, offset, protocol) into LDS and
 //      mark repeated offsets (pico_tree_insert rejects a repeated key: the earliest arrival
 //      of each offset is kept);
@@ -24,7 +24,7 @@
 //      (rank by offset among the kept fragments, LDS broadcast reads; a wave prefix scan of
 //      the sorted transport lengths against the offsets, up to the first fragment without MF,
 //      which must be the last in tree order), copies the first fragment's 20 (IPv6: 40) header bytes,
-//      then gathers fragments 0 mod 4;
+//      then gathers fragments 0 mod 4 (one wave per datagram: the same, in order);
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
 //      16-byte units, 3 x 64 units per wave per step (two 1480-byte payloads): two aligned
 //      16-byte loads per unit through one buffer window over both payloads (out-of-range slots
@@ -39,7 +39,8 @@
 //      Measured (profiles/r03): one fragment per step 154.6 / 171.9 us (c3_reasm / c3_reasm6),
 //      pairs 148.9 / 162.0 us (ab_frag2.txt), pipelined 144.8 / 153.4 us (ab_frag_pipe.txt);
 //      without the stores 89.5 / 97.6 us, without the gather 18.2 / 26.2 us (ab_frag_ablate.txt,
-//      FRAG_AB measurement builds).
+//      FRAG_AB measurement builds); one wave per datagram at 4096 datagrams 145.6 / 154.8 us vs
+//      149.0 / 157.9 at four (ab_frag_wpd.txt).
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
@@ -61,6 +62,9 @@ __device__ __forceinline__ uint32_t sel4s(uint32_t q, uint32_t a, uint32_t b, ui
     return (q & 2u) ? hi : lo;
 }
 
+#ifndef FRAG_WPD_FORCE
+#define FRAG_WPD_FORCE 0   // measurement builds only: waves per datagram (1, 4) regardless of batch size
+#endif
 #ifndef FRAG_AB
 #define FRAG_AB 0       // measurement builds only: 1 = no gather stores, 2 = no gather
 #endif
@@ -94,9 +98,11 @@ struct FragLds {
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*p; }
 
-template <bool V6>
-__global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
+// WPD waves per datagram (1 or 4; the launcher picks it from the batch size)
+template <bool V6, int WPD>
+__global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;          // PICO_SIZE_IP6HDR / PICO_SIZE_IP4HDR
+    constexpr uint32_t NT = 64u * WPD;
     __shared__ FragLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t g = blockIdx.x;
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
     //         tot - net_len, frag); IPv6 as pico_ipv6_extension_headers does (the walk must reach
     //         the transport behind a fragment header; transport_len = payload_len - (net_len - 40))
     if (!bad0) {
-        for (uint32_t j = tid; j < cnt; j += 256u) {
+        for (uint32_t j = tid; j < cnt; j += NT) {
             const pico_csum_desc_dev d = p.frag[first + j];
             uint32_t key = 0, tl = 0, hl = 0;
             if (d.len < HDR || d.off > p.base_len || d.len > p.base_len - d.off) {
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
     __syncthreads();
     bool bad = L.bad != 0;                              // workgroup-uniform
     if (!bad) {                                         // repeated offsets: the earliest arrival stays
-        for (uint32_t j = tid; j < cnt; j += 256u) {
+        for (uint32_t j = tid; j < cnt; j += NT) {
             const uint32_t fj = L.key[j] & 0xFFFFu;
             bool dup = false;
             for (uint32_t k = 0; k < j; ++k) dup |= (L.key[k] & 0xFFFFu) == fj;
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
         }
     }
 
-    // ---- 3. gather + checksum, all waves (wave w: fragments w, w + 4, ... in arrival order, two
+    // ---- 3. gather + checksum, all waves (wave w: fragments w, w + WPD, ... in arrival order, two
     //         at a time), each kept fragment at its own offset.  Software-pipelined: a step's
     //         loads are issued before the previous step is stored, and every load and store of a
     //         step is issued unconditionally (buffer operations, out-of-range offsets do nothing),
@@ -241,36 +247,37 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
         // a kept fragment the output region can hold (else its datagram is not reassembled:
         // past the region's end, or larger than it); wave-uniform
         auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
-        // this wave's fragments (j = w + 4 i, i < 128) held in two lanes' registers, read once: the
-        // loop below reads no LDS (an LDS read there would wait on the loads issued ahead of it)
+        // this wave's fragments j = w + WPD i, held 64 at a time in one register per field (lane
+        // i - cb: fragment i), read when the walk enters the block: the loop below reads no LDS
+        // inside a block (an LDS read there waits on the loads issued ahead of it)
         const uint32_t w = uni(wv);
-        uint32_t ck[2], ct[2], cl[2], ch[2];
-        uint64_t gm[2];                       // bit i: fragment i is gathered
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t j = w + 4u * (lane + 64u * h);
+        const uint32_t nidx = cnt > w ? (cnt - w + WPD - 1u) / WPD : 0u;   // this wave's fragments
+        constexpr uint32_t NONE_I = 0xFFFFFFFFu;
+        uint32_t cb = 0, ck, ct, cl, ch;
+        uint64_t gm;                          // bit i - cb: fragment i is gathered
+        auto load_block = [&](uint32_t b) {
+            cb = b;
+            const uint32_t j = w + WPD * (b + lane);
             const bool in = j < cnt;
-            ck[h] = in ? L.key[j] : 0u;
-            ct[h] = in ? L.tl[j] : 0u;
+            ck = in ? L.key[j] : 0u;
+            ct = in ? L.tl[j] : 0u;
             const uint64_t x = in ? L.src[j] : 0ull;
-            cl[h] = (uint32_t)x;
-            ch[h] = (uint32_t)(x >> 32);
+            cl = (uint32_t)x;
+            ch = (uint32_t)(x >> 32);
             // kept, and inside the output region (else the datagram is not reassembled: past the
             // region's end, or larger than it)
-            gm[h] = __builtin_amdgcn_ballot_w64(in && (ck[h] >> 24) == 0 && (ck[h] & 0xFFFFu) + ct[h] <= cap);
-        }
-        auto field = [](const uint32_t (&c)[2], uint32_t i) {
-            return (uint32_t)(i < 64u ? __builtin_amdgcn_readlane((int)c[0], (int)i)
-                                      : __builtin_amdgcn_readlane((int)c[1], (int)(i - 64u)));
+            gm = __builtin_amdgcn_ballot_w64(in && (ck >> 24) == 0 && (ck & 0xFFFFu) + ct <= cap);
         };
-        auto next_gathered = [&](uint32_t i) {        // first gathered i' >= i, else 128
-            if (i < 64u) {
-                const uint64_t m = gm[0] & (~0ull << i);
-                if (m) return (uint32_t)__builtin_ctzll(m);
-                i = 64u;
+        load_block(0);
+        auto field = [&](uint32_t c, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)c, (int)(i - cb)); };
+        auto next_gathered = [&](uint32_t i) {        // first gathered i' >= i (its block loaded), else NONE_I
+            for (;;) {
+                if (i >= nidx) return NONE_I;
+                if (i >= cb + 64u) load_block(i & ~63u);
+                const uint64_t m = gm & (~0ull << (i - cb));
+                if (m) return cb + (uint32_t)__builtin_ctzll(m);
+                i = cb + 64u;
             }
-            const uint64_t m = i < 128u ? gm[1] & (~0ull << (i - 64u)) : 0ull;
-            return m ? 64u + (uint32_t)__builtin_ctzll(m) : 128u;
         };
         auto src_of = [&](uint32_t i) { return ((uint64_t)field(ch, i) << 32) | field(cl, i); };
         constexpr int U = 3;                   // 64-unit slots per step: two 1480 B payloads
@@ -284,22 +291,22 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
         auto make_pair = [&](uint32_t i0) {
             Step st;
             const uint32_t i = next_gathered(i0);
-            st.valid = i < 128u;
+            st.valid = i != NONE_I;
             st.u0 = 0;
             st.i = st.i2 = i;
             st.wlo = tb;
             st.wsz = 0;
             st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.sa = st.sb = 0;
             if (!st.valid) return st;
-            const uint32_t i2 = next_gathered(i + 1u);
             const uint64_t sa = src_of(i);
             st.ta = field(ct, i);
             st.na = (st.ta + 15u) >> 4;
             st.ata = field(ck, i) & 0xFFFFu;
+            const uint32_t i2 = next_gathered(i + 1u);   // (may move the block past i)
             uint64_t sb = sa;
             st.tb = st.atb = 0;
             uint32_t nb = 0;
-            if (i2 < 128u) {
+            if (i2 != NONE_I) {
                 sb = src_of(i2);
                 const uint32_t tb2 = field(ct, i2);
                 const uint64_t lo = min64s(sa, sb) & ~15ull, hi = max64s(sa + st.ta, sb + tb2) + 16u;
@@ -424,9 +431,13 @@ __global__ __launch_bounds__(256) void reassemble_kernel(FragArgs p) {
         uint32_t l4 = 0, v = V_MALFORMED;
         const uint32_t len = L.len, proto = L.proto;
         if (!bad) {
-            const uint32_t s = L.acc[0] + L.acc[1] + L.acc[2] + L.acc[3];
-            const uint32_t word0 = L.w0[0] | L.w0[1] | L.w0[2] | L.w0[3];
-            const uint32_t word1 = L.w1[0] | L.w1[1] | L.w1[2] | L.w1[3];
+            uint32_t s = 0, word0 = 0, word1 = 0;
+#pragma unroll
+            for (int k = 0; k < WPD; ++k) {
+                s += L.acc[k];
+                word0 |= L.w0[k];
+                word1 |= L.w1[k];
+            }
             v = V_ACCEPT;
             if constexpr (!V6) {
                 if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
@@ -469,9 +480,19 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     FragArgs a{static_cast<const uint8_t*>(base), flags, base_len, static_cast<const pico_csum_desc_dev*>(frag),
                groups, n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
                static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict};
-    const dim3 grid(n_dgram), block(256);
-    if (v6) hipLaunchKernelGGL(reassemble_kernel<true>, grid, block, 0, static_cast<hipStream_t>(stream), a);
-    else hipLaunchKernelGGL(reassemble_kernel<false>, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    // waves per datagram: 4 each while the batch is small, 1 each once the batch fills the chip's
+    // one-wave workgroup slots (16 per CU, LDS-bound): c3_reasm (4096 datagrams) 145.6 vs 149.0 us
+    // at 4 waves, 2 waves 165.0 us (2560 slots: a partial second round), ab_frag_wpd.txt
+    const int wpd = FRAG_WPD_FORCE ? FRAG_WPD_FORCE : n_dgram >= 3072u ? 1 : 4;
+    const dim3 grid(n_dgram), block(64 * wpd);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (wpd == 1) {
+        if (v6) hipLaunchKernelGGL((reassemble_kernel<true, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((reassemble_kernel<false, 1>), grid, block, 0, s, a);
+    } else {
+        if (v6) hipLaunchKernelGGL((reassemble_kernel<true, 4>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((reassemble_kernel<false, 4>), grid, block, 0, s, a);
+    }
     return (int)hipGetLastError();
 }
 

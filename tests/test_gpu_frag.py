@@ -163,3 +163,22 @@ def test_ipv6_reassembly_limits():
     buf[f4 + 6] = 17                                     # no fragment header: UDP straight away
     wl, wv = check(buf, d, grp, od, size, v6=True)
     assert (wv == 8).all()
+
+
+@pytest.mark.parametrize("v6", [False, True])
+@pytest.mark.parametrize("n", [1600, 3200])
+def test_batch_shapes(n, v6):
+    """Batches below and above the launcher's switch to one wave per datagram (3072), with
+    datagrams of more than 64 fragments per wave (the gather's metadata blocks)."""
+    rng = np.random.default_rng(n + v6)
+    lens = rng.integers(0, 3000, n)
+    lens[rng.integers(0, n, 24)] = rng.integers(8200, 9000, 24)   # 129-141 fragments of 64 B
+    lens = lens.tolist()
+    if v6:
+        buf, off, flen, grp = synth.ipv6_fragments(lens, seed=n, proto=6, frag_payload=64)
+    else:
+        buf, off, flen, grp = synth.ipv4_fragments(lens, seed=n, proto=6, frag_payload=64)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=4, hdr=40 if v6 else 20)
+    wl, wv = check(buf, d, grp, od, size, v6=v6)
+    assert (wv != 8).all() and (wl == np.array(lens)).all()
