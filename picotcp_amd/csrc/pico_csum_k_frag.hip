@@ -40,7 +40,8 @@
 //      pairs 148.9 / 162.0 us (ab_frag2.txt), pipelined 144.8 / 153.4 us (ab_frag_pipe.txt);
 //      without the stores 89.5 / 97.6 us, without the gather 18.2 / 26.2 us (ab_frag_ablate.txt,
 //      FRAG_AB measurement builds); one wave per datagram at 4096 datagrams 145.6 / 154.8 us vs
-//      149.0 / 157.9 at four (ab_frag_wpd.txt).
+//      149.0 / 157.9 at four (ab_frag_wpd.txt).  Stores keep the default cache policy: nt 194 /
+//      201 us, sc1 244 / 255 us (ab_frag_saux.txt).
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 for (int w = 0; w < 4; ++w)
                     __builtin_amdgcn_raw_buffer_store_b32(xw[w], ow.rsrc,
                                                           (int)(!a16 && 4u * w + 4u <= nbytes ? so + 4u * w : WIN_OOB),
-                                                          0, 0);
+                                                          0, FRAG_STORE_AUX);
                 const uint32_t pw = nbytes >> 2, nr = nbytes & 3u;
                 const uint32_t tw = sel4s(pw & 3u, xw[0], xw[1], xw[2], xw[3]);
 #pragma unroll
