@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 for (int w = 0; w < 4; ++w)
                     __builtin_amdgcn_raw_buffer_store_b32(xw[w], ow.rsrc,
                                                           (int)(!a16 && 4u * w + 4u <= nbytes ? so + 4u * w : WIN_OOB),
-                                                          0, FRAG_STORE_AUX);
+                                                          0, 0);
                 const uint32_t pw = nbytes >> 2, nr = nbytes & 3u;
                 const uint32_t tw = sel4s(pw & 3u, xw[0], xw[1], xw[2], xw[3]);
 #pragma unroll
