@@ -155,6 +155,7 @@ __device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool NT>
 __device__ __forceinline__ uint4 load_chunk_t(const uint8_t* a0, uint32_t k) {

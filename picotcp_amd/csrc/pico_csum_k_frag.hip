@@ -26,14 +26,15 @@
 //      which must be the last in tree order), copies the first fragment's 20 (IPv6: 40) header bytes,
 //      then gathers fragments 0 mod 4 (one wave per datagram: the same, in order);
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
-//      16-byte units, 3 x 64 units per wave per step (two 1480-byte payloads): two aligned
+//      16-byte units on the output's 16-byte lines, 3 x 64 units per wave per step (two 1480-byte
+//      payloads): two aligned
 //      16-byte loads per unit through one buffer window over both payloads (out-of-range slots
 //      read zeros, no branches) and a shift by the unit's payload alignment (dword select +
 //      alignbyte); v_dot2 sums on the fly (every unit is a whole number of checksum words); a
 //      workgroup reduction at the end.  Software-pipelined over two register sets: the next
 //      step's loads are issued before this step's stores, and the stores are a fixed sequence
-//      per unit (one 16-byte store if the unit is whole and 16-byte aligned in the output, else
-//      dwords, then the bytes of a last partial dword; the others at an out-of-range offset), so
+//      per unit (one 16-byte store if the unit is whole, else its whole dwords as a b64 and / or a
+//      b32, then a last partial dword's bytes; the others at an out-of-range offset), so
 //      the loads are waited on with the stores still in flight.  The fragments' metadata is
 //      held in registers across two lanes' worth of indices (no LDS reads in the loop).
 //      Measured (profiles/r03): one fragment per step 154.6 / 171.9 us (c3_reasm / c3_reasm6),
@@ -41,7 +42,9 @@
 //      without the stores 89.5 / 97.6 us, without the gather 18.2 / 26.2 us (ab_frag_ablate.txt,
 //      FRAG_AB measurement builds); one wave per datagram at 4096 datagrams 145.6 / 154.8 us vs
 //      149.0 / 157.9 at four (ab_frag_wpd.txt).  Stores keep the default cache policy: nt 194 /
-//      201 us, sc1 244 / 255 us (ab_frag_saux.txt).
+//      201 us, sc1 244 / 255 us (ab_frag_saux.txt).  Units on the output's 16-byte lines (every
+//      interior unit one aligned b128 store, 5 store instructions per slot instead of 8): 130.6 /
+//      140.2 us vs 145.5 / 154.7 (profiles/r03s2/ab_frag_grid.txt).
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
@@ -284,8 +287,12 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
         constexpr int U = 3;                   // 64-unit slots per step: two 1480 B payloads
         struct Step {                          // plain scalars (a buffer resource inside a copied
             uint64_t wlo;                      // struct ends up in an LDS-promoted alloca)
-            uint32_t wsz, i, i2, va, vb, na, nt, ta, tb, ata, atb, sa, sb, u0, valid;
+            uint32_t wsz, i, i2, va, vb, na, nt, ta, tb, ata, atb, sa, sb, oa, ob, u0, valid;
         };
+        // Units follow the OUTPUT's 16-byte lines: a fragment whose place starts o = (t + offset) & 15
+        // bytes into a line has units [0, (o + tl + 15) / 16), unit u = its bytes [16 u - o, 16 u - o + 16),
+        // so every unit but its first and last is one aligned 16-byte store (units on the payload's own
+        // grid gave dword stores for every unit of a fragment at 8 mod 16).  The loads take the shift.
         // fragment A = i and (if any) B = i2: units [0, na) are A's, [na, nt) B's, read through
         // one buffer window over both payloads' 16-byte lines when they lie within 1 GiB of each
         // other (else B waits for the next step)
@@ -297,31 +304,33 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
             st.i = st.i2 = i;
             st.wlo = tb;
             st.wsz = 0;
-            st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.sa = st.sb = 0;
+            st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.sa = st.sb = st.oa = st.ob = 0;
             if (!st.valid) return st;
-            const uint64_t sa = src_of(i);
-            st.ta = field(ct, i);
-            st.na = (st.ta + 15u) >> 4;
             st.ata = field(ck, i) & 0xFFFFu;
+            st.oa = (uint32_t)((tb + st.ata) & 15u);
+            const uint64_t sa = src_of(i) - st.oa;        // where unit 0 starts (o bytes before the payload)
+            st.ta = field(ct, i);
+            st.na = (st.oa + st.ta + 15u) >> 4;
             const uint32_t i2 = next_gathered(i + 1u);   // (may move the block past i)
             uint64_t sb = sa;
             st.tb = st.atb = 0;
             uint32_t nb = 0;
             if (i2 != NONE_I) {
-                sb = src_of(i2);
+                const uint32_t atb = field(ck, i2) & 0xFFFFu, ob = (uint32_t)((tb + atb) & 15u);
+                const uint64_t sb2 = src_of(i2) - ob;
                 const uint32_t tb2 = field(ct, i2);
-                const uint64_t lo = min64s(sa, sb) & ~15ull, hi = max64s(sa + st.ta, sb + tb2) + 16u;
+                const uint64_t lo = min64s(sa, sb2) & ~15ull, hi = max64s(sa + st.oa + st.ta, sb2 + ob + tb2) + 16u;
                 if (hi - lo < (1ull << 30)) {
-                    nb = (tb2 + 15u) >> 4;
+                    sb = sb2;
+                    nb = (ob + tb2 + 15u) >> 4;
                     st.tb = tb2;
-                    st.atb = field(ck, i2) & 0xFFFFu;
+                    st.atb = atb;
+                    st.ob = ob;
                     st.i2 = i2;
-                } else {
-                    sb = sa;
                 }
             }
             const uint64_t wlo = (nb ? min64s(sa, sb) : sa) & ~15ull;
-            const uint64_t whi = nb ? max64s(sa + st.ta, sb + st.tb) : sa + st.ta;
+            const uint64_t whi = nb ? max64s(sa + st.oa + st.ta, sb + st.ob + st.tb) : sa + st.oa + st.ta;
             st.wlo = wlo;
             st.wsz = (uint32_t)(((whi + 15u) & ~15ull) - wlo + 16u);
             st.va = (uint32_t)(sa - wlo);
@@ -357,40 +366,50 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x;
                 const uint32_t s = inb ? st.sb : st.sa, q = s >> 2, sbb = s & 3u;
-                const uint32_t tl = inb ? st.tb : st.ta, at = inb ? st.atb : st.ata;
+                const uint32_t tl = inb ? st.tb : st.ta, at = inb ? st.atb : st.ata, o = inb ? st.ob : st.oa;
                 const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
                 uint32_t xw[4];
 #pragma unroll
                 for (int w = 0; w < 4; ++w)                 // bytes [s, s + 16) of the 32 loaded
                     xw[w] = __builtin_amdgcn_alignbyte(sel4s(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
                                                        sel4s(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sbb);
-                const uint32_t b0 = 16u * u, nbytes = ok ? min(16u, tl - b0) : 0u, ob = at + b0;
+                // the unit's fragment bytes are [lo, hi) of its 16 (lo = o in unit 0, a multiple of 4;
+                // hi < 16 only in the last unit); the rest is the neighbours' and reads as zero
+                const uint32_t lo = ok && u == 0u ? o : 0u, hi = ok ? min(16u, o + tl - 16u * u) : 0u;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {               // bytes past the fragment read as zero
-                    const uint32_t kb = min((uint32_t)max((int)nbytes - 4 * w, 0), 4u);
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t kb = 4u * w < lo ? 0u : min((uint32_t)max((int)hi - 4 * w, 0), 4u);
                     xw[w] &= (uint32_t)(0xFFFFFFFFull >> (32u - 8u * kb));
                 }
-                // stores: one 16-byte store for a whole, 16-byte aligned unit, else dwords, then the
-                // last partial dword's bytes -- 8 store instructions per slot, out-of-range ones void
-                const uint32_t so = FRAG_AB == 1 ? ob | WIN_OOB : ob;   // (measurement builds: no stores)
-                const bool whole = nbytes == 16u, a16 = whole && ((tb + ob) & 15u) == 0u;
+                // stores, a fixed sequence of 5 per slot (out-of-range ones void): the whole unit as
+                // one aligned 16-byte store; else its whole dwords [a, a + c) as a b64 and / or a b32,
+                // then a last partial dword's bytes as a b16 and / or a b8
+                const uint32_t ou = at + 16u * u - o;       // the unit's place (16-byte aligned in t)
+                const uint32_t so = FRAG_AB == 1 ? ou | WIN_OOB : ou;   // (measurement builds: no stores)
+                const bool whole = lo == 0u && hi == 16u;
+                const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
+                const uint32_t nr = hi > lo ? hi & 3u : 0u;
                 __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
-                                                       (int)(a16 ? so : WIN_OOB), 0, 0);
-#pragma unroll
-                for (int w = 0; w < 4; ++w)
-                    __builtin_amdgcn_raw_buffer_store_b32(xw[w], ow.rsrc,
-                                                          (int)(!a16 && 4u * w + 4u <= nbytes ? so + 4u * w : WIN_OOB),
-                                                          0, 0);
-                const uint32_t pw = nbytes >> 2, nr = nbytes & 3u;
-                const uint32_t tw = sel4s(pw & 3u, xw[0], xw[1], xw[2], xw[3]);
-#pragma unroll
-                for (uint32_t i = 0; i < 3; ++i)
-                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * i)), ow.rsrc,
-                                                         (int)(i < nr ? so + 4u * pw + i : WIN_OOB), 0, 0);
+                                                       (int)(whole ? so : WIN_OOB), 0, 0);
+                const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
+                    (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc,
+                                                      (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, 0);
+                const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc,
+                                                      (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
+                                                     (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, 0);
                 acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));   // even offset
-                if (ok && ob == 0u) {                       // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
-                    w0 = xw[0];
-                    w1 = xw[1];
+                if (ok && at + 16u * u <= o + 4u) {         // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint32_t tp = at + 16u * u + 4u * w - o;   // (wraps below the transport: no match)
+                        w0 |= tp == 0u ? xw[w] : 0u;
+                        w1 |= tp == 4u ? xw[w] : 0u;
+                    }
                 }
             }
         };
