@@ -69,10 +69,19 @@ __device__ __forceinline__ uint32_t sel4s(uint32_t q, uint32_t a, uint32_t b, ui
 #ifndef FRAG_WPD_FORCE
 #define FRAG_WPD_FORCE 0   // measurement builds only: waves per datagram (1, 4) regardless of batch size
 #endif
+#ifndef FRAG_C1DPP
+#define FRAG_C1DPP 1    // a unit's second input line from the next lane's first (DPP) instead of a second load
+#endif
+#ifndef FRAG_UNALIGNED
+#define FRAG_UNALIGNED 1   // one byte-unaligned 16-byte load per unit (0: two aligned loads + shift)
+#endif
 #ifndef FRAG_AB
 #define FRAG_AB 0       // measurement builds only: 1 = no gather stores, 2 = no gather
 #endif
-constexpr uint32_t FRAG_MAX = 512;     // fragments per datagram handled on device
+#ifndef FRAG_MAX_N
+#define FRAG_MAX_N 512
+#endif
+constexpr uint32_t FRAG_MAX = FRAG_MAX_N;   // fragments per datagram handled on device
 
 struct FragArgs {
     const uint8_t* base;
@@ -355,7 +364,19 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 const uint32_t u = inb ? x - st.na : x, v = inb ? st.vb : st.va;
                 const bool ok = st.valid && x < st.nt, sh = (inb ? st.sb : st.sa) != 0u;
                 c0[k] = load_win<true>(win, ok ? v - (v & 15u) + 16u * u : WIN_OOB);
+#if FRAG_UNALIGNED
+                c0[k] = load_win<true>(win, ok ? v + 16u * u : WIN_OOB);   // A/B only: byte-unaligned loads
+                c1[k] = make_uint4(0, 0, 0, 0);
+                continue;
+#endif
+#if FRAG_C1DPP
+                // the unit's second line is the next lane's first (process() takes it by DPP), except
+                // in lane 63 and in a fragment's last unit: only those lanes load it
+                const bool own = lane == 63u || x + 1u == st.na || x + 1u == st.nt;
+                c1[k] = load_win<true>(win, ok && sh && own ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
+#else
                 c1[k] = load_win<true>(win, ok && sh ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
+#endif
             }
         };
         auto process = [&](const Step& st, const uint4 (&c0)[U], const uint4 (&c1)[U]) {
@@ -365,9 +386,21 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 const bool ok = x < st.nt;
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x;
-                const uint32_t s = inb ? st.sb : st.sa, q = s >> 2, sbb = s & 3u;
+                const uint32_t s = FRAG_UNALIGNED ? 0u : inb ? st.sb : st.sa, q = s >> 2, sbb = s & 3u;
                 const uint32_t tl = inb ? st.tb : st.ta, at = inb ? st.atb : st.ata, o = inb ? st.ob : st.oa;
+#if FRAG_UNALIGNED
+                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, 0u, 0u, 0u, 0u};
+#elif FRAG_C1DPP
+                const bool own = lane == 63u || x + 1u == st.na || x + 1u == st.nt;
+                auto shl1 = [](uint32_t v) {            // DPP wave_shl:1 -- lane l gets lane l + 1's v
+                    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+                };
+                const uint4 nx = make_uint4(shl1(c0[k].x), shl1(c0[k].y), shl1(c0[k].z), shl1(c0[k].w));
+                const uint4 e1 = own ? c1[k] : nx;
+                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, e1.x, e1.y, e1.z, e1.w};
+#else
                 const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+#endif
                 uint32_t xw[4];
 #pragma unroll
                 for (int w = 0; w < 4; ++w)                 // bytes [s, s + 16) of the 32 loaded
