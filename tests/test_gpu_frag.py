@@ -182,3 +182,24 @@ def test_batch_shapes(n, v6):
     od, size = layout(lens, shift=4, hdr=40 if v6 else 20)
     wl, wv = check(buf, d, grp, od, size, v6=v6)
     assert (wv != 8).all() and (wl == np.array(lens)).all()
+
+
+@pytest.mark.parametrize("v6", [False, True])
+@pytest.mark.parametrize("shift", [0, 4, 8, 12])
+@pytest.mark.parametrize("payload", [8, 16, 24, 40])
+def test_unit_grid(payload, shift, v6):
+    """The gather's units follow the output's 16-byte lines: every placement of the transport
+    in its line (o = 0, 4, 8, 12 via the region shift and the 8-byte fragment offsets), fragments
+    shorter than a unit (first unit = last unit, o + len < 16), odd and 1-3-byte tails, shuffled
+    arrival -- every reassembled byte and checksum against the oracle."""
+    rng = np.random.default_rng(payload * 16 + shift + v6)
+    lens = list(range(0, 70)) + rng.integers(70, 700, 30).tolist()
+    if v6:
+        buf, off, flen, grp = synth.ipv6_fragments(lens, seed=payload + shift, proto=17, frag_payload=payload)
+    else:
+        buf, off, flen, grp = synth.ipv4_fragments(lens, seed=payload + shift, proto=6, frag_payload=payload)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=shift, hdr=40 if v6 else 20)
+    wl, wv = check(buf, d, grp, od, size, v6=v6)
+    ok = wv != 8
+    assert ok.mean() > 0.9 and (wl[ok] == np.array(lens)[ok]).all()
