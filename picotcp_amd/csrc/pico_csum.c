@@ -483,13 +483,13 @@ struct pico_csum_ctx {
     /* descriptor batches (allocated on first use): rebased descriptors (pinned host ->
      * device) and the per-frame results of a chunk */
     struct pico_csum_desc *h_desc[2], *d_desc[2];
-    uint16_t *d_net[2], *d_l4[2];
-    uint8_t *d_ver[2];
+    /* a chunk's results, packed [net: 2 cnt B | transport: 2 cnt B | verdict: cnt B], so one D2H
+     * brings them all back */
+    uint8_t *d_res[2];
     /* pinned result staging: the D2H stays asynchronous (into pageable memory HIP would block
      * the host loop until it completes, serialising the chunks); copied out when the slot is
      * next reused or at the end */
-    uint16_t *h_net[2], *h_l4[2];
-    uint8_t *h_ver[2];
+    uint8_t *h_res[2];
     uint32_t pend_first[2], pend_cnt[2];
     int desc_ready;
 };
@@ -606,15 +606,10 @@ static void ctx_desc_free(struct pico_csum_ctx *c)
     for (i = 0; i < 2; i++) {
         if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
         if (c->d_desc[i]) hipFree(c->d_desc[i]);
-        if (c->d_net[i]) hipFree(c->d_net[i]);
-        if (c->d_l4[i]) hipFree(c->d_l4[i]);
-        if (c->d_ver[i]) hipFree(c->d_ver[i]);
-        if (c->h_net[i]) hipHostFree(c->h_net[i]);
-        if (c->h_l4[i]) hipHostFree(c->h_l4[i]);
-        if (c->h_ver[i]) hipHostFree(c->h_ver[i]);
+        if (c->d_res[i]) hipFree(c->d_res[i]);
+        if (c->h_res[i]) hipHostFree(c->h_res[i]);
         c->h_desc[i] = c->d_desc[i] = NULL;
-        c->d_net[i] = c->d_l4[i] = c->h_net[i] = c->h_l4[i] = NULL;
-        c->d_ver[i] = c->h_ver[i] = NULL;
+        c->d_res[i] = c->h_res[i] = NULL;
     }
     c->desc_ready = 0;
 }
@@ -629,11 +624,8 @@ static int ctx_desc_alloc(struct pico_csum_ctx *c)
     for (i = 0; i < 2; i++) {
         if (hipHostMalloc((void **)&c->h_desc[i], nd * sizeof(struct pico_csum_desc), hipHostMallocDefault) != hipSuccess ||
             hipMalloc((void **)&c->d_desc[i], nd * sizeof(struct pico_csum_desc)) != hipSuccess ||
-            hipMalloc((void **)&c->d_net[i], nd * 2u) != hipSuccess || hipMalloc((void **)&c->d_l4[i], nd * 2u) != hipSuccess ||
-            hipMalloc((void **)&c->d_ver[i], nd) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_net[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_l4[i], nd * 2u, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_ver[i], nd, hipHostMallocDefault) != hipSuccess) {
+            hipMalloc((void **)&c->d_res[i], nd * 5u) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_res[i], nd * 5u, hipHostMallocDefault) != hipSuccess) {
             ctx_desc_free(c);
             return fail(PICO_CSUM_ENOMEM, "ctx descriptor staging (%llu descriptors)", (unsigned long long)nd);
         }
@@ -686,10 +678,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
     do {                                                                                           \
         uint32_t f0 = c->pend_first[bb], fc = c->pend_cnt[bb];                                     \
         if (fc) {                                                                                  \
-            if (out) memcpy(out + f0, c->h_l4[bb], (size_t)fc * 2u);                               \
-            if (out_net) memcpy(out_net + f0, c->h_net[bb], (size_t)fc * 2u);                      \
-            if (out_l4) memcpy(out_l4 + f0, c->h_l4[bb], (size_t)fc * 2u);                         \
-            if (verdict) memcpy(verdict + f0, c->h_ver[bb], fc);                                   \
+            const uint8_t *r_ = c->h_res[bb];                                                      \
+            if (out) memcpy(out + f0, r_ + 2u * (size_t)fc, (size_t)fc * 2u);                      \
+            if (out_net) memcpy(out_net + f0, r_, (size_t)fc * 2u);                                \
+            if (out_l4) memcpy(out_l4 + f0, r_ + 2u * (size_t)fc, (size_t)fc * 2u);                \
+            if (verdict) memcpy(verdict + f0, r_ + 4u * (size_t)fc, fc);                           \
             c->pend_cnt[bb] = 0;                                                                   \
         }                                                                                          \
     } while (0)
@@ -702,6 +695,10 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         uint64_t lo = UINT64_MAX, hi = 0, hlo = UINT64_MAX;
         uint32_t j = i, k, cnt;
         hipError_t e;
+        int vbase;
+        uint8_t *kbase, *r_ver;
+        uint64_t klen;
+        uint16_t *r_net, *r_l4;
         /* grow the chunk while the span fits the staging buffer */
         while (j < n && (uint64_t)(j - i) < maxd) {
             uint64_t o = desc[j].off, oa, end;
@@ -724,13 +721,27 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
          * done, and its results copied out */
         TRY(hipEventSynchronize(c->done[b]), "event synchronize")
         FLUSH(b);
-        for (k = 0; k < cnt; k++) {
-            const struct pico_csum_desc *s = &desc[i + k];
-            struct pico_csum_desc *t = &c->h_desc[b][k];
-            t->off = in_bounds(s, base_len) ? s->off - lo : UINT64_MAX;
-            t->len = s->len;
-            t->seed = s->seed;
+        /* The kernel sees the staged span through a base pointer lo bytes below the staging
+         * buffer, with base_len = hi: the caller's descriptors go over unchanged (one memcpy, no
+         * rebase), a descriptor outside base_len stays outside [0, hi).  (A staging buffer at a
+         * device address below lo -- never, in practice -- gets rebased descriptors.) */
+        vbase = (uintptr_t)c->d_buf[b] >= lo;
+        if (vbase) {
+            memcpy(c->h_desc[b], desc + i, (size_t)cnt * sizeof(struct pico_csum_desc));
+        } else {
+            for (k = 0; k < cnt; k++) {
+                const struct pico_csum_desc *s = &desc[i + k];
+                struct pico_csum_desc *t = &c->h_desc[b][k];
+                t->off = in_bounds(s, base_len) ? s->off - lo : UINT64_MAX;
+                t->len = s->len;
+                t->seed = s->seed;
+            }
         }
+        kbase = vbase ? (uint8_t *)c->d_buf[b] - lo : (uint8_t *)c->d_buf[b];
+        klen = vbase ? hi : hi - lo;
+        r_net = (uint16_t *)c->d_res[b];
+        r_l4 = (uint16_t *)(c->d_res[b] + 2u * (size_t)cnt);
+        r_ver = c->d_res[b] + 4u * (size_t)cnt;
         if (write && hi > hlo && hlo < whi[b ^ 1] && wlo[b ^ 1] < hi)
             TRY(hipStreamWaitEvent(c->st[b], c->done[b ^ 1], 0), "stream wait")
         if (hi > lo)
@@ -739,30 +750,27 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
                            hipMemcpyHostToDevice, c->st[b]), "H2D")
         switch (mode) {
         case HB_RAW:
-            rc = pico_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, crc_off, flags, c->d_l4[b], NULL,
-                                         c->st[b]);
+            rc = pico_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, crc_off, flags, r_l4, NULL, c->st[b]);
             break;
         case HB_IPV4:
-            rc = pico_ipv4_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, c->d_net[b], c->d_l4[b],
-                                              c->d_ver[b], c->st[b]);
+            rc = pico_ipv4_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, r_net, r_l4, r_ver, c->st[b]);
             break;
         case HB_IPV6:
-            rc = pico_ipv6_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, c->d_l4[b], c->d_ver[b],
-                                              c->st[b]);
+            rc = pico_ipv6_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, r_l4, r_ver, c->st[b]);
             break;
         default:
-            rc = pico_eth_checksum_batch_dev(c->d_buf[b], hi - lo, c->d_desc[b], cnt, flags, mac, c->d_net[b],
-                                             c->d_l4[b], c->d_ver[b], c->st[b]);
+            rc = pico_eth_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, mac, r_net, r_l4, r_ver, c->st[b]);
             break;
         }
         if (rc)
             break;
-        if (out || out_l4)
-            TRY(hipMemcpyAsync(c->h_l4[b], c->d_l4[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]), "D2H")
-        if (out_net)
-            TRY(hipMemcpyAsync(c->h_net[b], c->d_net[b], (size_t)cnt * 2u, hipMemcpyDeviceToHost, c->st[b]), "D2H")
-        if (verdict)
-            TRY(hipMemcpyAsync(c->h_ver[b], c->d_ver[b], (size_t)cnt, hipMemcpyDeviceToHost, c->st[b]), "D2H")
+        /* every requested result in one D2H (from the first requested array to the last) */
+        {
+            const size_t r0 = out_net ? 0u : (out || out_l4) ? 2u * (size_t)cnt : 4u * (size_t)cnt;
+            const size_t r1 = verdict ? 5u * (size_t)cnt : (out || out_l4) ? 4u * (size_t)cnt : 2u * (size_t)cnt;
+            if ((out || out_net || out_l4 || verdict) && r1 > r0)
+                TRY(hipMemcpyAsync(c->h_res[b] + r0, c->d_res[b] + r0, r1 - r0, hipMemcpyDeviceToHost, c->st[b]), "D2H")
+        }
         c->pend_first[b] = i;
         c->pend_cnt[b] = cnt;
         if (write && hi > hlo) {
