@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2tx_nw|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
@@ -9,6 +9,7 @@ A step = one pass of the hot path over one batch resident in HBM:
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
   c2tx: the same datagrams, fused TX (checksums computed and written in place)
   c2tx_nw: fused TX computed and returned only (F_TX without F_WRITE: the driver's header write-out)
+  c2nat: the same datagrams through the NAT batch (address / port rewrite + full checksum recompute)
   c2v6: 256K IMIX+20 B IPv6/TCP datagrams, fused IPv6 pseudo-header RX verify
   c2eth: the C2 frames through the Ethernet front end (one launch: ethertype dispatch + RX verify)
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
@@ -72,6 +73,10 @@ CONFIGS = {
                     workload="C2 compute-only TX: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams, IPv4 header "
                              "and TCP checksums computed with the crc fields read as zero and returned (F_TX "
                              "without F_WRITE: the driver writes them with its headers)"),
+    "c2nat": dict(kind="ipv4", frames=262144, nat=True,
+                  workload="C2 NAT (SURVEY 8f row 4): 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams, "
+                           "pico_ipv4_nat_outbound / _inbound's frame work per record (address + port rewritten, "
+                           "TCP and IPv4 header checksums recomputed over the whole datagram, all in place)"),
     "c3_frag": dict(kind="ipv4", frames=16384, frame_bytes=64512,
                     workload="C3 reassembled: 16K x 64512 B (PICO_IPV4_FRAG_MAX_SIZE) IPv4/TCP datagrams, fused "
                              "IPv4 header + TCP pseudo-header RX verify"),
@@ -292,7 +297,7 @@ def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
     return out
 
 
-def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float):
+def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float, nat=None):
     """The oracle's fused IPv4/IPv6/Ethernet restatement (oracle/pico_csum_oracle.c, a port of
     the reference's callers over its pico_checksum) on 1 host core over a bounded sample
     of the same datagrams (the reference's own IPv4/TCP modules need the whole stack)."""
@@ -303,6 +308,9 @@ def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float):
     ipv6 = kind == "ipv6"
     fn = {"ipv6": lambda: O.batch_ipv6(buf, sample, tx=tx), "ipv4": lambda: O.batch_ipv4(buf, sample, tx=tx),
           "eth": lambda: O.batch_eth(buf, sample, mac=MAC, tx=tx)}[kind]
+    if nat is not None:                                  # in place on a copy (idempotent: same records)
+        nbuf = buf.copy()
+        fn = lambda: O.batch_ipv4_nat(nbuf, sample, nat[:k])  # noqa: E731
     t0 = time.perf_counter()
     fn()
     reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))
@@ -311,9 +319,12 @@ def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float):
         fn()
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} datagrams of the batch ({nbytes / 2**20:.0f} MiB), oracle fused "
-                      f"{ {'ipv6': 'IPv6', 'ipv4': 'IPv4', 'eth': 'Ethernet + IPv4/IPv6'}[kind]} "
-                      f"{'TX' if tx else 'RX'} restatement, gcc -O3, 1 thread, {reps} passes"}
+            "sample": f"first {k} datagrams of the batch ({nbytes / 2**20:.0f} MiB), oracle "
+                      + ("NAT restatement (oracle_batch_ipv4_nat: rewrite + full recompute, as pico_nat.c)"
+                         if nat is not None else
+                         f"fused { {'ipv6': 'IPv6', 'ipv4': 'IPv4', 'eth': 'Ethernet + IPv4/IPv6'}[kind]} "
+                         f"{'TX' if tx else 'RX'} restatement")
+                      + f", gcc -O3, 1 thread, {reps} passes"}
 
 
 def cpu_baseline_frag(st, target_s: float, v6: bool = False):
@@ -391,7 +402,12 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
         tx = bool(cfg.get("tx"))
         now = b.cpu().numpy()
         src = hbuf if tx else now                   # TX: the pre-write bytes are the input
-        if kind == "ipv4":
+        nat_bytes = None
+        if kind == "ipv4" and cfg.get("nat"):
+            after = cfg["_nat_before"].copy()
+            want = O.batch_ipv4_nat(after, hdesc, cfg["_nat_host"])
+            nat_bytes = int((now != after).sum())
+        elif kind == "ipv4":
             want = O.batch_ipv4(src, hdesc, tx=tx)
         elif kind == "eth":
             want = O.batch_eth(src, hdesc, mac=MAC, tx=tx)
@@ -406,12 +422,16 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
         for g_, w_ in zip(got, want):
             miss |= g_ != w_
         frames, bad = int(hdesc.size), int(miss.sum())
+        if nat_bytes is not None:
+            bad += int(nat_bytes > 0)
         if tx and cfg.get("write", True):           # the in-place writes: oracle RX on them accepts
             rx = O.batch_ipv4(now, hdesc) if kind == "ipv4" else None
             if rx is not None:
                 bad += int(((want[2] == 1) & (rx[2] != 1)).sum())
         what = f"every datagram vs the oracle's fused {kind} {'TX' if tx else 'RX'} restatement" + \
             (" (+ RX of the written bytes)" if tx and kind == "ipv4" and cfg.get("write", True) else "")
+        if nat_bytes is not None:
+            what = "every datagram vs oracle_batch_ipv4_nat: checksums, verdicts and every byte of the rewritten batch"
     return {"frames": frames, "mismatches": bad, "checker": what, "seconds": round(time.perf_counter() - t0, 2)}
 
 
@@ -586,6 +606,23 @@ def main():
         frame_bytes = sets[0][2]
         # datagrams + descriptors + (2+2+1) B results (+ the two 2-byte crc fields written in place on TX)
         algo_bytes = frame_bytes + 16 * n + 5 * n + (4 * n if wr else 0)
+        if cfg.get("nat"):
+            # NAT records (8 B: addr, port, dir): outbound / inbound halves, a few without a tuple
+            g = np.random.default_rng(31 + rank)
+            nat_host = np.zeros(n, batch.NAT_DTYPE)
+            nat_host["addr"] = g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+            nat_host["port"] = g.integers(0, 1 << 16, n).astype(np.uint16)
+            nat_host["dir"] = g.choice(np.array([0, 1, 2], np.uint8), n, p=[0.02, 0.49, 0.49])
+            nat_dev = torch.from_numpy(nat_host.view(np.uint8)).to(dev)
+            cfg["_nat_host"] = nat_host                  # for the parity check and the CPU leg
+            cfg["_nat_before"] = sets[0][0].cpu().numpy()  # slot 0 as the NAT first sees it
+
+            def step(i):                                 # noqa: F811 (the NAT batch instead)
+                b, d, _, _ = sets[i % rot]
+                batch.ipv4_nat_batch(b, d, n, nat_dev, out=outs[i % rot])
+            # datagrams + descriptors + records read, (2+2+1) B results, 10 B written in place per
+            # translated datagram (address 4, port 2, two checksums 4)
+            algo_bytes = frame_bytes + 16 * n + 8 * n + 5 * n + 10 * int((nat_host["dir"] != 0).sum())
     elif cfg["kind"] == "eth":
         n = cfg["frames"]
         ln = 0
@@ -738,8 +775,8 @@ def main():
     elif rank == 0 and world == 1 and cfg["kind"] in ("ipv4", "ipv6", "eth"):
         if not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline_fused(sets[0][3], cfg["kind"], bool(cfg.get("tx")),
-                                                     a.cpu_seconds / 2)
-        if not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not ln:
+                                                     a.cpu_seconds / 2, nat=cfg.get("_nat_host"))
+        if not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not cfg.get("nat") and not ln:
             out["e2e_host_to_host"] = e2e_rate_desc(sets[0][3])
     elif rank == 0 and world == 1 and cfg["kind"] == "frag":
         if not a.no_cpu:

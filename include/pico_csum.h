@@ -107,6 +107,9 @@ struct pico_csum_desc {
                                      version that does not match it (:143-150, :162-176) */
 #define PICO_CSUM_V_ARP      64u  /* Ethernet batch: ARP frame, handed to pico_arp_receive (:186-187) */
 #define PICO_CSUM_V_IPV6    128u  /* Ethernet batch: set on every IPv6 frame (ethertype 0x86DD) */
+#define PICO_CSUM_V_UNTOUCHED 32u /* NAT batch only (same bit as V_DROP_L2): left as it is -- no
+                                     rewrite record (the host's tuple lookup failed), or a protocol
+                                     the reference's NAT returns -1 on (pico_nat.c:472-474, :537-539) */
 
 /* ---------------------------------------------------------------- layer 1 */
 
@@ -225,6 +228,37 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
  * shorter than 20 bytes are MALFORMED and untouched.  d_verdict may be NULL. */
 int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
                                 uint8_t *d_verdict, void *stream);
+
+/* NAT rewrite of a batch of IPv4 datagrams: the frame work of
+ * pico_ipv4_nat_outbound / pico_ipv4_nat_inbound (modules/pico_nat.c:424-545) once the host's
+ * tuple table has chosen the new address and port.  desc.off -> IPv4 header, desc.len = bytes
+ * available; nat[i] for datagram i (8-byte aligned device array):
+ *   dir PICO_CSUM_NAT_OUTBOUND: hdr->src = addr, transport sport = port (:509-510, :525-526)
+ *   dir PICO_CSUM_NAT_INBOUND:  hdr->dst = addr, transport dport = port (:446-447, :462-463)
+ *   dir PICO_CSUM_NAT_NONE:     left as it is (V_UNTOUCHED; the lookup failed)
+ * addr and port as they are stored in the frame (network byte order).  TCP and UDP then get
+ * their transport checksum recomputed over the whole transport with the pseudo header of the
+ * rewritten header -- UDP too, even if its crc was 0 (:461-465) -- and every translated or ICMPv4
+ * datagram its header checksum (:478-481, :543-546); ICMPv4 is not rewritten (:466-468); other
+ * protocols are V_UNTOUCHED.  All of it is written in place (V_ACCEPT).  As the reference
+ * recomputes rather than adjusts, a wrong stored transport checksum comes out right.
+ * A fragment (MF or an offset) is V_FRAG and untouched (it reaches reassembly, not NAT:
+ * pico_ipv4.c:446-455); infeasible lengths, or a TCP / UDP transport shorter than its header
+ * with a record, are V_MALFORMED and untouched.  d_out_net / d_out_transport: the stored
+ * values (0 where none); any output pointer may be NULL.  One pass over each datagram: the
+ * rewritten words enter the sums as deltas of the old ones (RFC 1624, on full sums). */
+#define PICO_CSUM_NAT_NONE     0u
+#define PICO_CSUM_NAT_OUTBOUND 1u
+#define PICO_CSUM_NAT_INBOUND  2u
+struct pico_csum_nat {
+    uint32_t addr;      /* new source (outbound) / destination (inbound) address, as stored */
+    uint16_t port;      /* new source / destination port, as stored */
+    uint8_t dir;        /* PICO_CSUM_NAT_* */
+    uint8_t reserved;
+};
+int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                            const struct pico_csum_nat *d_nat, uint16_t *d_out_net, uint16_t *d_out_transport,
+                            uint8_t *d_verdict, void *stream);
 
 /* IPv4 fragment reassembly fused with the transport check of the reassembled datagram
  * (pico_ipv4_process_frag / pico_fragments_check_complete /

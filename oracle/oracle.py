@@ -77,6 +77,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_ipv6_walk_frag.argtypes = [_vp, _u32, _vp, _vp, _vp]
         L.oracle_batch_ipv4_forward.restype = None
         L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
+        L.oracle_batch_ipv4_nat.restype = None
+        L.oracle_batch_ipv4_nat.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
         L.oracle_uniform_mt.argtypes = [_vp, _vp, _u64, _u32, _u32, _vp, _u32]
         _olib = L
@@ -209,6 +211,22 @@ def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:
     v = np.zeros(desc.shape[0], np.uint8)
     lib().oracle_batch_ipv4_forward(_p(base), _p(desc), desc.shape[0], _p(v))
     return v
+
+
+NAT_DTYPE = np.dtype([("addr", "<u4"), ("port", "<u2"), ("dir", "u1"), ("reserved", "u1")])
+NAT_NONE, NAT_OUTBOUND, NAT_INBOUND = 0, 1, 2
+
+
+def batch_ipv4_nat(base: np.ndarray, desc: np.ndarray, nat: np.ndarray):
+    """pico_ipv4_nat_outbound / _inbound's frame work (oracle_batch_ipv4_nat), in place on
+    `base` (a writable uint8 array); returns (out_net, out_l4, verdict)."""
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    nat = np.ascontiguousarray(nat, dtype=NAT_DTYPE)
+    n = desc.shape[0]
+    assert nat.shape[0] == n
+    on, ol, v = np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8)
+    lib().oracle_batch_ipv4_nat(_p(base), _p(desc), n, _p(nat), _p(on), _p(ol), _p(v))
+    return on, ol, v
 
 
 # ---------------------------------------------------------------- reference

@@ -823,6 +823,77 @@ void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, ui
     }
 }
 
+/* modules/pico_nat.c:424-545, pico_ipv4_nat_inbound / pico_ipv4_nat_outbound after the tuple
+ * lookup (the host's table decides rw[i]; dir 0 = no tuple: return -1, nothing written).  The
+ * frame as pico_ipv4_process_in leaves it (:392-405): net_len = 20 + options, transport_len =
+ * (uint16)(tot_len - net_len), transport_hdr = net_hdr + net_len; f->sock NULL, so the pseudo
+ * header comes from the (rewritten) IP header (pico_tcp.c:428-443, pico_udp.c:42-57).  In place:
+ *   TCP / UDP: addr into src (outbound, :509 / :525) or dst (inbound, :446 / :462), port into
+ *     sport / dport (:510 / :526, :447 / :463); crc = 0; crc = short_be(pico_tcp_checksum_ipv4 /
+ *     pico_udp_checksum_ipv4) (:448-449, :464-465, :515-516, :531-532) -- UDP included, whatever
+ *     its crc was; then the header checksum (:480-481, :545-546).
+ *   ICMPv4: no rewrite (:466-468, :533-535), the header checksum only.
+ *   Other protocols: return -1 (:472-474, :537-539): untouched.
+ * Datagrams the batch leaves alone as the stack never NATs them: a fragment (handed to
+ * reassembly first, pico_ipv4.c:446-455) -> FRAG; infeasible lengths (the TX-path bounds of
+ * oracle_batch_ipv4) or a TCP / UDP transport shorter than 20 / 8 bytes with a record (the
+ * reference would write past it) -> MALFORMED.  out_net / out_l4: the values stored (else 0). */
+void oracle_batch_ipv4_nat(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const struct oracle_nat *rw,
+                           uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict)
+{
+    uint32_t i;
+    for (i = 0; i < n; i++) {
+        uint8_t *h = base + d[i].off, *t;
+        uint32_t avail = d[i].len, net_len, s;
+        uint16_t tot, transport_len, frag, cs;
+        uint8_t proto;
+
+        out_net[i] = 0; out_l4[i] = 0; verdict[i] = PICO_CSUM_V_MALFORMED;
+        if (avail < 20)
+            continue;
+        net_len = 20u + ((h[0] & 0x0Fu) > 5u ? 4u * ((h[0] & 0x0Fu) - 5u) : 0u);
+        tot = (uint16_t)((h[2] << 8) | h[3]);
+        transport_len = (uint16_t)(tot - net_len);
+        frag = (uint16_t)((h[6] << 8) | h[7]);
+        proto = h[9];
+        if (net_len > avail || net_len + (uint32_t)transport_len > avail)
+            continue;
+        if (frag & 0x3FFFu) {
+            verdict[i] = PICO_CSUM_V_FRAG;
+            continue;
+        }
+        t = h + net_len;
+        if (rw[i].dir != 1 && rw[i].dir != 2) {
+            verdict[i] = PICO_CSUM_V_UNTOUCHED;
+            continue;
+        }
+        if (proto == 6 || proto == 17) {
+            const uint32_t crc_at = proto == 6 ? 16u : 6u;
+            if (transport_len < (proto == 6 ? 20u : 8u))
+                continue;                                                /* MALFORMED */
+            memcpy(h + (rw[i].dir == 1 ? 12 : 16), &rw[i].addr, 4);
+            memcpy(t + (rw[i].dir == 1 ? 0 : 2), &rw[i].port, 2);
+            t[crc_at] = 0;
+            t[crc_at + 1] = 0;
+            s = oracle_ipv4_pseudo_sum(h + 12, h + 16, proto, transport_len);
+            cs = oracle_checksum_finalize(oracle_checksum_adder(s, t, transport_len));
+            t[crc_at] = (uint8_t)(cs >> 8);                              /* short_be */
+            t[crc_at + 1] = (uint8_t)cs;
+            out_l4[i] = cs;
+        } else if (proto != 1) {
+            verdict[i] = PICO_CSUM_V_UNTOUCHED;
+            continue;
+        }
+        h[10] = 0;
+        h[11] = 0;
+        cs = oracle_checksum(h, net_len);
+        h[10] = (uint8_t)(cs >> 8);
+        h[11] = (uint8_t)cs;
+        out_net[i] = cs;
+        verdict[i] = PICO_CSUM_V_ACCEPT;
+    }
+}
+
 /* ---- multi-threaded CPU baseline driver (bench.py cpu_baseline leg) ---- */
 
 struct mt_job {

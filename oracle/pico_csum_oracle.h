@@ -22,6 +22,15 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_DROP_L2  32u
 #define PICO_CSUM_V_ARP      64u
 #define PICO_CSUM_V_IPV6    128u
+#define PICO_CSUM_V_UNTOUCHED 32u  /* NAT batch */
+
+/* Same 8-byte layout as include/pico_csum.h struct pico_csum_nat. */
+struct oracle_nat {
+    uint32_t addr;
+    uint16_t port;
+    uint8_t dir;        /* 0 none, 1 outbound (src, sport), 2 inbound (dst, dport) */
+    uint8_t reserved;
+};
 
 #define ORACLE_IPV4_TX 1u
 /* IPv6 RX: check TCP / UDP by the transport's own protocol (PICO_CSUM_F_NXTHDR_DISPATCH);
@@ -61,6 +70,8 @@ void oracle_ipv6_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
                             uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t flags);
 void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict);
+void oracle_batch_ipv4_nat(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const struct oracle_nat *rw,
+                           uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,
                          uint32_t n, uint16_t *out, uint32_t nthreads);
 #endif

@@ -35,7 +35,12 @@
  *   on it for TCP / UDP, else -1), 0 when none was reassembled.
  * rr_eth_init(mac) / rr_eth_rx(frame, avail): pico_ethernet_receive on an Ethernet device with
  *   that MAC; returns 1 queued for IPv4, 2 queued for IPv6, 3 handed to ARP, 0 discarded.
- * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py, make_ref_eth.py) only pass datagrams whose reference reads stay inside
+ * rr_nat(dir, datagram, avail, nat_addr): pico_ipv4_nat_outbound (dir 1) or pico_ipv4_nat_inbound
+ *   (dir 2) (modules/pico_nat.c:424-545) on the datagram as pico_ipv4_process_in leaves it
+ *   (net_len, transport_hdr, transport_len :392-405), NAT enabled on the link nat_addr (from the
+ *   first call on; tuples persist: an inbound reply finds the outbound's tuple); the frame's
+ *   bytes after the call are copied back.  Returns the function's result (0 translated).
+ * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py, make_ref_eth.py, make_ref_nat.py) only pass datagrams whose reference reads stay inside
  * avail and whose walk terminates (the oracle restatement decides which; the others are
  * restatement-only and documented so).
  */
@@ -52,6 +57,7 @@
 #include "pico_icmp4.h"
 #include "pico_queue.h"
 #include "pico_dev_null.h"
+#include "pico_nat.h"
 
 int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
@@ -73,6 +79,7 @@ int rr_eth_rx(const uint8_t *d, uint32_t avail);
 int rr_init(void);
 int rr_ipv4_link(uint32_t addr);
 int rr_ipv4_rx(const uint8_t *d, uint32_t avail);
+int rr_nat(int dir, uint8_t *d, uint32_t avail, uint32_t nat_addr);
 int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
 int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
              uint32_t cap, uint32_t *out_len, uint32_t *module, int *check);
@@ -350,5 +357,37 @@ int rr_eth_rx(const uint8_t *d, uint32_t avail)
     }
     if (g_arp)
         r = 3;
+    return r;
+}
+
+int rr_nat(int dir, uint8_t *d, uint32_t avail, uint32_t nat_addr)
+{
+    struct pico_frame *f;
+    struct pico_ip4 a;
+    struct pico_ipv4_link *link;
+    uint32_t net_len;
+    int r;
+    if (!g_dev || avail < 20 || (dir != 1 && dir != 2))
+        return -2;
+    a.addr = nat_addr;
+    link = pico_ipv4_link_get(&a);
+    if (!link && rr_ipv4_link(nat_addr) == 0)
+        link = pico_ipv4_link_get(&a);
+    if (!link)
+        return -2;
+    /* enabled once per process (each pico_ipv4_nat_enable adds a cleanup timer); callers load a
+     * private copy of this library for NAT, so no other fixture sees the link */
+    if (!pico_ipv4_nat_is_enabled(&a) && pico_ipv4_nat_enable(link) != 0)
+        return -2;
+    f = mk(d, avail);
+    if (!f)
+        return -2;
+    net_len = 20u + ((d[0] & 0x0Fu) > 5u ? 4u * ((d[0] & 0x0Fu) - 5u) : 0u);
+    f->net_len = (uint16_t)net_len;
+    f->transport_hdr = f->net_hdr + net_len;
+    f->transport_len = (uint16_t)(((uint32_t)d[2] << 8 | d[3]) - net_len);
+    r = dir == 1 ? pico_ipv4_nat_outbound(f, &a) : pico_ipv4_nat_inbound(f, &a);
+    memcpy(d, f->buffer, avail);
+    pico_frame_discard(f);
     return r;
 }

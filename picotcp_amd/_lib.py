@@ -29,6 +29,7 @@ EXPORTED = (
     "pico_ipv6_checksum_batch_dev",
     "pico_eth_checksum_batch_dev",
     "pico_ipv4_forward_batch_dev",
+    "pico_ipv4_nat_batch_dev",
     "pico_ipv4_reassemble_batch_dev",
     "pico_ipv6_reassemble_batch_dev",
     "pico_csum_ctx_create",
@@ -52,6 +53,7 @@ V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
 V_FRAG = 16                # RX / TX batches (V_EXPIRED: the forwarding batch)
 ABI_VERSION = 2
 V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
+V_UNTOUCHED = 32            # NAT batch (same bit as V_DROP_L2)
 EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12
 
 
@@ -94,6 +96,7 @@ def load() -> ctypes.CDLL:
     sig("pico_ipv6_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp)
     sig("pico_eth_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp)
+    sig("pico_ipv4_nat_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, vp)
     sig("pico_ipv6_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, u32, vp)
     sig("pico_csum_ctx_create", vp, ctypes.c_int, u64)

@@ -26,9 +26,12 @@ import torch
 
 from . import _lib
 from ._lib import (F_NXTHDR_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_FRAG,  # noqa: F401
-                   V_IPV6, V_L4_BAD, V_MALFORMED, V_NET_BAD)
+                   V_IPV6, V_L4_BAD, V_MALFORMED, V_NET_BAD, V_UNTOUCHED)
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+# struct pico_csum_nat (include/pico_csum.h): the NAT batch's per-datagram record
+NAT_DTYPE = np.dtype([("addr", "<u4"), ("port", "<u2"), ("dir", "u1"), ("reserved", "u1")])
+NAT_NONE, NAT_OUTBOUND, NAT_INBOUND = 0, 1, 2
 assert DESC_DTYPE.itemsize == 16
 
 
@@ -213,6 +216,32 @@ def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: 
                lib.pico_ipv4_forward_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, _ptr(verdict),
                                                _stream_handle(stream)))
     return verdict
+
+
+def ipv4_nat_batch(base: torch.Tensor, desc: torch.Tensor, n: int, nat: torch.Tensor, stream=None, out=None):
+    """NAT rewrite (pico_ipv4_nat_outbound / _inbound's frame work, pico_nat.c:424-545) in place on
+    n IPv4 datagrams: nat = 8-byte records {addr u32, port u16, dir u8, 0} as uint8 / int64 tensor
+    (NAT_DTYPE layout).  Returns (out_net int16[n], out_transport int16[n], verdict uint8[n]):
+    V_ACCEPT translated, V_UNTOUCHED, V_FRAG, V_MALFORMED."""
+    _require_device(base, "base")
+    _require_device(desc, "desc")
+    _require_device(nat, "nat")
+    if desc.numel() < 16 * n:
+        raise ValueError("descriptor tensor shorter than n entries")
+    if nat.numel() * nat.element_size() < 8 * n or not nat.is_contiguous():
+        raise ValueError("nat must be a contiguous tensor of n 8-byte records")
+    dev = base.device
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+               torch.empty(n, dtype=torch.uint8, device=dev))
+    out_net, out_l4, verdict = out
+    for t, nm, sz in ((out_net, "out_net", 2), (out_l4, "out_transport", 2), (verdict, "verdict", 1)):
+        _check_out(t, n, nm, dev, sz)
+    lib = _lib.load()
+    _lib.check("pico_ipv4_nat_batch_dev",
+               lib.pico_ipv4_nat_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, _ptr(nat), _ptr(out_net),
+                                           _ptr(out_l4), _ptr(verdict), _stream_handle(stream)))
+    return out_net, out_l4, verdict
 
 
 def _require_u8(t: torch.Tensor, name: str) -> None:

@@ -30,6 +30,9 @@ int pico_csum_launch_raw(const void *base, uint64_t base_len, uint64_t stride, u
 int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t *out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
                                 uint32_t win, void *stream);
+/* kernel-only flags (pico_csum_dev.h F_MACF / F_NAT), set by this layer */
+#define KF_MACF 0x10000u
+#define KF_NAT 0x20000u
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
@@ -348,6 +351,29 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                          "pico_ipv4_checksum_batch_dev");
 }
 
+int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                            const struct pico_csum_nat *d_nat, uint16_t *d_out_net, uint16_t *d_out_transport,
+                            uint8_t *d_verdict, void *stream)
+{
+    uint32_t fpw = 0;
+    int rc;
+    if (n == 0)
+        return 0;
+    if (!d_base || !d_desc || !d_nat)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (((uintptr_t)d_desc & 15u) != 0 || ((uintptr_t)d_nat & 7u) != 0)
+        return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte, NAT records 8-byte aligned");
+    if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
+        return rc;
+    /* the IPv4 kernel in TX + in-place mode with the NAT stage; the records' address rides in the
+     * launcher's 64-bit MAC argument (used as a MAC by the Ethernet mode only) */
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1,
+                                                 PICO_CSUM_F_TX | PICO_CSUM_F_WRITE | KF_NAT | ablate_flags(), NULL,
+                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw,
+                                                 (uint64_t)(uintptr_t)d_nat, stream),
+                         "pico_ipv4_nat_batch_dev");
+}
+
 int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc,
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream)
@@ -372,9 +398,6 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                                  NULL, NULL, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv6_checksum_batch_dev");
 }
-
-/* kernel flag: filter destination MACs (Ethernet mode; the public flags reject it) */
-#define KF_MACF 0x10000u
 
 int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
                                 uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,

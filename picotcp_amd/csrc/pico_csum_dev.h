@@ -130,6 +130,15 @@ __device__ __forceinline__ void store_crc(uint8_t* p, uint32_t ret) {
     }
 }
 
+// The low n bytes of v, little-endian, at p (any alignment): 16-bit stores when p is even.
+__device__ __forceinline__ void store_le(uint8_t* p, uint32_t v, int n) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
+        for (int i = 0; i < n; i += 2) *reinterpret_cast<uint16_t*>(p + i) = (uint16_t)(v >> (8 * i));
+    } else {
+        for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
+    }
+}
+
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* a0, uint32_t k) {
     return *reinterpret_cast<const uint4*>(a0 + ((uint64_t)k << 4));
 }
@@ -231,6 +240,10 @@ constexpr uint32_t V_ACCEPT = 1u, V_NET_BAD = 2u, V_L4_BAD = 4u, V_MALFORMED = 8
 constexpr uint32_t V_FRAG = 16u;        // RX / TX batches (V_EXPIRED: the forwarding batch only)
 constexpr uint32_t V_DROP_L2 = 32u, V_ARP = 64u, V_IPV6 = 128u;   // Ethernet mode (include/pico_csum.h)
 constexpr uint32_t F_MACF = 0x10000u;   // kernel flag (set by the host layer): filter destination MACs
+constexpr uint32_t F_NAT = 0x20000u;    // kernel flag (pico_ipv4_nat_batch_dev): IPv4 mode, NAT rewrite
+constexpr uint32_t V_UNTOUCHED = 32u;   // NAT batch: left as it is (include/pico_csum.h)
+// NAT state of a frame (IPv4 mode, F_NAT), in the l2v byte of the phase-4 state
+constexpr uint32_t NS_XLATE = 1u, NS_HDR = 2u, NS_SKIP = 4u, NS_BAD = 8u;
 constexpr uint32_t F_NXD = 0x4u;        // PICO_CSUM_F_NXTHDR_DISPATCH (IPv6 RX)
 // phase-1 outcomes applied after the IPv4 header check (sorted kernel)
 constexpr uint32_t PV_DROP = 1u, PV_FRAG = 2u;

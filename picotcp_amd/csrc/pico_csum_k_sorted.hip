@@ -232,7 +232,7 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
                             l4 = finalize(pseudo + tsum);
                             if (l4 != 0) verdict |= V_L4_BAD;
                         }
-                    } else if (proto == 6u) {
+                    } else if (proto != 1u) {         // TCP (and, NAT, UDP): pseudo header
                         l4 = finalize(pseudo + tsum - acc_x);
                     } else {
                         l4 = finalize(tsum - acc_x);
@@ -240,7 +240,26 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
                 }
                 if (verdict == 0) verdict = V_ACCEPT;
             }
-            if (tx && (p.flags & 1u) && !ABLATE(p, 0x400u)) {
+            const bool nat = MODE == 1 && (p.flags & F_NAT);
+            if (nat) {
+                // pico_ipv4_nat_outbound / _inbound's stores (pico_nat.c:443-449, :461-465,
+                // :478-481, :511-517, :527-532, :543-546): address, port, transport crc, header crc
+                const uint32_t ns = l2v & 15u, ndir = l2v >> 4;
+                if (parsed && post != PV_FRAG)
+                    verdict = ns == NS_SKIP ? V_UNTOUCHED : ns == NS_BAD ? V_MALFORMED : V_ACCEPT;
+                if (verdict != V_ACCEPT) net = 0;
+                if (ns != NS_XLATE || verdict != V_ACCEPT) l4 = 0;
+                if (verdict == V_ACCEPT && (p.flags & 1u)) {
+                    store_crc(fp + 10, net);
+                    if (ns == NS_XLATE) {
+                        const uint8_t* rec = reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo);
+                        const uint2 rw = *reinterpret_cast<const uint2*>(rec + 8ull * idx);
+                        store_crc(fp + hl + (proto == 6u ? 16u : 6u), l4);
+                        store_le(fp + (ndir == 1u ? 12u : 16u), rw.x, 4);
+                        store_le(fp + hl + (ndir == 1u ? 0u : 2u), rw.y, 2);
+                    }
+                }
+            } else if (tx && (p.flags & 1u) && !ABLATE(p, 0x400u)) {
                 if (verdict == V_ACCEPT) {
                     store_crc(fp + 10, net);
                     if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
@@ -452,12 +471,51 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                             else { l4_needed = true; xpos = r + hl + 6u; ext = max(span, hl + 8u); }
                         }
                     } else {
+                        // NAT (F_NAT): TCP and UDP are recomputed in full (pico_nat.c:443-449,
+                        // :461-465, :511-517, :527-532), ICMP only gets its header checksum
+                        const bool nat = IPV4 && (p.flags & F_NAT);
                         if (proto == 6u) {
                             if (tl < 20u) verdict |= V_MALFORMED;
                             else { l4_needed = true; xpos = r + hl + 16u; }
-                        } else if (proto == 1u) {
+                        } else if (proto == 17u && nat) {
+                            if (tl < 8u) verdict |= V_MALFORMED;
+                            else { l4_needed = true; xpos = r + hl + 6u; }
+                        } else if (proto == 1u && !nat) {
                             if (tl < 8u) verdict |= V_MALFORMED;
                             else { l4_needed = true; xpos = r + hl + 2u; }
+                        }
+                    }
+                }
+            }
+            if constexpr (IPV4) {
+                // pico_ipv4_nat_outbound / _inbound (modules/pico_nat.c:424-545) after the host's
+                // tuple lookup: record {addr, port, dir} per frame (dir 1 outbound: src + sport,
+                // 2 inbound: dst + dport, 0 none).  The rewritten words enter the sums as deltas
+                // (header, pseudo header, region), so the one pass over the old bytes gives the
+                // checksums of the new ones (RFC 1624's incremental update, applied to full sums).
+                if (p.flags & F_NAT) {
+                    const uint8_t* nat = reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo);
+                    uint2 rw = make_uint2(0u, 0u);
+                    if (lane < cnt) rw = *reinterpret_cast<const uint2*>(nat + 8ull * (f0 + lane));
+                    const uint32_t dir = (rw.y >> 16) & 0xFFu;
+                    l2v = NS_SKIP;
+                    if (parsed && post == 0u && (dir == 1u || dir == 2u)) {
+                        if ((proto == 6u || proto == 17u) && !(l4_needed && staged)) {
+                            l2v = NS_BAD;                            // transport too short (or > 2 GiB batch)
+                        } else if (proto == 6u || proto == 17u) {
+                            uint32_t H[5];
+                            window_words<5, false>(hw, r, H);
+                            const uint32_t old = dir == 1u ? H[3] : H[4];
+                            const uint32_t da = (rw.x & 0xFFFFu) + (rw.x >> 16) - (old & 0xFFFFu) - (old >> 16);
+                            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
+                            const uint32_t sw = (lane & (HW - 1)) << 4, pb = r + hl + (dir == 1u ? 0u : 2u);
+                            const uint32_t op = (uint32_t)row[pb ^ sw] | ((uint32_t)row[(pb + 1u) ^ sw] << 8);
+                            hdr20 += da;
+                            pseudo += da;
+                            p_all = da + (rw.y & 0xFFFFu) - op;     // the region's share of both words
+                            l2v = NS_XLATE | (dir << 4);
+                        } else if (proto == 1u) {
+                            l2v = NS_HDR;
                         }
                     }
                 }
