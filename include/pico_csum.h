@@ -244,7 +244,8 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
  * recomputes rather than adjusts, a wrong stored transport checksum comes out right.
  * A fragment (MF or an offset) is V_FRAG and untouched (it reaches reassembly, not NAT:
  * pico_ipv4.c:446-455); infeasible lengths, or a TCP / UDP transport shorter than its header
- * with a record, are V_MALFORMED and untouched.  d_out_net / d_out_transport: the stored
+ * with a record, are V_MALFORMED and untouched (so is, in a batch over 2 GiB, a datagram more
+ * than 1 GiB past the first datagram of its 64-datagram wave).  d_out_net / d_out_transport: the stored
  * values (0 where none); any output pointer may be NULL.  One pass over each datagram: the
  * rewritten words enter the sums as deltas of the old ones (RFC 1624, on full sums). */
 #define PICO_CSUM_NAT_NONE     0u
