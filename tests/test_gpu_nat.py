@@ -60,7 +60,7 @@ def test_imix_burst_vs_oracle(seed):
     nat = np.zeros(n, O.NAT_DTYPE)
     nat["addr"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     nat["port"] = rng.integers(0, 1 << 16, n).astype(np.uint16)
-    nat["dir"] = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.1, 0.5, 0.4])
+    nat["dir"] = rng.choice(np.array([0, 1, 2, 3, 255], np.uint8), n, p=[0.08, 0.5, 0.4, 0.01, 0.01])
     desc = batch.make_desc(net.astype(np.uint64), avail)
     got, on, ol, v = run(buf, desc, nat)
     want = buf.copy()
