@@ -27,10 +27,10 @@
 //      then gathers fragments 0 mod 4 (one wave per datagram: the same, in order);
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
 //      16-byte units on the output's 16-byte lines, 3 x 64 units per wave per step (two 1480-byte
-//      payloads): two aligned
-//      16-byte loads per unit through one buffer window over both payloads (out-of-range slots
-//      read zeros, no branches) and a shift by the unit's payload alignment (dword select +
-//      alignbyte); v_dot2 sums on the fly (every unit is a whole number of checksum words); a
+//      payloads): one byte-unaligned 16-byte load per unit through one buffer window over both
+//      payloads (out-of-range slots read zeros, no branches; FRAG_UNALIGNED 0 builds load two
+//      aligned lines and shift, the second taken from the next lane by DPP); v_dot2 sums on the
+//      fly (every unit is a whole number of checksum words); a
 //      workgroup reduction at the end.  Software-pipelined over two register sets: the next
 //      step's loads are issued before this step's stores, and the stores are a fixed sequence
 //      per unit (one 16-byte store if the unit is whole, else its whole dwords as a b64 and / or a
@@ -44,7 +44,11 @@
 //      149.0 / 157.9 at four (ab_frag_wpd.txt).  Stores keep the default cache policy: nt 194 /
 //      201 us, sc1 244 / 255 us (ab_frag_saux.txt).  Units on the output's 16-byte lines (every
 //      interior unit one aligned b128 store, 5 store instructions per slot instead of 8): 130.6 /
-//      140.2 us vs 145.5 / 154.7 (profiles/r03s2/ab_frag_grid.txt).
+//      140.2 us vs 145.5 / 154.7 (profiles/r03s2/ab_frag_grid.txt); the second line by DPP 128.5 /
+//      138.3 us; one unaligned load 124.0 / 133.8 us (ab_frag_una.txt).  Tried, not kept (r03s2):
+//      larger-occupancy LDS tables, three register sets, the completeness check or the header
+//      copy after the gather, a lean whole-unit slot path with the edge units in 4 lanes, the
+//      gather in tree order.
 // The bytes of an output region are unspecified when its datagram is not reassembled.
 #include "pico_csum_dev.h"
 
