@@ -62,10 +62,35 @@ struct SortedWaveLds {
 // A wave's LDS.  Fused modes: the phase-1 head-window staging (64 frames x HW chunks,
 // chunk slots XOR-swizzled) shares the space with the state it is parsed into -- 8 KiB a
 // wave, 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
+// Stream-order waves for dense MODE 1 batches (stream_batch).  Product shape, measured
+// (profiles/r03s3/README.md): 8 chunks per lane per step (8 KiB; StreamLds 10 KiB a wave, 4
+// workgroups of 4 waves per CU), two steps in flight, non-temporal loads.  A/B builds: -D...=0.
+#ifndef PICO_STREAM
+#define PICO_STREAM 1
+#endif
+#ifndef PICO_STREAM_CPL
+#define PICO_STREAM_CPL 8
+#endif
+#ifndef PICO_STREAM_NT
+#define PICO_STREAM_NT 1
+#endif
+#ifndef PICO_STREAM_DB
+#define PICO_STREAM_DB 1
+#endif
+constexpr uint32_t SCPL = PICO_STREAM_CPL;   // chunks per lane per step
+constexpr uint32_t SQ = 64u * SCPL;          // chunks per step
+struct StreamLds {
+    uint4 raw[SQ];           // the step's bytes, chunk slots swizzled (sslot)
+    uint32_t pxc[SQ];        // exclusive prefix sum before each chunk, chunk order
+};
+
 template <bool STAGE>
 union SortedWaveSmem {
     SortedWaveLds s;
     uint4 stage[64 * HW];
+#if PICO_STREAM
+    StreamLds st;
+#endif
 };
 template <>
 union SortedWaveSmem<false> {
@@ -157,12 +182,8 @@ __device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L
 // pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in the out_net / out_l4 / verdict fields of FlatArgs.
 // Phase 4: lane `lane` finalizes its frame (output index idx) from the LDS state.
 template <int MODE>
-__device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t idx,
-                                              bool tx) {
-    asm volatile("" ::: "memory");
-    const uint32_t acc_all = L.acc_all[lane], acc_x = L.acc_x[lane], acc_opt = L.acc_opt[lane];
-    const uint4 info = L.info[lane], fin = L.fin[lane];
-    const uint32_t xpos = L.xo[lane].x;
+__device__ __forceinline__ void finish_frame(const FlatArgs& p, uint64_t idx, bool tx, uint32_t acc_all,
+                                             uint32_t acc_x, uint32_t acc_opt, uint4 info, uint4 fin, uint32_t xpos) {
     const uint32_t r = info.w & 15u;
     uint8_t* fp = p.base + (((((uint64_t)info.y) << 32) | info.x) + r);
     uint32_t verdict = fin.x & 8u;               // V_MALFORMED from phase 1, or 0
@@ -273,6 +294,14 @@ __device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& 
         if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
         if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
     }
+}
+
+template <int MODE>
+__device__ __forceinline__ void sorted_finish(const FlatArgs& p, SortedWaveLds& L, uint32_t lane, uint64_t idx,
+                                              bool tx) {
+    asm volatile("" ::: "memory");
+    finish_frame<MODE>(p, idx, tx, L.acc_all[lane], L.acc_x[lane], L.acc_opt[lane], L.info[lane], L.fin[lane],
+                       L.xo[lane].x);
 }
 
 // The NW little-endian dwords at byte position pos of a frame's head window (pos < 16, or
@@ -739,6 +768,281 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     __builtin_amdgcn_wave_barrier();
 }
 
+#if PICO_STREAM
+// ---------------------------------------------------------------- stream-order wave (MODE 1)
+//
+// A wave whose 64 datagrams lie densely in one span of the batch (a TAP / ring burst: back to
+// back behind their link headers) reads that span in address order -- 64 lanes x SCPL
+// coalesced 16-byte loads a step, every line fetched once -- instead of sorting the frames
+// into size-class rounds.  Each step is staged in LDS and turned into exclusive prefix sums
+// per dword (in the memory-even little-endian word domain, plain 32-bit sums: a region's sum
+// is the difference of two prefixes, exact below 128 KiB).  Lane j meanwhile collects frame
+// j's head window from the stage, parses it as soon as its first two chunks are in, and
+// reads the prefixes at its region boundaries (options start, transport start / end, the
+// isolated crc field) when they pass.  Frames of odd start byte take the byte-swapped fold.
+
+// Chunk q's slot: lane-major readers (lane L, chunks SCPL L + c) and column-major writers
+// (lane l, chunks 64 c + l) both land on distinct banks within their ds_read/write_b128 groups.
+__device__ __forceinline__ uint32_t sslot(uint32_t q) { return q ^ ((q >> 4) & (SCPL - 1u)); }
+
+// The prefix at byte position b of the span (the sum of the span's bytes before b), taken when
+// b's last byte before it lies in the step starting at byte byte0.
+__device__ __forceinline__ void stream_point(const StreamLds& S, uint32_t b, uint32_t byte0, uint32_t& P) {
+    const uint32_t t = b - 1u - byte0;
+    if (b != 0u && t < 16u * SQ) {
+        const uint32_t q = t >> 4, m = (t & 15u) + 1u;       // bytes of chunk q before b: 1..16
+        const uint4 u = S.raw[sslot(q)];
+        uint32_t a = S.pxc[q];
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (uint32_t d = 0; d < 4; ++d) {
+            const uint32_t nb = m > 4u * d ? min(m - 4u * d, 4u) : 0u;
+            a = dot2_add(w[d] & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * nb)) - 1u), a);
+        }
+        P = a;
+    }
+}
+
+template <int OP, int CTRL, int RM>
+__device__ __forceinline__ int scan_step(int x) {
+    const int o = __builtin_amdgcn_update_dpp(OP == 0 ? 0 : x, x, CTRL, RM, 0xF, false);
+    return OP == 0 ? x + o : OP == 1 ? min(x, o) : max(x, o);
+}
+template <int OP>
+__device__ __forceinline__ int wave_incl(int v) {
+    v = scan_step<OP, 0x111, 0xF>(v);
+    v = scan_step<OP, 0x112, 0xF>(v);
+    v = scan_step<OP, 0x114, 0xF>(v);
+    v = scan_step<OP, 0x118, 0xF>(v);
+    v = scan_step<OP, 0x142, 0xA>(v);
+    v = scan_step<OP, 0x143, 0xC>(v);
+    return v;
+}
+
+// The two bytes at head-window position pos (pos + 1 < 16 * n), low byte first.
+template <uint32_t N>
+__device__ __forceinline__ uint32_t hw_pair(const uint4 (&hw)[HW], uint32_t pos) {
+    const uint32_t q = pos >> 2;
+    uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4 * N; ++k) {
+        const uint4 c = hw[k >> 2];
+        const uint32_t d = (k & 3u) == 0 ? c.x : (k & 3u) == 1 ? c.y : (k & 3u) == 2 ? c.z : c.w;
+        d0 = q == k ? d : d0;
+        d1 = q + 1u == k ? d : d1;
+    }
+    return __builtin_amdgcn_alignbyte(d1, d0, pos & 3u) & 0xFFFFu;
+}
+
+// An even-domain sum as the frame's own word pairing sees it: unchanged for an even start,
+// folded (zero stays zero, anything else stays in [1, 0xFFFF]) and byte-swapped for an odd one.
+__device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
+    if (!odd) return v;
+    v = (v & 0xFFFFu) + (v >> 16);
+    v = (v & 0xFFFFu) + (v >> 16);
+    return ((v >> 8) | (v << 8)) & 0xFFFFu;
+}
+
+// Returns false (nothing written) when the wave's frames are not one dense span; the caller
+// then runs the sorted-rounds batch.
+__device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane,
+                                             uint64_t f0) {
+    if (p.flags & (F_NAT | F_MACF)) return false;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const bool tx = (p.flags & 2u) != 0;
+    uint4 dcur = make_uint4(0, 0, 0, 0);
+    if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+    uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
+    uint32_t len = lane < cnt ? dcur.z : 0u;
+    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
+    if (oob || lane >= cnt) { len = 0; off = 0; }
+    const bool valid = len >= 20u;                            // shorter: MALFORMED, nothing to sum
+    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off;
+    // the span, relative to the first valid frame's line (a frame more than 512 MiB away:
+    // not one span)
+    const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
+    if (vb == 0) return false;
+    const int fv = __builtin_ffsll((long long)vb) - 1;
+    const uint64_t la = addr & ~(uint64_t)15;
+    const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+    const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
+    if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
+    const int mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0), 63);
+    const int mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : 0), 63);
+    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(valid ? (int)len : 0), 63);
+    const uint64_t lo = anchor + (int64_t)mn;
+    const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
+    if (!(extent <= 2ull * sum + 4096u)) return false;
+
+    const Window w = make_window(lo, (uint32_t)extent);
+    const uint32_t nq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(extent >> 4));
+    const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
+    const uint32_t r = rel & 15u, hq = rel >> 4;
+    constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
+    const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
+    uint4 hw[HW];
+#pragma unroll
+    for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
+    // boundaries (span byte positions, 0 = none): options start, transport start / end, field
+    uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
+    bool pre = !valid;
+    uint32_t base = 0;
+    // two steps in flight: step k + 1's loads go out before step k is staged and summed
+    uint4 v[SCPL];
+#pragma unroll
+    for (uint32_t c = 0; c < SCPL; ++c) {
+        const uint32_t q = 64u * c + lane;
+        v[c] = load_win<PICO_STREAM_NT != 0>(w, q < nq ? 16u * q : WIN_OOB);
+    }
+    STAMP(1);
+    for (uint32_t qb = 0; qb < nq; qb += SQ) {
+        uint4 vn[SCPL];
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) {
+            const uint32_t q = (PICO_STREAM_DB ? qb + SQ : qb) + 64u * c + lane;
+            if (PICO_STREAM_DB || qb != 0) vn[c] = load_win<PICO_STREAM_NT != 0>(w, q < nq ? 16u * q : WIN_OOB);
+            else vn[c] = v[c];
+        }
+        if (!PICO_STREAM_DB) {
+#pragma unroll
+            for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = v[c];
+        __builtin_amdgcn_wave_barrier();
+        // lane-major: lane L's SCPL chunks, chunk prefixes, one wave scan of the lane totals
+        uint32_t loc[SCPL];
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; ++k) {
+            loc[k] = t;
+            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
+        }
+        const uint32_t inc = (uint32_t)wave_incl<0>((int)t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        const uint32_t ex = base + inc - t;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; k += 4)
+            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
+                make_uint4(ex + loc[k], ex + loc[k + 1], ex + loc[k + 2], ex + loc[k + 3]);
+        __builtin_amdgcn_wave_barrier();
+        // frame j's head window chunks that are in this step
+#pragma unroll
+        for (uint32_t i = 0; i < HS; ++i) {
+            const uint32_t qi = hq + i - qb;
+            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
+        }
+        // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
+        // fails the header checks below never reads them)
+        if (!pre && hq + 1u < qb + SQ) {
+            pre = true;
+            uint32_t H[3];
+            window_words<3, false>(hw, r, H);
+            const uint32_t ihl = H[0] & 0x0Fu;
+            const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+            const uint32_t tot16 = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+            const uint32_t tl = (tot16 - hl) & 0xFFFFu;
+            const uint32_t pr = (H[2] >> 8) & 0xFFu;
+            b1 = rel + min(hl, len);
+            b2 = rel + min(hl + tl, len);
+            if (hl > 20u) {                  // options: their sum and the field, by prefixes too
+                b0 = rel + 20u;
+                const uint32_t xo = !tx ? (pr == 17u ? 6u : 0u) : pr == 6u ? 16u : pr == 1u ? 2u : 0u;
+                if (xo && hl + xo + 2u <= len) { x0 = rel + hl + xo; x1 = x0 + 2u; }
+            }
+        }
+        const uint32_t byte0 = 16u * qb;
+        stream_point(S, b1, byte0, P1);
+        stream_point(S, b2, byte0, P2);
+        if (__builtin_amdgcn_ballot_w64(b0 != 0u)) {
+            stream_point(S, b0, byte0, P0);
+            stream_point(S, x0, byte0, P3);
+            stream_point(S, x1, byte0, P4);
+        }
+        base += tot;
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    STAMP(2);
+    // the header (pico_ipv4_process_in's checks and dispatch, as sorted_batch)
+    uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, post = 0;
+    bool parsed = false, l4_needed = false, hasx = false;
+    if (valid) {
+        uint32_t H[5];
+        window_words<5, false>(hw, r, H);
+        const uint32_t ihl = H[0] & 0x0Fu;
+        hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+        const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
+        proto = (H[2] >> 8) & 0xFFu;
+        ipcrc = H[2] >> 16;
+        tl = (tot - hl) & 0xFFFFu;
+        const uint32_t max_allowed = (len - 20u) & 0xFFFFu;
+        if (!(hl > len || (!tx && tl > max_allowed) || hl + tl > len)) {
+            parsed = true;
+            verdict = 0;
+#pragma unroll
+            for (int m = 0; m < 5; ++m) hdr20 = dot2_add(H[m], hdr20);
+            pseudo = (H[3] & 0xFFFFu) + (H[3] >> 16) + (H[4] & 0xFFFFu) + (H[4] >> 16) + (proto << 8) +
+                     (((tl & 0xFFu) << 8) | (tl >> 8));
+            const uint32_t frag = ((H[1] >> 8) & 0xFF00u) | (H[1] >> 24);
+            const uint32_t s0 = H[3] & 0xFFu;
+            const bool bad_src = H[3] == 0xFFFFFFFFu || (s0 != 0xFFu && (s0 & 0xE0u) == 0xE0u) || s0 == 0x7Fu;
+            if (!tx && (bad_src || (frag & 0x8000u) || ihl < 5u)) post = PV_DROP;
+            else if (frag & 0x3FFFu) post = PV_FRAG;
+            if (!post && !tx) {
+                if (proto == 6u) {
+                    l4_needed = true;
+                } else if (proto == 17u) {
+                    if (hl + 8u > len) post = PV_DROP;
+                    else { l4_needed = true; hasx = true; }
+                }
+            } else if (!post) {
+                if (proto == 6u) {
+                    if (tl < 20u) verdict |= V_MALFORMED;
+                    else { l4_needed = true; hasx = true; }
+                } else if (proto == 1u) {
+                    if (tl < 8u) verdict |= V_MALFORMED;
+                    else { l4_needed = true; hasx = true; }
+                }
+            }
+        }
+    }
+    const bool odd = r & 1u;
+    // the field (frame pairing xp, even domain xe): from the head window, or with options by prefixes
+    uint32_t xe = 0, xp = 0;
+    if (hasx) {
+        if (hl == 20u) {
+            const uint32_t xo = !tx ? 6u : proto == 6u ? 16u : 2u;
+            xp = hw_pair<HS>(hw, r + 20u + xo);
+            xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
+        } else {
+            xe = P4 - P3;
+            xp = odd ? ((xe >> 8) | (xe << 8)) & 0xFFFFu : xe;
+        }
+    }
+    // transport; TX: the field's share kept apart (finish subtracts it; TX fields lie inside the
+    // region), RX: the field only says "present" (a UDP crc may lie past a short region)
+    const uint32_t tsum = tx ? pairing(P2 - P1 - xe, odd) + xp : pairing(P2 - P1, odd);
+    const uint32_t opt = hl > 20u ? pairing(P1 - P0, odd) : 0u;
+    const uint64_t a0off = valid ? off - r : 0u;
+    if (lane < cnt)
+        finish_frame<1>(p, f0 + lane, tx, hdr20 + opt + tsum, xp, opt,
+                        make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, r),
+                        make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
+                                       (proto << 8) | (tl << 16),
+                                   hl | (ipcrc << 16), pseudo, hdr20),
+                        NONE);
+    STAMP(3);
+    return true;
+}
+#endif
+
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
 #ifndef PICO_SORTED_WPB
@@ -753,7 +1057,14 @@ __global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(Fl
     SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
     const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
     STAMP(0);
-    if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+    if (f0 < p.n) {
+#if PICO_STREAM
+        if constexpr (MODE == 1) {
+            if (stream_batch(p, S.st, lane, f0)) return;
+        }
+#endif
+        sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+    }
     STAMP(3);
 }
 

@@ -16,7 +16,7 @@ for r in $(seq ${ROUNDS:-3}); do
     [ $v != new ] && lib=$R/picotcp_amd/ab/libpicocsum_$v.so
     for c in ${CFGS:-c2 c2v6 c2eth c2tx}; do
       PICO_CSUM_LIB=$lib timeout -k 10 120 python bench.py --config $c --steps ${STEPS:-100} --warmup 10 \
-          --no-e2e --no-cpu ${VERIFY:---no-verify} > $O/ab_line.json 2> $O/ab_err.txt
+          --no-e2e --no-cpu ${VERIFY:---no-verify} ${EXTRA:-} > $O/ab_line.json 2> $O/ab_err.txt
       python -c "
 import json; d=json.load(open('$O/ab_line.json')); r=d['roofline']
 print('$v', '$c', r['kernel_avg_us'], d['value'], d.get('verified', {}).get('mismatches', '-'))" >> $O/ab_$TAG.txt
