@@ -844,14 +844,22 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
 }
 
 // Returns false (nothing written) when the wave's frames are not one dense span; the caller
-// then runs the sorted-rounds batch.
+// then runs the sorted-rounds batch.  NATM: the NAT batch (F_NAT), its own instantiation so the
+// RX / TX waves carry none of its registers or instructions.
+template <bool NATM>
 __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane,
                                              uint64_t f0) {
-    if (p.flags & (F_NAT | F_MACF)) return false;
+    if (p.flags & F_MACF) return false;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = (p.flags & 2u) != 0;
+    constexpr bool natm = NATM;
     uint4 dcur = make_uint4(0, 0, 0, 0);
     if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+    // NAT: the frame's record {addr, port | dir << 16} (sorted_batch's NAT stage)
+    uint2 rw = make_uint2(0u, 0u);
+    if (NATM && lane < cnt)
+        rw = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo) +
+                                             8ull * (f0 + lane));
     uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
     uint32_t len = lane < cnt ? dcur.z : 0u;
     const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
@@ -972,7 +980,8 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     STAMP(2);
     // the header (pico_ipv4_process_in's checks and dispatch, as sorted_batch)
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, post = 0;
-    bool parsed = false, l4_needed = false, hasx = false;
+    uint32_t l2v = natm ? NS_SKIP : 0u, nop = 0, nnw = 0;   // NAT: state, old / new port (frame pairing)
+    bool parsed = false, l4_needed = false, hasx = false, nat_opt = false;
     if (valid) {
         uint32_t H[5];
         window_words<5, false>(hw, r, H);
@@ -1003,22 +1012,47 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
                     else { l4_needed = true; hasx = true; }
                 }
             } else if (!post) {
+                // NAT: TCP and UDP recomputed in full, ICMP only its header checksum (as sorted_batch)
                 if (proto == 6u) {
                     if (tl < 20u) verdict |= V_MALFORMED;
                     else { l4_needed = true; hasx = true; }
-                } else if (proto == 1u) {
+                } else if (proto == (natm ? 17u : 1u)) {
                     if (tl < 8u) verdict |= V_MALFORMED;
                     else { l4_needed = true; hasx = true; }
                 }
             }
+            // NAT (pico_nat.c:424-545): the rewritten address enters the header and pseudo sums as
+            // a delta, the port the region's (below) -- sorted_batch's NAT stage, with the old port
+            // from the head window (a datagram with options falls back to the sorted rounds)
+            if constexpr (NATM) {
+                const uint32_t dir = (rw.y >> 16) & 0xFFu;
+                l2v = NS_SKIP;
+                if (post == 0u && (dir == 1u || dir == 2u)) {
+                    if ((proto == 6u || proto == 17u) && !l4_needed) {
+                        l2v = NS_BAD;
+                    } else if (proto == 6u || proto == 17u) {
+                        const uint32_t old = dir == 1u ? H[3] : H[4];
+                        const uint32_t da = (rw.x & 0xFFFFu) + (rw.x >> 16) - (old & 0xFFFFu) - (old >> 16);
+                        hdr20 += da;
+                        pseudo += da;
+                        if (hl == 20u) nop = hw_pair<HS>(hw, r + 20u + (dir == 1u ? 0u : 2u));
+                        else nat_opt = true;
+                        nnw = rw.y & 0xFFFFu;
+                        l2v = NS_XLATE | (dir << 4);
+                    } else if (proto == 1u) {
+                        l2v = NS_HDR;
+                    }
+                }
+            }
         }
     }
+    if (__builtin_amdgcn_ballot_w64(nat_opt)) return false;
     const bool odd = r & 1u;
     // the field (frame pairing xp, even domain xe): from the head window, or with options by prefixes
     uint32_t xe = 0, xp = 0;
     if (hasx) {
         if (hl == 20u) {
-            const uint32_t xo = !tx ? 6u : proto == 6u ? 16u : 2u;
+            const uint32_t xo = (!tx || proto == 17u) ? 6u : proto == 6u ? 16u : 2u;
             xp = hw_pair<HS>(hw, r + 20u + xo);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         } else {
@@ -1028,7 +1062,9 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     }
     // transport; TX: the field's share kept apart (finish subtracts it; TX fields lie inside the
     // region), RX: the field only says "present" (a UDP crc may lie past a short region)
-    const uint32_t tsum = tx ? pairing(P2 - P1 - xe, odd) + xp : pairing(P2 - P1, odd);
+    // NAT: the old port leaves the region in the even domain (no wrap below zero), the new enters
+    const uint32_t noe = odd ? ((nop >> 8) | (nop << 8)) & 0xFFFFu : nop;
+    const uint32_t tsum = tx ? pairing(P2 - P1 - xe - noe, odd) + xp + nnw : pairing(P2 - P1, odd);
     const uint32_t opt = hl > 20u ? pairing(P1 - P0, odd) : 0u;
     const uint64_t a0off = valid ? off - r : 0u;
     if (lane < cnt)
@@ -1036,7 +1072,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
                         make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, r),
                         make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
                                        (proto << 8) | (tl << 16),
-                                   hl | (ipcrc << 16), pseudo, hdr20),
+                                   hl | (l2v << 8) | (ipcrc << 16), pseudo, hdr20),
                         NONE);
     STAMP(3);
     return true;
@@ -1060,7 +1096,8 @@ __global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(Fl
     if (f0 < p.n) {
 #if PICO_STREAM
         if constexpr (MODE == 1) {
-            if (stream_batch(p, S.st, lane, f0)) return;
+            if ((p.flags & F_NAT) ? stream_batch<true>(p, S.st, lane, f0) : stream_batch<false>(p, S.st, lane, f0))
+                return;
         }
 #endif
         sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);

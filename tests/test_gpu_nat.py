@@ -70,3 +70,50 @@ def test_imix_burst_vs_oracle(seed):
     np.testing.assert_array_equal(ol, wol)
     np.testing.assert_array_equal(got, want)
     assert {1, 16, 32}.issubset(set(np.unique(v).tolist()))
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_dense_burst_with_options_vs_oracle(seed):
+    """Densely packed datagrams (odd and even starts) of which a few carry IPv4 options: the waves
+    without options take the stream-order batch (NAT old port from the head window), a wave
+    holding a translated datagram with options falls back to the sorted rounds -- every byte,
+    stored checksum and verdict against the oracle."""
+    rng = np.random.default_rng(seed)
+    n = 16384
+    lens = rng.integers(60, 1500, n).astype(np.uint32)
+    ihl = np.where(rng.random(n) < 0.004, rng.integers(6, 16, n), 5)
+    parts, net, pos = [], np.zeros(n, np.int64), 0
+    for h in np.unique(ihl):                            # one packed batch per header length
+        sel = np.flatnonzero(ihl == h)
+        b, o, _ = synth.ipv4_batch(lens[sel], seed=seed + int(h), proto=6, ihl=int(h))
+        ends = np.append(o[1:].astype(np.int64), b.size)
+        for k, i in enumerate(sel):
+            parts.append((i, b[int(o[k]):int(ends[k])]))
+    parts.sort(key=lambda t: t[0])
+    for i, fb in parts:                                  # back in datagram order, packed
+        net[i] = pos
+        pos += fb.size
+    buf = np.concatenate([fb for _, fb in parts])
+    proto = rng.choice(np.array([6, 17, 1], np.uint8), n, p=[0.5, 0.4, 0.1])
+    udp = proto == 17
+    buf[net + 9] = proto
+    hl = 4 * ihl
+    ul = lens - hl                                       # UDP length field for the UDP datagrams
+    buf[(net + hl + 4)[udp]] = (ul[udp] >> 8).astype(np.uint8)
+    buf[(net + hl + 5)[udp]] = (ul[udp] & 0xFF).astype(np.uint8)
+    nat = np.zeros(n, O.NAT_DTYPE)
+    nat["addr"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    nat["port"] = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    nat["dir"] = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.1, 0.5, 0.4])
+    desc = batch.make_desc(net.astype(np.uint64), lens)
+    assert (net & 1).any() and (ihl > 5).any()
+    for fpw in (0, 64):
+        if fpw:
+            batch.set_launch_override(0, 0, fpw)
+        got, on, ol, v = run(buf, desc, nat)
+        want = buf.copy()
+        won, wol, wv = O.batch_ipv4_nat(want, desc, nat)
+        np.testing.assert_array_equal(v, wv)
+        np.testing.assert_array_equal(on, won)
+        np.testing.assert_array_equal(ol, wol)
+        np.testing.assert_array_equal(got, want)
