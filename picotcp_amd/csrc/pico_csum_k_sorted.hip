@@ -845,8 +845,10 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
 
 // Returns false (nothing written) when the wave's frames are not one dense span; the caller
 // then runs the sorted-rounds batch.  NATM: the NAT batch (F_NAT), its own instantiation so the
-// RX / TX waves carry none of its registers or instructions.
-template <bool NATM>
+// RX / TX waves carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for
+// datagrams whose transport follows the 40-byte header (descriptor seed 0; RX next header TCP /
+// UDP / ICMPv6 -- anything else needs the extension-header walk: the sorted rounds).
+template <bool NATM, bool V6 = false>
 __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane,
                                              uint64_t f0) {
     if (p.flags & F_MACF) return false;
@@ -864,7 +866,8 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     uint32_t len = lane < cnt ? dcur.z : 0u;
     const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
     if (oob || lane >= cnt) { len = 0; off = 0; }
-    const bool valid = len >= 20u;                            // shorter: MALFORMED, nothing to sum
+    const bool valid = len >= (V6 ? 40u : 20u);               // shorter: MALFORMED, nothing to sum
+    if (V6 && __builtin_amdgcn_ballot_w64(valid && dcur.w != 0u)) return false;   // a stack-walked seed
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off;
     // the span, relative to the first valid frame's line (a frame more than 512 MiB away:
     // not one span)
@@ -945,7 +948,17 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
         }
         // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
         // fails the header checks below never reads them)
-        if (!pre && hq + 1u < qb + SQ) {
+        if (V6 && !pre && hq + 1u < qb + SQ) {
+            pre = true;
+            uint32_t H[2];
+            window_words<2, false>(hw, r, H);
+            const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+            const uint32_t nh = (H[1] >> 16) & 0xFFu;
+            b1 = rel + 40u;
+            b2 = rel + min(40u + plen, len);
+            if (tx && nh == 6u && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }   // TCP crc: past the head chunks
+        }
+        if (!V6 && !pre && hq + 1u < qb + SQ) {
             pre = true;
             uint32_t H[3];
             window_words<3, false>(hw, r, H);
@@ -965,7 +978,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
         const uint32_t byte0 = 16u * qb;
         stream_point(S, b1, byte0, P1);
         stream_point(S, b2, byte0, P2);
-        if (__builtin_amdgcn_ballot_w64(b0 != 0u)) {
+        if (__builtin_amdgcn_ballot_w64(b0 != 0u || x0 != 0u)) {
             stream_point(S, b0, byte0, P0);
             stream_point(S, x0, byte0, P3);
             stream_point(S, x1, byte0, P4);
@@ -978,6 +991,66 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     }
 
     STAMP(2);
+    if constexpr (V6) {
+        // pico_ipv6_process_in / pico_transport_crc_check as sorted_batch's MODE 2 (seed 0, no
+        // extension header): lengths, byte-9 dispatch (ipcrc), the field, the pseudo header
+        uint32_t verdict = V_MALFORMED, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, xo = NONE;
+        bool parsed = false, l4_needed = false, walk = false;
+        if (valid) {
+            uint32_t H[10];
+            window_words<10, false>(hw, r, H);
+            tl = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+            proto = (H[1] >> 16) & 0xFFu;
+            if (!tx && proto != 6u && proto != 17u && proto != 58u) {
+                walk = true;
+            } else if (40u + tl <= len) {
+                uint32_t addr = 0;
+#pragma unroll
+                for (int m = 2; m < 10; ++m) addr = dot2_add(H[m], addr);
+                pseudo = addr + (((tl & 0xFFu) << 8) | (tl >> 8)) + (proto << 8);
+                parsed = true;
+                verdict = 0;
+                if (!tx) {
+                    ipcrc = (H[2] >> 8) & 0xFFu;
+                    const bool ref17 = !(p.flags & F_NXD) && ipcrc == 17u;
+                    if (proto == 6u && !ref17) {
+                        l4_needed = true;
+                    } else if (proto == 17u || proto == 6u) {
+                        if (48u > len) { parsed = false; verdict = V_MALFORMED; }
+                        else { l4_needed = true; xo = 6u; }
+                    } else if (proto == 58u) {
+                        if (41u > len) { parsed = false; verdict = V_MALFORMED; }
+                        else { l4_needed = true; xo = 0u; }
+                    }
+                } else if (proto == 6u || proto == 17u || proto == 58u) {
+                    if (tl < (proto == 6u ? 20u : proto == 17u ? 8u : 4u)) { parsed = false; verdict = V_MALFORMED; }
+                    else { l4_needed = true; xo = proto == 6u ? 16u : proto == 17u ? 6u : 2u; }
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(walk)) return false;
+        const bool odd = r & 1u;
+        uint32_t xe = 0, xp = 0;
+        if (xo == 16u) {                       // TX TCP: by prefixes
+            xe = P4 - P3;
+            xp = odd ? ((xe >> 8) | (xe << 8)) & 0xFFFFu : xe;
+        } else if (xo != NONE) {
+            xp = hw_pair<HS>(hw, r + 40u + xo);
+            xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
+        }
+        const uint32_t tsum = tx ? pairing(P2 - P1 - xe, odd) + xp : pairing(P2 - P1, odd);
+        // the transport's line and offset (finish stores the field relative to it)
+        const uint32_t rt = (r + 40u) & 15u;
+        const uint64_t a0t = valid ? off + 40u - rt : 0u;
+        if (lane < cnt)
+            finish_frame<2>(p, f0 + lane, tx, tsum, xp, 0u, make_uint4((uint32_t)a0t, (uint32_t)(a0t >> 32), 0u, rt),
+                            make_uint4(verdict | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
+                                           (proto << 8) | (tl << 16),
+                                       ipcrc << 16, pseudo, 0u),
+                            NONE);
+        STAMP(3);
+        return true;
+    }
     // the header (pico_ipv4_process_in's checks and dispatch, as sorted_batch)
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, post = 0;
     uint32_t l2v = natm ? NS_SKIP : 0u, nop = 0, nnw = 0;   // NAT: state, old / new port (frame pairing)
@@ -1095,6 +1168,9 @@ __global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(Fl
     STAMP(0);
     if (f0 < p.n) {
 #if PICO_STREAM
+        if constexpr (MODE == 2) {
+            if (stream_batch<false, true>(p, S.st, lane, f0)) return;
+        }
         if constexpr (MODE == 1) {
             if ((p.flags & F_NAT) ? stream_batch<true>(p, S.st, lane, f0) : stream_batch<false>(p, S.st, lane, f0))
                 return;

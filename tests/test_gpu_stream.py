@@ -1,0 +1,83 @@
+"""GPU: the stream-order waves (K4s, `stream_batch` in pico_csum_k_sorted.hip) on densely packed
+IPv6 batches -- TCP / UDP / ICMPv6 mixed per datagram, odd and even starts, a few datagrams with
+a hop-by-hop header (RX: the extension-header walk, so their waves fall back to the sorted rounds)
+-- RX, TX with the fields written in place and RX of the written bytes, against the oracle."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from picotcp_amd import batch, synth
+from tests.test_gpu_parity import to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _reset_override():
+    yield
+    batch.set_launch_override(0, 0, 0)
+
+
+def packed_ipv6(rng, n, seed, p_hbh):
+    """n datagrams, each drawn from one of the per-kind batches, copied back to back."""
+    kinds = [dict(proto=6), dict(proto=17), dict(proto=58, icmp_type=128), dict(proto=6, hbh=True, walked=True)]
+    pk = np.array([0.5, 0.3, 0.2, 0.0]) * (1 - p_hbh) + np.array([0, 0, 0, p_hbh])
+    kind = rng.choice(len(kinds), n, p=pk)
+    lens = rng.integers(68, 1500, n).astype(np.uint32)
+    frames = [None] * n
+    for k, kw in enumerate(kinds):
+        sel = np.flatnonzero(kind == k)
+        if sel.size == 0:
+            continue
+        b, o, _, _ = synth.ipv6_batch(lens[sel], seed=seed + k, eth=False, **kw)
+        ends = np.append(o[1:].astype(np.int64), b.size)
+        for j, i in enumerate(sel):
+            frames[i] = b[int(o[j]):int(ends[j])]
+    net = np.zeros(n, np.uint64)
+    net[1:] = np.cumsum([f.size for f in frames])[:-1]
+    buf = np.concatenate(frames)
+    avail = np.array([f.size for f in frames], np.uint32)
+    return buf, batch.make_desc(net, avail)
+
+
+@pytest.mark.parametrize("p_hbh", [0.0, 0.003])
+@pytest.mark.parametrize("fpw", [0, 64, 17])
+def test_dense_ipv6_rx_tx(p_hbh, fpw):
+    rng = np.random.default_rng(77 + int(p_hbh * 1000) + fpw)
+    n = 20000
+    buf, desc = packed_ipv6(rng, n, 500 + fpw, p_hbh)
+    assert (desc["off"] & 1).any()
+    if fpw:
+        batch.set_launch_override(2, fpw=fpw)
+    d_desc = batch.desc_to_device(desc, "cuda:0")
+    # TX, written in place
+    d_buf = to_dev(buf)
+    l4, v = batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize()
+    wl, wv = O.batch_ipv6(buf, desc, tx=True)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    np.testing.assert_array_equal(l4.cpu().numpy().view(np.uint16), wl)
+    # the bytes: the oracle's values stored big-endian at the field of every accepted TCP / UDP /
+    # ICMPv6 datagram (offset 16 / 6 / 2 behind the 40-byte header), nothing else changed
+    want = buf.copy()
+    off = desc["off"].astype(np.int64)
+    nh = buf[off + 6]
+    fo = np.select([nh == 6, nh == 17, nh == 58], [16, 6, 2], -1)
+    w = np.flatnonzero((wv == 1) & (fo >= 0))
+    pos = off[w] + 40 + fo[w]
+    want[pos] = (wl[w] >> 8).astype(np.uint8)
+    want[pos + 1] = (wl[w] & 0xFF).astype(np.uint8)
+    got = d_buf.cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    # RX of the written datagrams (every TCP / UDP / ICMPv6 one accepted), and of the originals
+    for b in (got, buf):
+        for nx in (False, True):                     # byte-9 dispatch (the reference's) / next header
+            l4, v = batch.ipv6_checksum_batch(to_dev(b), d_desc, n, flags=batch.F_NXTHDR_DISPATCH if nx else 0)
+            wl, wv = O.batch_ipv6(b, desc, nxthdr_dispatch=nx)
+            np.testing.assert_array_equal(v.cpu().numpy(), wv)
+            np.testing.assert_array_equal(l4.cpu().numpy().view(np.uint16), wl)
+            if nx and b is got:                      # every written datagram verifies
+                assert (wv == 1).sum() >= n - int(p_hbh * n * 3) - 5
