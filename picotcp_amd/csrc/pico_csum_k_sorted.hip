@@ -848,10 +848,13 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
 // RX / TX waves carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for
 // datagrams whose transport follows the 40-byte header (descriptor seed 0; RX next header TCP /
 // UDP / ICMPv6 -- anything else needs the extension-header walk: the sorted rounds).
-template <bool NATM, bool V6 = false>
+// ETH: the Ethernet batch (MODE 3) for IPv4 behind the 14-byte header (ARP / dropped frames need
+// no sums; a wave holding an IPv6 frame falls back after the loop).
+template <bool NATM, bool V6 = false, bool ETH = false>
 __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane,
                                              uint64_t f0) {
-    if (p.flags & F_MACF) return false;
+    constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
+    if (!ETH && (p.flags & F_MACF)) return false;
     const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
     const bool tx = (p.flags & 2u) != 0;
     constexpr bool natm = NATM;
@@ -866,7 +869,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     uint32_t len = lane < cnt ? dcur.z : 0u;
     const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
     if (oob || lane >= cnt) { len = 0; off = 0; }
-    const bool valid = len >= (V6 ? 40u : 20u);               // shorter: MALFORMED, nothing to sum
+    const bool valid = len >= (V6 ? 40u : ETH ? 14u : 20u);  // shorter: MALFORMED, nothing to sum
     if (V6 && __builtin_amdgcn_ballot_w64(valid && dcur.w != 0u)) return false;   // a stack-walked seed
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off;
     // the span, relative to the first valid frame's line (a frame more than 512 MiB away:
@@ -958,21 +961,25 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
             b2 = rel + min(40u + plen, len);
             if (tx && nh == 6u && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }   // TCP crc: past the head chunks
         }
-        if (!V6 && !pre && hq + 1u < qb + SQ) {
+        if (!V6 && !pre && hq + (ETH ? 2u : 1u) < qb + SQ) {
             pre = true;
             uint32_t H[3];
-            window_words<3, false>(hw, r, H);
+            window_words<3, ETH>(hw, r + L2, H);
+            const uint32_t ilen = len - L2;
             const uint32_t ihl = H[0] & 0x0Fu;
             const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
             const uint32_t tot16 = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
             const uint32_t tl = (tot16 - hl) & 0xFFFFu;
             const uint32_t pr = (H[2] >> 8) & 0xFFu;
-            b1 = rel + min(hl, len);
-            b2 = rel + min(hl + tl, len);
+            b1 = rel + L2 + min(hl, ilen);
+            b2 = rel + L2 + min(hl + tl, ilen);
             if (hl > 20u) {                  // options: their sum and the field, by prefixes too
-                b0 = rel + 20u;
+                b0 = rel + L2 + 20u;
                 const uint32_t xo = !tx ? (pr == 17u ? 6u : 0u) : pr == 6u ? 16u : pr == 1u ? 2u : 0u;
-                if (xo && hl + xo + 2u <= len) { x0 = rel + hl + xo; x1 = x0 + 2u; }
+                if (xo && hl + xo + 2u <= ilen) { x0 = rel + L2 + hl + xo; x1 = x0 + 2u; }
+            } else if (ETH && tx && pr == 6u && 38u <= ilen) {   // TX TCP crc: past the head chunks
+                x0 = rel + L2 + 36u;
+                x1 = x0 + 2u;
             }
         }
         const uint32_t byte0 = 16u * qb;
@@ -1054,18 +1061,42 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     // the header (pico_ipv4_process_in's checks and dispatch, as sorted_batch)
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, post = 0;
     uint32_t l2v = natm ? NS_SKIP : 0u, nop = 0, nnw = 0;   // NAT: state, old / new port (frame pairing)
-    bool parsed = false, l4_needed = false, hasx = false, nat_opt = false;
-    if (valid) {
+    bool parsed = false, l4_needed = false, hasx = false, nat_opt = false, ip4 = valid, eth6 = false;
+    const uint32_t ilen = len - L2;
+    if constexpr (ETH) {
+        // pico_ethernet_receive (pico_ethernet.c:180-235): destination filter, ethertype, version
+        ip4 = false;
+        if (valid) {
+            uint32_t M[2], T[1];
+            window_words<2, true>(hw, r, M);
+            window_words<1, true>(hw, r + 12u, T);
+            const uint32_t m0 = M[0], m1 = M[1] & 0xFFFFu, et = T[0] & 0xFFFFu;
+            const bool mine = !(p.flags & F_MACF) || tx || (m0 == p.mac_lo && m1 == p.mac_hi) ||
+                              (m0 & 0xFFFFFFu) == 0x5E0001u || (m0 & 0xFFFFu) == 0x3333u ||
+                              (m0 == 0xFFFFFFFFu && m1 == 0xFFFFu);
+            if (!mine) l2v = V_DROP_L2;
+            else if (et == 0x0608u) l2v = V_ARP;
+            else if (et == 0xDD86u) eth6 = true;         // IPv6: the sorted rounds
+            else if (et != 0x0008u) l2v = V_DROP_L2;
+            else if (ilen != 0u) {
+                uint32_t V[1];
+                window_words<1, true>(hw, r + 14u, V);
+                if ((V[0] & 0xF0u) != 0x40u) l2v = V_DROP_L2;
+                else ip4 = true;
+            }
+        }
+    }
+    if (ETH ? ip4 && ilen >= 20u : valid) {
         uint32_t H[5];
-        window_words<5, false>(hw, r, H);
+        window_words<5, ETH>(hw, r + L2, H);
         const uint32_t ihl = H[0] & 0x0Fu;
         hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
         const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
         proto = (H[2] >> 8) & 0xFFu;
         ipcrc = H[2] >> 16;
         tl = (tot - hl) & 0xFFFFu;
-        const uint32_t max_allowed = (len - 20u) & 0xFFFFu;
-        if (!(hl > len || (!tx && tl > max_allowed) || hl + tl > len)) {
+        const uint32_t max_allowed = (ilen - 20u) & 0xFFFFu;
+        if (!(hl > ilen || (!tx && tl > max_allowed) || hl + tl > ilen)) {
             parsed = true;
             verdict = 0;
 #pragma unroll
@@ -1081,7 +1112,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
                 if (proto == 6u) {
                     l4_needed = true;
                 } else if (proto == 17u) {
-                    if (hl + 8u > len) post = PV_DROP;
+                    if (hl + 8u > ilen) post = PV_DROP;
                     else { l4_needed = true; hasx = true; }
                 }
             } else if (!post) {
@@ -1119,14 +1150,14 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
             }
         }
     }
-    if (__builtin_amdgcn_ballot_w64(nat_opt)) return false;
+    if (__builtin_amdgcn_ballot_w64(ETH ? eth6 : nat_opt)) return false;
     const bool odd = r & 1u;
     // the field (frame pairing xp, even domain xe): from the head window, or with options by prefixes
     uint32_t xe = 0, xp = 0;
     if (hasx) {
-        if (hl == 20u) {
+        if (hl == 20u && !(ETH && tx && proto == 6u)) {
             const uint32_t xo = (!tx || proto == 17u) ? 6u : proto == 6u ? 16u : 2u;
-            xp = hw_pair<HS>(hw, r + 20u + xo);
+            xp = hw_pair<HS>(hw, r + L2 + 20u + xo);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         } else {
             xe = P4 - P3;
@@ -1139,10 +1170,12 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     const uint32_t noe = odd ? ((nop >> 8) | (nop << 8)) & 0xFFFFu : nop;
     const uint32_t tsum = tx ? pairing(P2 - P1 - xe - noe, odd) + xp + nnw : pairing(P2 - P1, odd);
     const uint32_t opt = hl > 20u ? pairing(P1 - P0, odd) : 0u;
-    const uint64_t a0off = valid ? off - r : 0u;
+    // the IPv4 header's line and offset (finish stores relative to it)
+    const uint32_t ri = (r + L2) & 15u;
+    const uint64_t a0off = valid ? off + L2 - ri : 0u;
     if (lane < cnt)
-        finish_frame<1>(p, f0 + lane, tx, hdr20 + opt + tsum, xp, opt,
-                        make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, r),
+        finish_frame<ETH ? 3 : 1>(p, f0 + lane, tx, hdr20 + opt + tsum, xp, opt,
+                        make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, ri),
                         make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
                                        (proto << 8) | (tl << 16),
                                    hl | (l2v << 8) | (ipcrc << 16), pseudo, hdr20),
@@ -1170,6 +1203,9 @@ __global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(Fl
 #if PICO_STREAM
         if constexpr (MODE == 2) {
             if (stream_batch<false, true>(p, S.st, lane, f0)) return;
+        }
+        if constexpr (MODE == 3) {
+            if (stream_batch<false, false, true>(p, S.st, lane, f0)) return;
         }
         if constexpr (MODE == 1) {
             if ((p.flags & F_NAT) ? stream_batch<true>(p, S.st, lane, f0) : stream_batch<false>(p, S.st, lane, f0))

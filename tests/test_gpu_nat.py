@@ -34,7 +34,7 @@ def run(buf, desc, nat):
 def test_reference_fixture(fpw):
     c = cases()
     if fpw:
-        batch.set_launch_override(0, 0, fpw)
+        batch.set_launch_override(2, fpw=fpw)
     got, on, ol, v = run(c["buf"], c["desc"], c["nat"])
     wo = c["buf"].copy()
     won, wol, wv = O.batch_ipv4_nat(wo, c["desc"], c["nat"])
@@ -109,7 +109,7 @@ def test_dense_burst_with_options_vs_oracle(seed):
     assert (net & 1).any() and (ihl > 5).any()
     for fpw in (0, 64):
         if fpw:
-            batch.set_launch_override(0, 0, fpw)
+            batch.set_launch_override(2, fpw=fpw)
         got, on, ol, v = run(buf, desc, nat)
         want = buf.copy()
         won, wol, wv = O.batch_ipv4_nat(want, desc, nat)
