@@ -47,7 +47,12 @@
 extern "C" {
 #endif
 
-#define PICO_CSUM_ABI_VERSION 2   /* 2: V_FRAG, the reference's IPv6 dispatch by default */
+/* ABI history (a caller must check pico_csum_abi_version() == PICO_CSUM_ABI_VERSION):
+ *   2: V_FRAG, the reference's IPv6 byte-9 dispatch by default;
+ *   3: F_NXTHDR_DISPATCH moved to 0x8 (bit 0x4 -- ABI 1's F_REF_DISPATCH, the opposite meaning --
+ *      is rejected with -EINVAL); the forwarding batch takes the host's link addresses and a
+ *      carried state (pico_ipv4_pre_forward_checks in full). */
+#define PICO_CSUM_ABI_VERSION 3
 
 /* picoTCP pico_err values used here (include/pico_protocol.h:27,31,38 + ENODEV) */
 #define PICO_CSUM_EIO     5
@@ -81,10 +86,19 @@ struct pico_csum_desc {
  * check.  With this flag the check follows the transport's own protocol instead (TCP always,
  * UDP when its crc != 0: the evident intent, not the reference's behaviour).  ICMPv6 is the
  * same either way (pico_icmp6_process_in checks it itself). */
-#define PICO_CSUM_F_NXTHDR_DISPATCH 0x4u
+#define PICO_CSUM_F_NXTHDR_DISPATCH 0x8u
+#define PICO_CSUM_F_RETIRED_0x4     0x4u  /* ABI 1's F_REF_DISPATCH: rejected (-EINVAL) since ABI 3 */
 
 /* Verdict byte of the fused batches: the reference's FIRST outcome for the frame, in its own
- * order (one value, plus V_IPV6 on the Ethernet batch's IPv6 frames). */
+ * order (one value, plus V_IPV6 on the Ethernet batch's IPv6 frames).
+ * The values are per batch kind: bits 16, 32 and 64 mean different things in different batches
+ * (V_FRAG / V_EXPIRED; V_DROP_L2 / V_UNTOUCHED / V_LOCAL_SRC; V_ARP / V_DUPLICATE).  Decode a
+ * verdict array only with the list given at the batch that produced it:
+ *   RX / TX (IPv4, IPv6):  ACCEPT, NET_BAD (IPv4), L4_BAD, MALFORMED, FRAG
+ *   Ethernet:              the RX / TX list, DROP_L2, ARP, | IPV6
+ *   forwarding:            ACCEPT, MALFORMED, EXPIRED, LOCAL_SRC, DUPLICATE
+ *   NAT:                   ACCEPT, MALFORMED, FRAG, UNTOUCHED
+ *   reassembly:            ACCEPT, L4_BAD, MALFORMED */
 #define PICO_CSUM_V_ACCEPT    1u  /* delivered to the transport and every checksum the reference
                                      checks passes: hand the frame on (a stack built with CRC=0
                                      need not check it again) */
@@ -102,6 +116,10 @@ struct pico_csum_desc {
                                      datagram): route it to the reassembly batch.  TX: the
                                      header checksum only (the transport's covers the datagram). */
 #define PICO_CSUM_V_EXPIRED  16u  /* forwarding batch only (same bit): TTL reached 0 (pico_ipv4.c:1549-1552) */
+#define PICO_CSUM_V_LOCAL_SRC 32u /* forwarding batch only: the source is one of the host's link addresses
+                                     (pico_ipv4.c:1559-1560) */
+#define PICO_CSUM_V_DUPLICATE 64u /* forwarding batch only: (src, id, dst, proto) of the last forwarded
+                                     datagram (pico_ipv4.c:1562-1565) */
 #define PICO_CSUM_V_DROP_L2  32u  /* Ethernet batch: discarded by the link layer -- foreign destination MAC
                                      (pico_ethernet.c:221-231), unknown ethertype (:201-202) or an IP
                                      version that does not match it (:143-150, :162-176) */
@@ -219,14 +237,34 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
                                 uint32_t flags, const uint8_t *mac, uint16_t *d_out_net, uint16_t *d_out_transport,
                                 uint8_t *d_verdict, void *stream);
 
-/* Forwarding step of pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) for a batch
- * of IPv4 datagrams routed through this host (desc.off -> IPv4 header, desc.len =
- * bytes available, >= 20): hdr->ttl is decremented in place; a datagram whose TTL
- * reaches 0 is PICO_CSUM_V_EXPIRED (the reference drops it, crc untouched); every
- * other one gets the reference's `hdr->crc++` (:1556, a native little-endian
- * increment of the stored field) and PICO_CSUM_V_ACCEPT.  Regions past base_len or
- * shorter than 20 bytes are MALFORMED and untouched.  d_verdict may be NULL. */
+/* Forwarding step: pico_ipv4_pre_forward_checks (modules/pico_ipv4.c:1535-1574), which
+ * pico_ipv4_forward (:1580-1603) runs on a datagram once route_find has a route for it, for a batch
+ * of IPv4 datagrams routed through this host (desc.off -> IPv4 header, desc.len = bytes available,
+ * >= 20), IN BATCH ORDER:
+ *   hdr->ttl is decremented in place; a datagram whose TTL reaches 0 is V_EXPIRED (the reference
+ *   drops it -- and sends pico_notify_ttl_expired, the caller's job -- crc untouched);
+ *   every other one gets the reference's `hdr->crc++` (:1556, a native little-endian increment of
+ *   the stored field), then:
+ *   V_LOCAL_SRC  its source is one of local_addrs[0 .. n_local) (the host's link addresses, as
+ *                stored: pico_ipv4_link_get's table, :1559; host memory, n_local <= 32);
+ *   V_DUPLICATE  (src, id, dst, proto) equals the last datagram that got this far (:1562-1571);
+ *   V_ACCEPT     forwarded: it becomes the last datagram (the caller goes on with NAT, the MTU
+ *                check and pico_datalink_send, :1600-1610).
+ * d_state (device memory, struct pico_csum_fwd_state) is the reference's static last tuple, carried
+ * from one batch to the next; zero it once at start (the reference's initial value: a first datagram
+ * with an all-zero tuple is a duplicate).  NULL: a zero state, not kept.  Calls that share a d_state
+ * must be ordered (one stream).  Regions past base_len or shorter than 20 bytes are V_MALFORMED,
+ * untouched, and leave the state alone.  d_verdict is required (the batch order is resolved through
+ * it).  Three kernel launches on `stream`. */
+struct pico_csum_fwd_state {
+    uint32_t src;       /* last_src, as stored */
+    uint32_t dst;       /* last_dst */
+    uint16_t id;        /* last_id, as stored (bytes 4-5 of the header) */
+    uint16_t proto;     /* last_proto */
+    uint32_t reserved;
+};
 int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                const uint32_t *local_addrs, uint32_t n_local, struct pico_csum_fwd_state *d_state,
                                 uint8_t *d_verdict, void *stream);
 
 /* NAT rewrite of a batch of IPv4 datagrams: the frame work of
@@ -244,8 +282,7 @@ int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pi
  * recomputes rather than adjusts, a wrong stored transport checksum comes out right.
  * A fragment (MF or an offset) is V_FRAG and untouched (it reaches reassembly, not NAT:
  * pico_ipv4.c:446-455); infeasible lengths, or a TCP / UDP transport shorter than its header
- * with a record, are V_MALFORMED and untouched (so is, in a batch over 2 GiB, a datagram more
- * than 1 GiB past the first datagram of its 64-datagram wave).  d_out_net / d_out_transport: the stored
+ * with a record, are V_MALFORMED and untouched.  d_out_net / d_out_transport: the stored
  * values (0 where none); any output pointer may be NULL.  One pass over each datagram: the
  * rewritten words enter the sums as deltas of the old ones (RFC 1624, on full sums). */
 #define PICO_CSUM_NAT_NONE     0u

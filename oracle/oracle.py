@@ -76,7 +76,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_ipv6_walk_frag.restype = ctypes.c_int
         L.oracle_ipv6_walk_frag.argtypes = [_vp, _u32, _vp, _vp, _vp]
         L.oracle_batch_ipv4_forward.restype = None
-        L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp]
+        L.oracle_batch_ipv4_forward.argtypes = [_vp, _vp, _u32, _vp, _u32, _vp, _vp]
         L.oracle_batch_ipv4_nat.restype = None
         L.oracle_batch_ipv4_nat.argtypes = [_vp, _vp, _u32, _vp, _vp, _vp, _vp]
         L.oracle_uniform_mt.restype = ctypes.c_double
@@ -205,11 +205,24 @@ def ipv6_walk_frag(dgram) -> tuple:
     return k, nl.value, pr.value, om.value
 
 
-def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray) -> np.ndarray:
-    """pico_ipv4_forward's TTL step, in place on `base` (a writable uint8 array); verdicts."""
+FWD_STATE_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("id", "<u2"), ("proto", "<u2"), ("reserved", "<u4")])
+
+
+def fwd_state() -> np.ndarray:
+    """A forwarding state at the reference's initial value (zeros)."""
+    return np.zeros(1, FWD_STATE_DTYPE)
+
+
+def batch_ipv4_forward(base: np.ndarray, desc: np.ndarray, local=(), state: np.ndarray | None = None) -> np.ndarray:
+    """pico_ipv4_pre_forward_checks in batch order, in place on `base` (a writable uint8 array);
+    `local` = the stack's link addresses as stored (uint32 little-endian views of the 4 bytes),
+    `state` (fwd_state(), updated) carries the last forwarded tuple between calls; verdicts."""
     desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    loc = np.ascontiguousarray(np.asarray(local, dtype=np.uint32))
+    st = fwd_state() if state is None else state
+    assert st.dtype == FWD_STATE_DTYPE and st.flags.c_contiguous
     v = np.zeros(desc.shape[0], np.uint8)
-    lib().oracle_batch_ipv4_forward(_p(base), _p(desc), desc.shape[0], _p(v))
+    lib().oracle_batch_ipv4_forward(_p(base), _p(desc), desc.shape[0], _p(loc), loc.size, _p(st), _p(v))
     return v
 
 

@@ -797,16 +797,25 @@ void oracle_ipv6_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
     oracle_reassemble(1, base, d, nd, grp, ng, out, od, out_len, out_l4, verdict, flags);
 }
 
-/* modules/pico_ipv4.c:1547-1556 (pico_ipv4_forward): hdr->ttl = (uint8_t)(hdr->ttl - 1);
- * if (hdr->ttl < 1) -> expired, dropped; else hdr->crc++ (uint16_t field, native LE
- * increment of the stored big-endian checksum).  In place on base; verdict per
- * datagram: ACCEPT (forwarded), EXPIRED, MALFORMED (< 20 bytes: untouched). */
-void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict)
+/* modules/pico_ipv4.c:1535-1574 (pico_ipv4_pre_forward_checks, called by pico_ipv4_forward :1600
+ * for a datagram whose destination has a route):
+ *   hdr->ttl = (uint8_t)(hdr->ttl - 1); if (hdr->ttl < 1) -> expired, dropped (crc untouched);
+ *   hdr->crc++ (uint16_t field, native LE increment of the stored big-endian checksum);
+ *   pico_ipv4_link_get(&hdr->src) -> a local source, dropped (:1559-1560);
+ *   (src, id, dst, proto) == the last tuple that reached this point -> dropped as a duplicate,
+ *   else it becomes the last tuple (:1562-1571; static state, zero at start).
+ * In place on base, in batch order; `st` carries the last tuple from one call to the next (the
+ * reference's statics; zero = its initial state).  Verdict per datagram: ACCEPT (forwarded),
+ * EXPIRED, LOCAL_SRC, DUPLICATE, MALFORMED (< 20 bytes: untouched, no state change). */
+void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const uint32_t *local,
+                               uint32_t n_local, struct oracle_fwd_state *st, uint8_t *verdict)
 {
-    uint32_t i;
+    uint32_t i, k;
     for (i = 0; i < n; i++) {
         uint8_t *h = base + d[i].off;
-        uint16_t crc;
+        uint16_t crc, id;
+        uint32_t src, dst;
+        int is_local = 0;
         if (d[i].len < 20) {
             verdict[i] = PICO_CSUM_V_MALFORMED;
             continue;
@@ -819,7 +828,22 @@ void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, ui
         memcpy(&crc, h + 10, 2);
         crc++;
         memcpy(h + 10, &crc, 2);
-        verdict[i] = PICO_CSUM_V_ACCEPT;
+        memcpy(&src, h + 12, 4);
+        memcpy(&dst, h + 16, 4);
+        memcpy(&id, h + 4, 2);
+        for (k = 0; k < n_local; k++)
+            is_local |= local[k] == src;
+        if (is_local) {
+            verdict[i] = PICO_CSUM_V_LOCAL_SRC;
+        } else if (st->src == src && st->id == id && st->dst == dst && st->proto == h[9]) {
+            verdict[i] = PICO_CSUM_V_DUPLICATE;
+        } else {
+            st->src = src;
+            st->dst = dst;
+            st->id = id;
+            st->proto = h[9];
+            verdict[i] = PICO_CSUM_V_ACCEPT;
+        }
     }
 }
 

@@ -18,6 +18,8 @@ struct pico_csum_desc {
 #define PICO_CSUM_V_L4_BAD    4u
 #define PICO_CSUM_V_MALFORMED 8u
 #define PICO_CSUM_V_EXPIRED  16u   /* forwarding batch */
+#define PICO_CSUM_V_LOCAL_SRC 32u  /* forwarding batch */
+#define PICO_CSUM_V_DUPLICATE 64u  /* forwarding batch */
 #define PICO_CSUM_V_FRAG     16u   /* RX / TX batches: a fragment (same bit, other batches) */
 #define PICO_CSUM_V_DROP_L2  32u
 #define PICO_CSUM_V_ARP      64u
@@ -69,7 +71,16 @@ void oracle_ipv4_reassemble(const uint8_t *base, const struct pico_csum_desc *d,
 void oracle_ipv6_reassemble(const uint8_t *base, const struct pico_csum_desc *d, uint32_t nd, const uint32_t *grp,
                             uint32_t ng, uint8_t *out, const struct pico_csum_desc *od, uint32_t *out_len, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t flags);
-void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, uint8_t *verdict);
+/* pico_ipv4_pre_forward_checks' static last tuple (modules/pico_ipv4.c:1537-1544), as stored */
+struct oracle_fwd_state {
+    uint32_t src;
+    uint32_t dst;
+    uint16_t id;
+    uint16_t proto;
+    uint32_t reserved;
+};
+void oracle_batch_ipv4_forward(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const uint32_t *local,
+                               uint32_t n_local, struct oracle_fwd_state *st, uint8_t *verdict);
 void oracle_batch_ipv4_nat(uint8_t *base, const struct pico_csum_desc *d, uint32_t n, const struct oracle_nat *rw,
                            uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict);
 double oracle_uniform_mt(oracle_checksum_fn fn, const uint8_t *base, uint64_t stride, uint32_t len,

@@ -40,6 +40,12 @@
  *   (net_len, transport_hdr, transport_len :392-405), NAT enabled on the link nat_addr (from the
  *   first call on; tuples persist: an inbound reply finds the outbound's tuple); the frame's
  *   bytes after the call are copied back.  Returns the function's result (0 translated).
+ * rr_forward(datagram, avail): pico_ipv4_pre_forward_checks (modules/pico_ipv4.c:1535-1574) on the
+ *   datagram with the stack's links as added by rr_ipv4_link (pico_ipv4_link_get's table); its
+ *   static last-forwarded state persists between calls (a fresh library copy starts at the
+ *   reference's zero state).  The bytes after the call are copied back.  Returns 0 forwarded,
+ *   1 TTL expired (:1549-1553), 2 local source (:1559-1560), 3 duplicate of the last forwarded
+ *   datagram (:1562-1565).
  * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py, make_ref_eth.py, make_ref_nat.py) only pass datagrams whose reference reads stay inside
  * avail and whose walk terminates (the oracle restatement decides which; the others are
  * restatement-only and documented so).
@@ -61,6 +67,7 @@
 
 int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
+int rr_ipv4_pre_forward_checks(struct pico_frame *f);
 int rr_ipv6_ext_headers(struct pico_frame *f);
 int rr_transport_crc_check(struct pico_frame *f);
 void rr_frag_reset(void);
@@ -80,6 +87,7 @@ int rr_init(void);
 int rr_ipv4_link(uint32_t addr);
 int rr_ipv4_rx(const uint8_t *d, uint32_t avail);
 int rr_nat(int dir, uint8_t *d, uint32_t avail, uint32_t nat_addr);
+int rr_forward(uint8_t *d, uint32_t avail);
 int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
 int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
              uint32_t cap, uint32_t *out_len, uint32_t *module, int *check);
@@ -390,4 +398,28 @@ int rr_nat(int dir, uint8_t *d, uint32_t avail, uint32_t nat_addr)
     memcpy(d, f->buffer, avail);
     pico_frame_discard(f);
     return r;
+}
+
+int rr_forward(uint8_t *d, uint32_t avail)
+{
+    struct pico_frame *f;
+    struct pico_ip4 src;
+    int r;
+    if (!g_dev || avail < 20)
+        return -2;
+    f = mk(d, avail);
+    if (!f)
+        return -2;
+    f->net_len = 20;
+    r = rr_ipv4_pre_forward_checks(f);
+    memcpy(d, f->buffer, avail);
+    pico_frame_discard(f);
+    if (r == 0)
+        return 0;
+    /* which discard: the TTL byte after the call is 0 only when it expired (crc untouched);
+     * else the source lookup (the same table the call consulted), else the duplicate rule */
+    if (d[8] == 0)
+        return 1;
+    memcpy(&src.addr, d + 12, 4);
+    return pico_ipv4_link_get(&src) ? 2 : 3;
 }

@@ -7,6 +7,9 @@
  * oracle/Makefile (`make refrx`) five times, once per REF_RX_UNIT:
  *   1: modules/pico_ipv4.c   rr_ipv4_process_in  = pico_ipv4_process_in   (:381-470)
  *                            rr_ipv4_crc_check   = pico_ipv4_crc_check    (:243-257)
+ *                            rr_ipv4_pre_forward_checks = pico_ipv4_pre_forward_checks (:1535-1574:
+ *                            TTL, crc++, local source, the duplicate of the last forwarded datagram;
+ *                            its static state lives in this library copy)
  *   2: modules/pico_ipv6.c   rr_ipv6_ext_headers = pico_ipv6_extension_headers (:707-809)
  *   3: stack/pico_socket.c   rr_transport_crc_check = pico_transport_crc_check (:1916-1968)
  *   4: modules/pico_fragments.c  rr_frag_reset: empties the two reassembly trees and forgets the
@@ -22,6 +25,8 @@ int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
 int rr_ipv4_process_in(struct pico_frame *f) { return pico_ipv4_process_in(&pico_proto_ipv4, f); }
 int rr_ipv4_crc_check(struct pico_frame *f) { return pico_ipv4_crc_check(f); }
+int rr_ipv4_pre_forward_checks(struct pico_frame *f);
+int rr_ipv4_pre_forward_checks(struct pico_frame *f) { return pico_ipv4_pre_forward_checks(f); }
 #elif REF_RX_UNIT == 2
 #include "pico_ipv6.c"
 int rr_ipv6_ext_headers(struct pico_frame *f);

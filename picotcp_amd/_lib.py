@@ -48,12 +48,13 @@ EXPORTED = (
 
 F_WRITE = 0x1
 F_TX = 0x2
-F_NXTHDR_DISPATCH = 0x4   # IPv6 RX: TCP / UDP by next header, not the reference's byte 9 (include/pico_csum.h)
+F_NXTHDR_DISPATCH = 0x8   # IPv6 RX: TCP / UDP by next header, not the reference's byte 9 (include/pico_csum.h)
 V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
 V_FRAG = 16                # RX / TX batches (V_EXPIRED: the forwarding batch)
-ABI_VERSION = 2
+ABI_VERSION = 3
 V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
 V_UNTOUCHED = 32            # NAT batch (same bit as V_DROP_L2)
+V_LOCAL_SRC, V_DUPLICATE = 32, 64   # forwarding batch (same bits as V_DROP_L2 / V_ARP)
 EINVAL, ENODEV, EIO, ENOMEM = 22, 19, 5, 12
 
 
@@ -95,7 +96,7 @@ def load() -> ctypes.CDLL:
     sig("pico_ipv4_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp)
     sig("pico_ipv6_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp)
     sig("pico_eth_checksum_batch_dev", ctypes.c_int, vp, u64, vp, u32, u32, vp, vp, vp, vp, vp)
-    sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp)
+    sig("pico_ipv4_forward_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, vp, vp)
     sig("pico_ipv4_nat_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, vp, vp, vp, vp)
     sig("pico_ipv4_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, vp)
     sig("pico_ipv6_reassemble_batch_dev", ctypes.c_int, vp, u64, vp, u32, vp, u32, vp, u64, vp, vp, vp, vp, u32, vp)

@@ -25,8 +25,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (F_NXTHDR_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_EXPIRED, V_FRAG,  # noqa: F401
-                   V_IPV6, V_L4_BAD, V_MALFORMED, V_NET_BAD, V_UNTOUCHED)
+from ._lib import (F_NXTHDR_DISPATCH, F_TX, F_WRITE, V_ACCEPT, V_ARP, V_DROP_L2, V_DUPLICATE,  # noqa: F401
+                   V_EXPIRED, V_FRAG, V_IPV6, V_L4_BAD, V_LOCAL_SRC, V_MALFORMED, V_NET_BAD, V_UNTOUCHED)
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("seed", "<u4")])
 # struct pico_csum_nat (include/pico_csum.h): the NAT batch's per-datagram record
@@ -199,21 +199,40 @@ def eth_checksum_batch(base: torch.Tensor, desc: torch.Tensor, n: int, flags: in
     return out_net, out_l4, verdict
 
 
-def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, verdict: torch.Tensor | None = None,
-                       stream=None) -> torch.Tensor:
-    """pico_ipv4_forward's TTL step (pico_ipv4.c:1547-1556) in place on n datagrams:
-    ttl - 1, then the reference's crc++ unless the TTL expired.  Returns the verdicts
-    (V_ACCEPT = forwarded, V_EXPIRED, V_MALFORMED)."""
+FWD_STATE_BYTES = 16          # struct pico_csum_fwd_state
+
+
+def fwd_state(device) -> torch.Tensor:
+    """A forwarding state (struct pico_csum_fwd_state) at the reference's initial value (zeros)."""
+    return torch.zeros(FWD_STATE_BYTES, dtype=torch.uint8, device=device)
+
+
+def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, local=(), state: torch.Tensor | None = None,
+                       verdict: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """pico_ipv4_pre_forward_checks (pico_ipv4.c:1535-1574) in batch order, in place on n datagrams:
+    ttl - 1, then unless the TTL expired the reference's crc++, the local-source check against
+    `local` (the host's link addresses as stored: uint32 little-endian views, <= 32) and the
+    duplicate check against the last forwarded tuple, carried in `state` (fwd_state(); None = a
+    zero state not kept).  Returns the verdicts (V_ACCEPT = forwarded, V_EXPIRED, V_LOCAL_SRC,
+    V_DUPLICATE, V_MALFORMED)."""
     _require_device(base, "base")
+    _require_u8(base, "base")
     _require_device(desc, "desc")
     if desc.numel() < 16 * n:
         raise ValueError("descriptor tensor shorter than n entries")
     if verdict is None:
         verdict = torch.empty(n, dtype=torch.uint8, device=base.device)
     _check_out(verdict, n, "verdict", base.device, 1)
+    if state is not None:
+        _require_device(state, "state")
+        if state.numel() * state.element_size() < FWD_STATE_BYTES or not state.is_contiguous():
+            raise ValueError("state must be a contiguous 16-byte tensor (fwd_state())")
+    loc = np.ascontiguousarray(np.asarray(local, dtype=np.uint32))
     lib = _lib.load()
     _lib.check("pico_ipv4_forward_batch_dev",
-               lib.pico_ipv4_forward_batch_dev(_ptr(base), base.numel(), _ptr(desc), n, _ptr(verdict),
+               lib.pico_ipv4_forward_batch_dev(_ptr(base), base.numel(), _ptr(desc), n,
+                                               loc.ctypes.data if loc.size else None, loc.size,
+                                               _ptr(state) if state is not None else None, _ptr(verdict),
                                                _stream_handle(stream)))
     return verdict
 
@@ -224,6 +243,7 @@ def ipv4_nat_batch(base: torch.Tensor, desc: torch.Tensor, n: int, nat: torch.Te
     (NAT_DTYPE layout).  Returns (out_net int16[n], out_transport int16[n], verdict uint8[n]):
     V_ACCEPT translated, V_UNTOUCHED, V_FRAG, V_MALFORMED."""
     _require_device(base, "base")
+    _require_u8(base, "base")
     _require_device(desc, "desc")
     _require_device(nat, "nat")
     if desc.numel() < 16 * n:

@@ -36,8 +36,8 @@ int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t st
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
-int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, uint8_t *verdict,
-                                  void *stream);
+int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
+                                  uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
                                 const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len, const void *out_desc,
                                 uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict, uint32_t flags, void *stream);
@@ -56,6 +56,13 @@ static int fail(int code, const char *fmt, ...)
 }
 
 const char *pico_csum_last_error(void) { return g_err; }
+
+/* ABI 1's F_REF_DISPATCH (0x4) meant the opposite of today's F_NXTHDR_DISPATCH (0x8): refused */
+static const char *retired_note(uint32_t flags)
+{
+    return (flags & PICO_CSUM_F_RETIRED_0x4) ? " (0x4 is the retired ABI-1 dispatch bit; ABI 3: F_NXTHDR_DISPATCH = 0x8)"
+                                             : "";
+}
 int pico_csum_abi_version(void) { return PICO_CSUM_ABI_VERSION; }
 
 /* ------------------------------------------------------------------ layer 1 */
@@ -387,7 +394,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
     if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_NXTHDR_DISPATCH))
-        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x%s", flags, retired_note(flags));
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((flags & PICO_CSUM_F_NXTHDR_DISPATCH) && (flags & PICO_CSUM_F_TX))
@@ -413,7 +420,7 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
     if (flags & ~(PICO_CSUM_F_WRITE | PICO_CSUM_F_TX | PICO_CSUM_F_NXTHDR_DISPATCH))
-        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x%s", flags, retired_note(flags));
     if ((flags & PICO_CSUM_F_WRITE) && !(flags & PICO_CSUM_F_TX))
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((flags & PICO_CSUM_F_NXTHDR_DISPATCH) && (flags & PICO_CSUM_F_TX))
@@ -431,18 +438,24 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
 }
 
 int pico_ipv4_forward_batch_dev(void *d_base, uint64_t base_len, const struct pico_csum_desc *d_desc, uint32_t n,
+                                const uint32_t *local_addrs, uint32_t n_local, struct pico_csum_fwd_state *d_state,
                                 uint8_t *d_verdict, void *stream)
 {
     int rc;
     if (n == 0)
         return 0;
-    if (!d_base || !d_desc)
-        return fail(PICO_CSUM_EINVAL, "NULL buffer");
+    if (!d_base || !d_desc || !d_verdict)
+        return fail(PICO_CSUM_EINVAL, "NULL buffer (d_verdict is required)");
     if (((uintptr_t)d_desc & 15u) != 0)
         return fail(PICO_CSUM_EINVAL, "descriptor array must be 16-byte aligned");
+    if (((uintptr_t)d_state & 3u) != 0)
+        return fail(PICO_CSUM_EINVAL, "d_state must be 4-byte aligned");
+    if (n_local > 32 || (n_local && !local_addrs))
+        return fail(PICO_CSUM_EINVAL, "local_addrs: at most 32 host addresses");
     if ((rc = need_device()) != 0)
         return rc;
-    return launch_status(pico_csum_launch_ipv4_forward(d_base, base_len, d_desc, n, d_verdict, stream),
+    return launch_status(pico_csum_launch_ipv4_forward(d_base, base_len, d_desc, n, local_addrs, n_local,
+                                                       (uint32_t *)d_state, d_verdict, stream),
                          "pico_ipv4_forward_batch_dev");
 }
 
@@ -461,7 +474,7 @@ static int reassemble_dev(int v6, const void *d_base, uint64_t base_len, const s
     if (((uintptr_t)d_groups & 3u) != 0 || ((uintptr_t)d_out & 3u) != 0)
         return fail(PICO_CSUM_EINVAL, "d_groups and d_out must be 4-byte aligned");
     if (flags & ~(v6 ? PICO_CSUM_F_NXTHDR_DISPATCH : 0u))
-        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x", flags);
+        return fail(PICO_CSUM_EINVAL, "unknown flags 0x%x%s", flags, retired_note(flags));
     if ((rc = need_device()) != 0)
         return rc;
     return launch_status(pico_csum_launch_reassemble(v6, d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out,

@@ -244,7 +244,7 @@ constexpr uint32_t F_NAT = 0x20000u;    // kernel flag (pico_ipv4_nat_batch_dev)
 constexpr uint32_t V_UNTOUCHED = 32u;   // NAT batch: left as it is (include/pico_csum.h)
 // NAT state of a frame (IPv4 mode, F_NAT), in the l2v byte of the phase-4 state
 constexpr uint32_t NS_XLATE = 1u, NS_HDR = 2u, NS_SKIP = 4u, NS_BAD = 8u;
-constexpr uint32_t F_NXD = 0x4u;        // PICO_CSUM_F_NXTHDR_DISPATCH (IPv6 RX)
+constexpr uint32_t F_NXD = 0x8u;        // PICO_CSUM_F_NXTHDR_DISPATCH (IPv6 RX)
 // phase-1 outcomes applied after the IPv4 header check (sorted kernel)
 constexpr uint32_t PV_DROP = 1u, PV_FRAG = 2u;
 

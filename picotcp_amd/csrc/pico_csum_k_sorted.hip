@@ -529,16 +529,25 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                     const uint32_t dir = (rw.y >> 16) & 0xFFu;
                     l2v = NS_SKIP;
                     if (parsed && post == 0u && (dir == 1u || dir == 2u)) {
-                        if ((proto == 6u || proto == 17u) && !(l4_needed && staged)) {
-                            l2v = NS_BAD;                            // transport too short (or > 2 GiB batch)
+                        if ((proto == 6u || proto == 17u) && !l4_needed) {
+                            l2v = NS_BAD;                            // transport shorter than its header
                         } else if (proto == 6u || proto == 17u) {
                             uint32_t H[5];
                             window_words<5, false>(hw, r, H);
                             const uint32_t old = dir == 1u ? H[3] : H[4];
                             const uint32_t da = (rw.x & 0xFFFFu) + (rw.x >> 16) - (old & 0xFFFFu) - (old >> 16);
-                            const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
-                            const uint32_t sw = (lane & (HW - 1)) << 4, pb = r + hl + (dir == 1u ? 0u : 2u);
-                            const uint32_t op = (uint32_t)row[pb ^ sw] | ((uint32_t)row[(pb + 1u) ^ sw] << 8);
+                            // the old port: from the LDS stage, or -- a frame outside the wave's window
+                            // (staged false: outside the wave's <= 2 GiB window around its first frame) -- from memory
+                            const uint32_t pb = r + hl + (dir == 1u ? 0u : 2u);
+                            uint32_t op;
+                            if (staged) {
+                                const uint8_t* row = reinterpret_cast<const uint8_t*>(stage + lane * HW);
+                                const uint32_t sw = (lane & (HW - 1)) << 4;
+                                op = (uint32_t)row[pb ^ sw] | ((uint32_t)row[(pb + 1u) ^ sw] << 8);
+                            } else {
+                                const uint8_t* q = fp + (pb - r);
+                                op = (uint32_t)q[0] | ((uint32_t)q[1] << 8);
+                            }
                             hdr20 += da;
                             pseudo += da;
                             p_all = da + (rw.y & 0xFFFFu) - op;     // the region's share of both words
@@ -1220,22 +1229,49 @@ __global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(Fl
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- IPv4 forwarding step
 //
-// pico_ipv4_forward (modules/pico_ipv4.c:1547-1556) on a batch of datagrams that are
-// routed through this host: hdr->ttl = ttl - 1 (written back whatever follows);
-// ttl < 1 -> expired (pico_notify_ttl_expired, the frame is dropped, crc untouched);
-// else hdr->crc++ -- the reference's "HACK: increase crc to compensate decreased
-// TTL": a native (little-endian) uint16 increment of the stored big-endian field.
-// That is the incremental update of RFC 1141 (+0x0100 on the checksum for -1 on the
-// TTL byte) except where it carries out of the first byte, and it is kept exactly
-// so, bit-compatible with the reference.  One lane per datagram; the 4 bytes at
-// header offset 8..11 (ttl, proto, crc) are read and written, nothing else.
+// pico_ipv4_pre_forward_checks (modules/pico_ipv4.c:1535-1574, called by pico_ipv4_forward :1600)
+// on a batch of datagrams routed through this host, in batch order:
+//   hdr->ttl = ttl - 1 (written back whatever follows); ttl < 1 -> expired (dropped, crc untouched);
+//   else hdr->crc++ -- the reference's "HACK: increase crc to compensate decreased TTL": a native
+//   (little-endian) uint16 increment of the stored big-endian field (RFC 1141's +0x0100 except where
+//   it carries out of the first byte; kept exactly so, bit-compatible);
+//   a source that is one of the host's link addresses -> dropped;
+//   (src, id, dst, proto) equal to the last datagram that got this far -> dropped as a duplicate,
+//   else it becomes the last one (static state in the reference; here a device struct carried from
+//   one batch to the next).
+// "The last datagram that got this far" is the nearest earlier datagram of the batch that passed the
+// TTL and source checks (a duplicate leaves the state as it was: it equals it), or the carried state.
+// Three launches on one stream:
+//   K5a  one lane per datagram: TTL, crc++, local source -> verdict ACCEPT / EXPIRED / LOCAL_SRC.
+//   K5b  one lane per datagram: the nearest earlier ACCEPT datagram (a wave ballot, then the
+//        workgroup's wave maxima in LDS, then -- for the workgroup's first one only -- a backward
+//        scan over the earlier verdict bytes, 256 a step), its tuple compared with this one's:
+//        DUPLICATE.  Bytes another workgroup turns from ACCEPT to DUPLICATE meanwhile count the
+//        same (both reached the check).
+//   K5c  one workgroup: the batch's last such datagram's tuple -> the carried state.
 struct FwdArgs {
     uint8_t* base;
     uint64_t base_len;
     const pico_csum_desc_dev* desc;
     uint32_t n;
+    uint32_t n_local;
     uint8_t* verdict;
+    uint32_t* state;          // {src, dst, id | proto << 16, reserved} as stored; NULL: zeros, not kept
+    uint32_t local[32];       // the host's link addresses as stored (pico_ipv4_link_get's table)
 };
+constexpr uint32_t V_LOCAL_SRC = 32u, V_DUPLICATE = 64u;   // forwarding batch (include/pico_csum.h)
+
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// (src, dst, id | proto << 16) of datagram j, as stored
+__device__ __forceinline__ uint3 fwd_tuple(const FwdArgs& p, uint32_t j) {
+    const uint4 d = *reinterpret_cast<const uint4*>(p.desc + j);
+    const uint8_t* h = p.base + (((uint64_t)d.y << 32) | d.x);
+    return make_uint3(ld_le32(h + 12), ld_le32(h + 16),
+                      ((uint32_t)h[4] | ((uint32_t)h[5] << 8)) | ((uint32_t)h[9] << 16));
+}
 
 __global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1254,12 +1290,92 @@ __global__ __launch_bounds__(256) void ipv4_forward_kernel(FwdArgs p) {
             const uint32_t inc = (crc + 1u) & 0xFFFFu;
             h[10] = (uint8_t)inc;
             h[11] = (uint8_t)(inc >> 8);
-            v = V_ACCEPT;
+            const uint32_t src = ld_le32(h + 12);
+            bool local = false;
+            for (uint32_t k = 0; k < p.n_local; ++k) local |= p.local[k] == src;
+            v = local ? V_LOCAL_SRC : V_ACCEPT;
         }
     }
-    if (p.verdict) p.verdict[i] = (uint8_t)v;
+    p.verdict[i] = (uint8_t)v;
 }
 
+__device__ __forceinline__ bool fwd_reached(uint32_t v) { return v == V_ACCEPT || v == V_DUPLICATE; }
+
+// The highest index < below (a multiple of 256) whose verdict byte says "reached the duplicate
+// check", or -1: the whole workgroup scans backwards 256 bytes a step.
+__device__ __forceinline__ int64_t fwd_scan_back(const FwdArgs& p, uint64_t below, int* wmax) {
+    const uint32_t t = threadIdx.x, w = t >> 6;
+    for (uint64_t top = below; top != 0; top -= 256u) {
+        const uint64_t j = top - 256u + t;
+        const bool e = fwd_reached(p.verdict[j]);
+        const uint64_t b = __builtin_amdgcn_ballot_w64(e);
+        __syncthreads();
+        if ((t & 63u) == 0) wmax[w] = b ? 63 - __builtin_clzll(b) + 64 * (int)w : -1;
+        __syncthreads();
+        const int m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m >= 0) return (int64_t)(top - 256u) + m;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void ipv4_forward_dup_kernel(FwdArgs p) {
+    __shared__ int wlast[4], wmax[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t blk0 = (uint64_t)blockIdx.x * 256u, i = blk0 + t;
+    const bool elig = i < p.n && p.verdict[i] == V_ACCEPT;   // this launch writes DUPLICATE only after the reads below
+    const uint64_t b = __builtin_amdgcn_ballot_w64(elig);
+    if (lane == 0) wlast[w] = b ? 63 - __builtin_clzll(b) : -1;
+    __syncthreads();
+    // nearest earlier eligible in the workgroup
+    int64_t prev = -1;
+    const uint64_t below = b & ((1ull << lane) - 1ull);
+    if (below) {
+        prev = (int64_t)(blk0 + 64u * w + 63u - __builtin_clzll(below));
+    } else {
+        for (int k = (int)w - 1; k >= 0; --k)
+            if (wlast[k] >= 0) { prev = (int64_t)(blk0 + 64u * k + wlast[k]); break; }
+    }
+    // the workgroup's first eligible datagram looks further back (workgroup-uniform condition)
+    const bool any = wlast[0] >= 0 || wlast[1] >= 0 || wlast[2] >= 0 || wlast[3] >= 0;
+    int64_t back = -1;
+    if (any && blk0 != 0) back = fwd_scan_back(p, blk0, wmax);
+    if (!elig) return;
+    if (prev < 0) prev = back;
+    uint3 last;
+    if (prev >= 0) {
+        last = fwd_tuple(p, (uint32_t)prev);
+    } else if (p.state) {
+        last = make_uint3(p.state[0], p.state[1], p.state[2] & 0x00FFFFFFu);
+    } else {
+        last = make_uint3(0u, 0u, 0u);
+    }
+    const uint3 mine = fwd_tuple(p, (uint32_t)i);
+    if (mine.x == last.x && mine.y == last.y && mine.z == last.z) p.verdict[i] = (uint8_t)V_DUPLICATE;
+}
+
+__global__ __launch_bounds__(256) void ipv4_forward_state_kernel(FwdArgs p) {
+    __shared__ int wmax[4];
+    const uint64_t top = ((uint64_t)p.n + 255u) & ~(uint64_t)255u;
+    // verdict bytes past n are not ours: scan [top - 256, n) first with them masked
+    const uint32_t t = threadIdx.x, w = t >> 6;
+    int64_t last = -1;
+    {
+        const uint64_t j = top - 256u + t;
+        const bool e = j < p.n && fwd_reached(p.verdict[j]);
+        const uint64_t b = __builtin_amdgcn_ballot_w64(e);
+        if ((t & 63u) == 0) wmax[w] = b ? 63 - __builtin_clzll(b) + 64 * (int)w : -1;
+        __syncthreads();
+        const int m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m >= 0) last = (int64_t)(top - 256u) + m;
+    }
+    if (last < 0 && top > 256u) last = fwd_scan_back(p, top - 256u, wmax);
+    if (last >= 0 && t == 0) {
+        const uint3 tu = fwd_tuple(p, (uint32_t)last);
+        p.state[0] = tu.x;
+        p.state[1] = tu.y;
+        p.state[2] = tu.z;
+    }
+}
 
 #endif
 
@@ -1323,12 +1439,18 @@ int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uin
     }
 }
 
-int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, uint8_t* verdict,
-                                  void* stream) {
+int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, const uint32_t* local,
+                                  uint32_t n_local, uint32_t* state, uint8_t* verdict, void* stream) {
     if (n == 0) return (int)hipSuccess;
-    FwdArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, verdict};
+    if (n_local > 32 || !verdict) return (int)hipErrorInvalidValue;
+    FwdArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, n_local, verdict,
+              state, {}};
+    for (uint32_t k = 0; k < n_local; ++k) a.local[k] = local[k];
+    const hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)(((uint64_t)n + 255u) / 256u)), block(256);
-    hipLaunchKernelGGL(ipv4_forward_kernel, grid, block, 0, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(ipv4_forward_kernel, grid, block, 0, s, a);
+    hipLaunchKernelGGL(ipv4_forward_dup_kernel, grid, block, 0, s, a);
+    if (state) hipLaunchKernelGGL(ipv4_forward_state_kernel, dim3(1), block, 0, s, a);
     return (int)hipGetLastError();
 }
 #endif  // SORTED_MODE == 0

@@ -50,10 +50,11 @@ def test_reference_symbol_signatures_are_drop_in():
 
 
 def test_abi_version():
-    assert _lib.load().pico_csum_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.load().pico_csum_abi_version() == _lib.ABI_VERSION == 3
     src = open(HEADER).read()
-    assert re.search(r"#define PICO_CSUM_ABI_VERSION 2\b", src)
-    for name, val in (("F_NXTHDR_DISPATCH", 4), ("V_FRAG", 16), ("V_EXPIRED", 16), ("V_MALFORMED", 8)):
+    assert re.search(r"#define PICO_CSUM_ABI_VERSION 3\b", src)
+    for name, val in (("F_NXTHDR_DISPATCH", 8), ("V_FRAG", 16), ("V_EXPIRED", 16), ("V_MALFORMED", 8),
+                      ("V_LOCAL_SRC", 32), ("V_DUPLICATE", 64)):
         m = re.search(rf"#define PICO_CSUM_{name}\s+(0x[0-9a-fA-F]+|[0-9]+)u", src)
         assert m and int(m.group(1), 0) == val, name
         assert getattr(_lib, name) == val
@@ -96,9 +97,26 @@ def test_argument_validation():
                                            None, None, None, None, None) == -_lib.EINVAL
     assert lib.pico_ipv4_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, _lib.F_NXTHDR_DISPATCH, None, None,
                                             None, None) == -_lib.EINVAL
+    # ABI 1's dispatch bit 0x4 (the opposite meaning) is refused, never silently reinterpreted
+    assert lib.pico_ipv6_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, 0x4, None, None, None) \
+        == -_lib.EINVAL
+    assert "retired" in lib.pico_csum_last_error().decode()
+    assert lib.pico_eth_checksum_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, 0x4, None, None, None, None,
+                                           None) == -_lib.EINVAL
+    # forwarding: the verdict array is required, at most 32 host addresses, an aligned state
+    loc = (ctypes.c_uint32 * 33)()
+    assert lib.pico_ipv4_forward_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, None, 0, None, None, None) \
+        == -_lib.EINVAL
+    assert lib.pico_ipv4_forward_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, loc, 33, None, vp(0x3000), None) \
+        == -_lib.EINVAL
+    assert lib.pico_ipv4_forward_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, None, 1, None, vp(0x3000), None) \
+        == -_lib.EINVAL
+    assert lib.pico_ipv4_forward_batch_dev(vp(0x1000), 1 << 20, vp(0x2000), 4, loc, 2, vp(0x4002), vp(0x3000),
+                                           None) == -_lib.EINVAL
     # reassembly: flags (IPv6: F_NXTHDR_DISPATCH only), alignment, NULL buffers
     ra = (vp(0x1000), 1 << 20, vp(0x2000), 4, vp(0x3000), 2, vp(0x4000), 1 << 20, vp(0x5000), None, None, None)
     assert lib.pico_ipv6_reassemble_batch_dev(*ra, _lib.F_TX, None) == -_lib.EINVAL
+    assert lib.pico_ipv6_reassemble_batch_dev(*ra, 0x4, None) == -_lib.EINVAL
     assert lib.pico_ipv6_reassemble_batch_dev(*ra[:6], vp(0x4002), *ra[7:], 0, None) == -_lib.EINVAL
     assert lib.pico_ipv4_reassemble_batch_dev(*ra[:8], vp(0x5008), None, None, None, None) == -_lib.EINVAL
     assert lib.pico_ipv4_reassemble_batch_dev(None, *ra[1:], None) == -_lib.EINVAL

@@ -1,23 +1,40 @@
-"""IPv4 forwarding step (the ad-hoc incremental update of
-modules/pico_ipv4.c:1547-1556): ttl - 1 in place, expired at 0, else the reference's
-`hdr->crc++` (a native little-endian increment of the stored big-endian field).
+"""IPv4 forwarding step: pico_ipv4_pre_forward_checks
+(modules/pico_ipv4.c:1535-1574), in batch order -- ttl - 1 in place, expired at 0, else the
+reference's `hdr->crc++` (a native little-endian increment of the stored big-endian field), the
+local-source discard (:1559) and the duplicate-of-the-last-forwarded discard (:1562-1571, static
+state carried from batch to batch).
 
-Parity unpinned: pico_ipv4_forward is static in pico_ipv4.c, which needs the whole
-stack, and the reference has no test or fixture for it; the oracle restates the three
-lines and is checked here against a second, independent restatement."""
+Pinned: tests/golden/ref_fwd_cases.npz (tests/golden/make_ref_fwd.py) is a 6000-datagram sequence
+run through the reference's own static function, compiled unmodified in oracle/_ref/libref_rx.so
+and reached through oracle/ref_rx_wrap.c unit 1, from its initial (zero) state.  The oracle and
+the kernels reproduce its bytes and verdicts, in one batch and split into batches whose state is
+carried.  When libref_rx.so is present, a fresh sequence is also re-run through the reference live.
+Datagrams shorter than 20 bytes never reach the function (restatement only)."""
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import pytest
 
 from oracle import oracle as O
 from picotcp_amd import batch, synth
+from tests import golden_data as G
+from tests.golden import make_ref_fwd as M
 
-V_ACCEPT, V_MALFORMED, V_EXPIRED = 1, 8, 16
+V_ACCEPT, V_MALFORMED, V_EXPIRED, V_LOCAL_SRC, V_DUPLICATE = 1, 8, 16, 32, 64
+
+
+def cases():
+    z = np.load(os.path.join(G.GOLDEN, "ref_fwd_cases.npz"))
+    c = {k: z[k] for k in z.files}
+    c["desc"] = batch.make_desc(c["off"], c["avail"])
+    return c
 
 
 def headers(n: int, seed: int):
-    """n IPv4 headers packed with 0..3 byte gaps (odd alignments), edge TTL / crc values."""
+    """n IPv4 headers packed with 0..3 byte gaps (odd alignments), edge TTL / crc values, tuples
+    drawn from small pools (duplicates back to back and interleaved), some local sources."""
     rng = np.random.default_rng(seed)
     lens = rng.integers(20, 90, n).astype(np.uint32)
     lens[:5] = [19, 0, 20, 20, 21]                    # too short, empty, minimal
@@ -26,20 +43,37 @@ def headers(n: int, seed: int):
     off[1:] = np.cumsum(lens.astype(np.uint64) + gaps)[:-1]
     buf = synth.random_bytes(seed, int(off[-1]) + int(lens[-1]) + 8)
     o = off.astype(np.int64)
+    ok = lens >= 20
     ttl = rng.integers(0, 256, n)
     ttl[5:13] = [0, 1, 2, 255, 1, 0, 128, 2]
-    buf[o + 8] = ttl.astype(np.uint8)
+    buf[o[ok] + 8] = ttl[ok].astype(np.uint8)
     crc = rng.integers(0, 1 << 16, n)
     crc[13:19] = [0xFFFF, 0x00FF, 0xFF00, 0, 0xFEFF, 0x0100]
-    buf[o + 10] = (crc >> 8).astype(np.uint8)         # stored big-endian (short_be)
-    buf[o + 11] = (crc & 0xFF).astype(np.uint8)
-    return buf, batch.make_desc(off, lens)
+    buf[o[ok] + 10] = (crc[ok] >> 8).astype(np.uint8)    # stored big-endian (short_be)
+    buf[o[ok] + 11] = (crc[ok] & 0xFF).astype(np.uint8)
+    pool = rng.integers(0, 1 << 32, (8, 3), dtype=np.uint64).astype(np.uint32)
+    pick = rng.integers(0, 8, n)
+    run = rng.random(n) < 0.3                         # repeat the previous row's tuple
+    for i in range(1, n):
+        if run[i]:
+            pick[i] = pick[i - 1]
+    for k, sh in ((12, 0), (16, 1)):
+        v = pool[pick, sh]
+        for b in range(4):
+            buf[o[ok] + k + b] = ((v[ok] >> (8 * b)) & 0xFF).astype(np.uint8)
+    idp = pool[pick, 2]
+    buf[o[ok] + 4], buf[o[ok] + 5] = (idp[ok] & 0xFF).astype(np.uint8), ((idp[ok] >> 8) & 0xFF).astype(np.uint8)
+    buf[o[ok] + 9] = ((idp[ok] >> 16) % 3).astype(np.uint8) * 5 + 1
+    local = pool[:2, 0].copy()                        # two of the pool's sources are the host's
+    return buf, batch.make_desc(off, lens), local
 
 
-def restated(buf: np.ndarray, desc: np.ndarray):
-    """Independent restatement of pico_ipv4.c:1547-1556 (Python ints)."""
+def restated(buf: np.ndarray, desc: np.ndarray, local, state=(0, 0, 0, 0)):
+    """Independent restatement of pico_ipv4.c:1535-1574 (Python ints), in order."""
     out = buf.copy()
     v = np.zeros(desc.size, np.uint8)
+    last = tuple(state)
+    loc = {int(x) for x in local}
     for i, (off, ln, _) in enumerate(desc.tolist()):
         if ln < 20:
             v[i] = V_MALFORMED
@@ -52,18 +86,71 @@ def restated(buf: np.ndarray, desc: np.ndarray):
         c = (int(out[off + 10]) | int(out[off + 11]) << 8) + 1   # hdr->crc++ on a LE host
         out[off + 10] = c & 0xFF
         out[off + 11] = (c >> 8) & 0xFF
-        v[i] = V_ACCEPT
+        src = int.from_bytes(bytes(out[off + 12:off + 16]), "little")
+        tup = (src, int.from_bytes(bytes(out[off + 16:off + 20]), "little"),
+               int(out[off + 4]) | int(out[off + 5]) << 8, int(out[off + 9]))
+        if src in loc:
+            v[i] = V_LOCAL_SRC
+        elif tup == last:
+            v[i] = V_DUPLICATE
+        else:
+            last = tup
+            v[i] = V_ACCEPT
     return out, v
 
 
-def test_oracle_forward_matches_restatement():
-    buf, desc = headers(3000, 7)
-    want_buf, want_v = restated(buf, desc)
+def test_oracle_matches_reference_fixture():
+    c = cases()
+    got = c["buf"].copy()
+    v = O.batch_ipv4_forward(got, c["desc"], c["local"])
+    np.testing.assert_array_equal(v, c["verdict"])
+    np.testing.assert_array_equal(got, c["want"])
+    assert set(np.unique(v).tolist()) == {V_ACCEPT, V_MALFORMED, V_EXPIRED, V_LOCAL_SRC, V_DUPLICATE}
+    assert c["verdict"][0] == V_DUPLICATE             # the all-zero tuple vs the initial state
+    # split into batches, the state carried
+    for step in (1, 13, 256, 777):
+        got = c["buf"].copy()
+        st = O.fwd_state()
+        vs = [O.batch_ipv4_forward(got, c["desc"][s:s + step], c["local"], st) for s in range(0, c["desc"].size, step)]
+        np.testing.assert_array_equal(np.concatenate(vs), c["verdict"])
+        np.testing.assert_array_equal(got, c["want"])
+
+
+def test_oracle_matches_restatement():
+    buf, desc, local = headers(3000, 7)
+    want_buf, want_v = restated(buf, desc, local)
     got = buf.copy()
-    v = O.batch_ipv4_forward(got, desc)
+    v = O.batch_ipv4_forward(got, desc, local)
     np.testing.assert_array_equal(v, want_v)
     np.testing.assert_array_equal(got, want_buf)
     assert (want_v == V_EXPIRED).sum() > 0 and (want_v == V_MALFORMED).sum() == 2
+    assert (want_v == V_DUPLICATE).sum() > 100 and (want_v == V_LOCAL_SRC).sum() > 100
+
+
+@pytest.mark.skipif(not os.path.exists(M.REF_RX), reason="oracle/_ref/libref_rx.so not built (make -C oracle refrx)")
+def test_reference_rerun_live():
+    """A fresh sequence through the reference now (a private library copy: its own zero state)."""
+    R = M.ref_lib()
+    buf, desc, _ = headers(1500, 23)
+    local = np.array([int.from_bytes(a, "little") for a in M.LOCAL], np.uint32)
+    o = desc["off"].astype(np.int64)
+    ok = desc["len"] >= 20
+    for k, a in zip(range(0, 1500, 37), M.LOCAL * 100):   # some of the reference's link addresses as sources
+        if ok[k]:
+            buf[o[k] + 12:o[k] + 16] = list(a)
+    want = buf.copy()
+    wv = np.zeros(desc.size, np.uint8)
+    for i in range(desc.size):
+        if not ok[i]:
+            wv[i] = V_MALFORMED
+            continue
+        d = np.ascontiguousarray(want[o[i]:o[i] + int(desc["len"][i])])
+        wv[i] = M.RET_VERDICT[R.rr_forward(d.ctypes.data, d.size)]
+        want[o[i]:o[i] + d.size] = d
+    got = buf.copy()
+    v = O.batch_ipv4_forward(got, desc, local)
+    np.testing.assert_array_equal(v, wv)
+    np.testing.assert_array_equal(got, want)
 
 
 def test_forward_keeps_valid_headers_valid():
@@ -79,23 +166,84 @@ def test_forward_keeps_valid_headers_valid():
         c = O.checksum(h)
         buf[o + 10], buf[o + 11] = c >> 8, c & 0xFF
     v = O.batch_ipv4_forward(buf, desc)
-    assert (v == V_ACCEPT).all()                       # ttl 64 -> 63
+    assert ((v == V_ACCEPT) | (v == V_DUPLICATE)).all()   # ttl 64 -> 63
     for o in net.astype(np.int64):
         assert O.checksum(buf[o:o + 20]) == 0
 
 
+# ---------------------------------------------------------------- GPU
+
+def _gpu_run(buf, desc, local, steps, dev="cuda:0"):
+    import torch
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_desc = batch.desc_to_device(desc, dev)
+    st = batch.fwd_state(dev)
+    vs = []
+    for s in range(0, desc.size, steps):
+        k = min(steps, desc.size - s)
+        vs.append(batch.ipv4_forward_batch(d_buf, d_desc[16 * s:16 * (s + k)], k, local, st).cpu().numpy())
+    torch.cuda.synchronize()
+    return d_buf.cpu().numpy(), np.concatenate(vs), st.cpu().numpy()
+
+
+@pytest.mark.gpu
+def test_gpu_forward_reference_fixture():
+    """The kernels on the reference's own sequence: one batch, and batches of 1 .. 1000 with the
+    device state carried (the cross-workgroup look-back at 256-datagram edges included)."""
+    c = cases()
+    for steps in (c["desc"].size, 1, 7, 255, 256, 257, 1000):
+        got, v, _ = _gpu_run(c["buf"].copy(), c["desc"], c["local"], steps)
+        np.testing.assert_array_equal(v, c["verdict"], err_msg=f"batches of {steps}")
+        np.testing.assert_array_equal(got, c["want"], err_msg=f"batches of {steps}")
+
+
 @pytest.mark.gpu
 def test_gpu_forward_matches_oracle():
-    import torch
-    for seed in (1, 2, 3):
-        buf, desc = headers(20000, seed)
+    for seed, n, steps in ((1, 20000, 20000), (2, 20000, 3000), (3, 300000, 300000), (4, 70000, 65536)):
+        buf, desc, local = headers(n, seed)
         want_buf = buf.copy()
-        want_v = O.batch_ipv4_forward(want_buf, desc)
-        d_buf = torch.from_numpy(buf).to("cuda:0")
-        v = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(desc, "cuda:0"), desc.size)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(v.cpu().numpy(), want_v)
-        np.testing.assert_array_equal(d_buf.cpu().numpy(), want_buf)
+        st = O.fwd_state()
+        want_v = np.concatenate([O.batch_ipv4_forward(want_buf, desc[s:s + steps], local, st)
+                                 for s in range(0, n, steps)])
+        got, v, gst = _gpu_run(buf, desc, local, steps)
+        np.testing.assert_array_equal(v, want_v)
+        np.testing.assert_array_equal(got, want_buf)
+        np.testing.assert_array_equal(gst.view(O.FWD_STATE_DTYPE), st)
+
+
+@pytest.mark.gpu
+def test_gpu_forward_long_discard_runs():
+    """Long runs of expired / local datagrams between two forwarded ones: the workgroup's first
+    eligible datagram scans back over many workgroups of verdicts; and a batch with none."""
+    import torch
+    n = 100000
+    buf, desc, local = headers(n, 9)
+    o = desc["off"].astype(np.int64)
+    ok = desc["len"] >= 20
+    keep = np.zeros(n, bool)
+    keep[[30, 31, 50000, 50001, 99990]] = True
+    buf[o[ok & ~keep] + 8] = 1                         # TTL 1: expires
+    buf[o[keep] + 8] = 64
+    buf[o[50001] + 4:o[50001] + 20] = buf[o[31] + 4:o[31] + 20]   # 50001 repeats 31's tuple...
+    buf[o[50001] + 8] = 64                             # (not its TTL)
+    buf[o[50000]:o[50000] + 20] = buf[o[31]:o[31] + 20]   # ...and so does 50000: a duplicate of 31
+    want = buf.copy()
+    st = O.fwd_state()
+    wv = O.batch_ipv4_forward(want, desc, local, st)
+    assert wv[50000] == V_DUPLICATE and wv[50001] == V_DUPLICATE
+    got, v, gst = _gpu_run(buf, desc, local, n)
+    np.testing.assert_array_equal(v, wv)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gst.view(O.FWD_STATE_DTYPE), st)
+    # nothing eligible at all: the state stays
+    buf2 = synth.random_bytes(3, 64 * 1000)
+    d2 = batch.make_desc(np.arange(1000, dtype=np.uint64) * 64, np.full(1000, 40, np.uint32))
+    buf2[np.arange(1000) * 64 + 8] = 1
+    d_buf = torch.from_numpy(buf2).to("cuda:0")
+    s = torch.from_numpy(np.array([(1, 2, 3, 4, 0)], O.FWD_STATE_DTYPE).view(np.uint8)).to("cuda:0")
+    v2 = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(d2, "cuda:0"), 1000, (), s).cpu().numpy()
+    assert (v2 == V_EXPIRED).all()
+    assert s.cpu().numpy().view(O.FWD_STATE_DTYPE)[0].tolist() == (1, 2, 3, 4, 0)
 
 
 @pytest.mark.gpu

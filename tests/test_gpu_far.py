@@ -60,3 +60,50 @@ def test_far_apart_over_2gib(ipv6):
             np.testing.assert_array_equal(u16(l4), wl, err_msg="l4 " + msg)
     del big
     torch.cuda.empty_cache()
+
+
+def test_nat_far_apart_over_2gib():
+    """The NAT batch on the same far layout: frames outside the wave's window read their old port
+    from memory (not the LDS stage) and are translated like any other."""
+    rng = np.random.default_rng(7100)
+    n = 96
+    buf, desc = random_datagrams(rng, n, ipv6=False)
+    desc["seed"] = 0
+    for o, ln in zip(desc["off"].astype(np.int64), desc["len"]):
+        if ln >= 8:
+            buf[o + 6], buf[o + 7] = 0x40, 0                # DF, no fragment: NAT's datagrams
+    nat = np.zeros(n, O.NAT_DTYPE)
+    nat["addr"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    nat["port"] = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    nat["dir"] = rng.choice(np.array([1, 2], np.uint8), n)
+    big_n = 9 << 28                                      # 2.25 GiB
+    spacing = (big_n - 4096) // n
+    far = desc.copy()
+    far["off"] = np.arange(n, dtype=np.uint64) * np.uint64(spacing) + rng.integers(0, 16, n).astype(np.uint64)
+    want_buf = buf.copy()
+    wn, wl, wv = O.batch_ipv4_nat(want_buf, desc, nat)
+    assert (wv == 1).sum() > 15
+    d_nat = torch.from_numpy(nat.view(np.uint8)).to(DEV)
+    d_desc = batch.desc_to_device(far, DEV)
+    big = torch.zeros(big_n, dtype=torch.uint8, device=DEV)
+    for shape in (None, 64, 7):
+        for i in range(n):
+            o, ln, t = int(desc["off"][i]), int(desc["len"][i]), int(far["off"][i])
+            if ln:
+                big[t:t + ln] = torch.from_numpy(buf[o:o + ln].copy()).to(DEV)
+        if shape is None:
+            batch.set_launch_override(0)
+        else:
+            batch.set_launch_override(2, fpw=shape)
+        net, l4, v = batch.ipv4_nat_batch(big, d_desc, n, d_nat)
+        torch.cuda.synchronize()
+        msg = f"shape={shape}"
+        np.testing.assert_array_equal(v.cpu().numpy(), wv, err_msg="verdict " + msg)
+        np.testing.assert_array_equal(u16(net), wn, err_msg="net " + msg)
+        np.testing.assert_array_equal(u16(l4), wl, err_msg="l4 " + msg)
+        for i in range(n):
+            o, ln, t = int(desc["off"][i]), int(desc["len"][i]), int(far["off"][i])
+            if ln:
+                np.testing.assert_array_equal(big[t:t + ln].cpu().numpy(), want_buf[o:o + ln], err_msg=f"bytes {i} {msg}")
+    del big
+    torch.cuda.empty_cache()
