@@ -46,6 +46,16 @@
  *   reference's zero state).  The bytes after the call are copied back.  Returns 0 forwarded,
  *   1 TTL expired (:1549-1553), 2 local source (:1559-1560), 3 duplicate of the last forwarded
  *   datagram (:1562-1565).
+ * rr_stack_rx(frame, len) / rr_take_delivered(&check): one frame in at the driver boundary --
+ *   pico_stack_recv (stack/pico_stack.c:465-477) on the Ethernet device of rr_eth_init -- then the
+ *   receive loops below the transport layer that pico_stack_tick runs (pico_devices_loop,
+ *   pico_protocol_datalink_loop, pico_protocol_network_loop, :766-773), so the frame goes through
+ *   pico_ethernet_receive, pico_ipv4_process_in / pico_ipv6_process_in (routing included) and, if
+ *   delivered, stops at the transport hand-off; rr_take_delivered returns that frame's protocol
+ *   (-1 none) and, for TCP / UDP, pico_transport_crc_check on it in *check (a CRC=0 build: the
+ *   no-op variant, always 1).  rr_ipv6_link adds a non-tentative /64 IPv6 link (DAD done:
+ *   pico_ipv6_link_add_no_dad) so unicast IPv6 to it is local.  The batched-driver test
+ *   (tests/test_burst_driver.py) runs this in a CRC=1 and a CRC=0 build of the stack.
  * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py, make_ref_eth.py, make_ref_nat.py) only pass datagrams whose reference reads stay inside
  * avail and whose walk terminates (the oracle restatement decides which; the others are
  * restatement-only and documented so).
@@ -64,6 +74,7 @@
 #include "pico_queue.h"
 #include "pico_dev_null.h"
 #include "pico_nat.h"
+#include "pico_protocol.h"
 
 int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
@@ -88,6 +99,10 @@ int rr_ipv4_link(uint32_t addr);
 int rr_ipv4_rx(const uint8_t *d, uint32_t avail);
 int rr_nat(int dir, uint8_t *d, uint32_t avail, uint32_t nat_addr);
 int rr_forward(uint8_t *d, uint32_t avail);
+int rr_ipv6_link(const uint8_t *addr16);
+void *rr_eth_dev(void);
+int rr_stack_rx(const uint8_t *frame, uint32_t len);
+int rr_take_delivered(int *check);
 int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
 int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
              uint32_t cap, uint32_t *out_len, uint32_t *module, int *check);
@@ -422,4 +437,67 @@ int rr_forward(uint8_t *d, uint32_t avail)
         return 1;
     memcpy(&src.addr, d + 12, 4);
     return pico_ipv4_link_get(&src) ? 2 : 3;
+}
+
+int rr_ipv6_link(const uint8_t *addr16)
+{
+    struct pico_ip6 a, m;
+    if (!g_dev)
+        return -1;
+    memcpy(a.addr, addr16, 16);
+    memset(m.addr, 0, 16);
+    memset(m.addr, 0xFF, 8);
+    return pico_ipv6_link_add_no_dad(g_dev, a, m) ? 0 : -1;
+}
+
+void *rr_eth_dev(void) { return g_edev; }
+
+int rr_stack_rx(const uint8_t *frame, uint32_t len)
+{
+    int k, r;
+    if (!g_edev)
+        return -2;
+    if (g_deliv) {
+        pico_frame_discard(g_deliv);
+        g_deliv = NULL;
+    }
+    g_frag = 0;
+    g_arp = 0;
+    r = pico_stack_recv(g_edev, (uint8_t *)frame, len);
+    for (k = 0; k < 3; k++) {
+        pico_devices_loop(64, PICO_LOOP_DIR_IN);
+        pico_protocol_datalink_loop(64, PICO_LOOP_DIR_IN);
+        pico_protocol_network_loop(64, PICO_LOOP_DIR_IN);
+    }
+    return r;
+}
+
+int rr_take_delivered(int *check)
+{
+    struct pico_frame *q;
+    int proto;
+    /* the UDP / ICMPv4 enqueues of pico_ipv4_process_bcast_in / _local_unicast_in (:299, :309, :359) */
+    while ((q = pico_dequeue(pico_proto_udp.q_in)) != NULL) {
+        if (g_deliv)
+            pico_frame_discard(g_deliv);
+        g_deliv = q;
+        g_deliv_proto = 17;
+    }
+    while ((q = pico_dequeue(pico_proto_icmp4.q_in)) != NULL) {
+        if (g_deliv)
+            pico_frame_discard(g_deliv);
+        g_deliv = q;
+        g_deliv_proto = 1;
+    }
+    *check = -1;
+    if (!g_deliv)
+        return -1;
+    proto = g_deliv_proto;
+    if (proto == 6 || proto == 17)
+        *check = delivered_check();
+    else {
+        pico_frame_discard(g_deliv);
+        g_deliv = NULL;
+    }
+    return proto;
 }

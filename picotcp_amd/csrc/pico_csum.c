@@ -759,9 +759,12 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         FLUSH(b);
         /* The kernel sees the staged span through a base pointer lo bytes below the staging
          * buffer, with base_len = hi: the caller's descriptors go over unchanged (one memcpy, no
-         * rebase), a descriptor outside base_len stays outside [0, hi).  (A staging buffer at a
-         * device address below lo -- never, in practice -- gets rebased descriptors.) */
-        vbase = (uintptr_t)c->d_buf[b] >= lo;
+         * rebase), a descriptor outside base_len stays outside [0, hi).  A staging buffer at a
+         * device address below lo (never, in practice) and a chunk that ends more than 1 GiB into
+         * the caller's buffer get rebased descriptors instead: the kernels' buffer windows (at
+         * most 2 GiB, from 1 GiB below a wave's first frame) then always cover a whole chunk, so
+         * no chunk takes their out-of-window paths. */
+        vbase = (uintptr_t)c->d_buf[b] >= lo && hi <= (1ull << 30);
         if (vbase) {
             memcpy(c->h_desc[b], desc + i, (size_t)cnt * sizeof(struct pico_csum_desc));
         } else {

@@ -144,3 +144,25 @@ def test_oversized_frame_mid_burst_with_write_changes_nothing(hb):
     import time
     time.sleep(0.2)                                  # nothing still in flight lands later
     np.testing.assert_array_equal(full, before)
+
+
+def test_host_burst_above_2gib(hb):
+    """A burst that sits more than 2 GiB into the caller's buffer: its chunks go over
+    with rebased descriptors, so the kernels' buffer windows always cover them (no out-of-window
+    path); RX, TX and the F_WRITE copy-back against the oracle on the same bytes packed low."""
+    small, d = imix_ipv4(30_000, 11)
+    hi_off = (9 << 28) + 3                                  # 2.25 GiB + 3 (odd starts)
+    big = np.zeros(hi_off + small.size + 64, np.uint8)      # untouched pages stay unallocated
+    big[hi_off:hi_off + small.size] = small
+    far = d.copy()
+    far["off"] += np.uint64(hi_off)
+    for fl in (0, _lib.F_TX):
+        on, ol, v = hb.ipv4_checksum_batch(big, far, flags=fl)
+        wn, wl, wv = O.batch_ipv4(small, d, tx=bool(fl))
+        np.testing.assert_array_equal(on, wn)
+        np.testing.assert_array_equal(ol, wl)
+        np.testing.assert_array_equal(v, wv)
+    hb.ipv4_checksum_batch(big, far, flags=_lib.F_TX | _lib.F_WRITE)
+    on, ol, v = hb.ipv4_checksum_batch(big, far)
+    assert (v == 1).sum() == (wv == 1).sum() and (on[v == 1] == 0).all() and (ol[v == 1] == 0).all()
+    del big
