@@ -41,10 +41,9 @@ __device__ uint32_t g_stamps_n;
 //      keeps its lanes busy; per-frame sums go to LDS;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
-constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1
-#ifndef PICO_HW_NT
-#define PICO_HW_NT 0         // non-temporal head-window loads: A/B builds only (5 % slower, profiles/r02nt)
-#endif
+constexpr uint32_t WPB = 4;  // waves per workgroup (8 measured the same on the sorted rounds, profiles/r02wpb)
+constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1 (temporal loads:
+                             // non-temporal ones measured 5 % slower, profiles/r02nt)
 
 struct SortedWaveLds {
     uint32_t acc_all[64];
@@ -62,22 +61,10 @@ struct SortedWaveLds {
 // A wave's LDS.  Fused modes: the phase-1 head-window staging (64 frames x HW chunks,
 // chunk slots XOR-swizzled) shares the space with the state it is parsed into -- 8 KiB a
 // wave, 4 workgroups of 4 waves per CU.  RAW mode: the state alone (3.75 KiB).
-// Stream-order waves for dense MODE 1 batches (stream_batch).  Product shape, measured
+// Stream-order waves for dense fused batches (stream_batch).  Product shape, measured
 // (profiles/r03s3/README.md): 8 chunks per lane per step (8 KiB; StreamLds 10 KiB a wave, 4
-// workgroups of 4 waves per CU), two steps in flight, non-temporal loads.  A/B builds: -D...=0.
-#ifndef PICO_STREAM
-#define PICO_STREAM 1
-#endif
-#ifndef PICO_STREAM_CPL
-#define PICO_STREAM_CPL 8
-#endif
-#ifndef PICO_STREAM_NT
-#define PICO_STREAM_NT 1
-#endif
-#ifndef PICO_STREAM_DB
-#define PICO_STREAM_DB 1
-#endif
-constexpr uint32_t SCPL = PICO_STREAM_CPL;   // chunks per lane per step
+// workgroups of 4 waves per CU), two steps in flight, non-temporal loads.
+constexpr uint32_t SCPL = 8;                 // chunks per lane per step
 constexpr uint32_t SQ = 64u * SCPL;          // chunks per step
 struct StreamLds {
     uint4 raw[SQ];           // the step's bytes, chunk slots swizzled (sslot)
@@ -88,9 +75,7 @@ template <bool STAGE>
 union SortedWaveSmem {
     SortedWaveLds s;
     uint4 stage[64 * HW];
-#if PICO_STREAM
     StreamLds st;
-#endif
 };
 template <>
 union SortedWaveSmem<false> {
@@ -409,7 +394,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
                 const uint32_t g = FPL * k + gi;
                 const uint32_t gv0 = (uint32_t)__shfl((int)v0, (int)g);
                 const uint32_t gn = (uint32_t)__shfl((int)nin, (int)g);
-                t[k] = load_win<PICO_HW_NT != 0>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
+                t[k] = load_win<false>(w, ci < gn ? gv0 + 16u * ci : WIN_OOB);
             }
 #pragma unroll
             for (uint32_t k = 0; k < HW; ++k) {
@@ -777,8 +762,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
     __builtin_amdgcn_wave_barrier();
 }
 
-#if PICO_STREAM
-// ---------------------------------------------------------------- stream-order wave (MODE 1)
+// ---------------------------------------------------------------- stream-order waves (fused modes)
 //
 // A wave whose 64 datagrams lie densely in one span of the batch (a TAP / ring burst: back to
 // back behind their link headers) reads that span in address order -- 64 lanes x SCPL
@@ -852,19 +836,50 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
     return ((v >> 8) | (v << 8)) & 0xFFFFu;
 }
 
-// Returns false (nothing written) when the wave's frames are not one dense span; the caller
-// then runs the sorted-rounds batch.  NATM: the NAT batch (F_NAT), its own instantiation so the
-// RX / TX waves carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for
-// datagrams whose transport follows the 40-byte header (descriptor seed 0; RX next header TCP /
-// UDP / ICMPv6 -- anything else needs the extension-header walk: the sorted rounds).
-// ETH: the Ethernet batch (MODE 3) for IPv4 behind the 14-byte header (ARP / dropped frames need
-// no sums; a wave holding an IPv6 frame falls back after the loop).
+// Workgroup-wide stream (round 4): the workgroup's WPB x fpw frames are split into WPB ranges of
+// whole frames with equal bytes (a workgroup scan of the lengths in frame order), and wave w streams
+// range w -- so the waves of a workgroup read the same number of bytes whatever the size mix, where
+// a wave of 64 IMIX frames alone reads 64 frames' worth (+-14 %, the largest 1.5x the mean: the
+// launch's end).  Lane j still owns frame j (its header chunks, its prefixes, its
+// finish): at every step the workgroup's stages sit in LDS together (two barriers a step) and lane j
+// reads the stage of the wave that streams its frame's range.  A frame never straddles two ranges,
+// so every prefix it needs comes from one wave's running sum.
+struct StreamWg {
+    uint64_t anc[WPB];     // each wave's first valid frame's line (the workgroup anchor)
+    uint32_t wsum[WPB];    // each wave's valid bytes (frame order prefix)
+    uint32_t flag[WPB];    // a wave that rules the stream out (stack-walked seed, huge frame)
+    int rmin[WPB];         // range r: first line, end, bytes (relative to the anchor)
+    int rmax[WPB];
+    uint32_t rsum[WPB];
+    uint32_t far;                      // a frame more than 512 MiB from the anchor
+};
+
+// Returns false (nothing written) for a wave whose frames are not streamed: the workgroup's
+// frames are not one dense span (every wave), or after the loop, this wave holds a frame the
+// stream does not finish (below).  Every wave of the workgroup must call it (barriers), whether or
+// not it has frames.  NATM: the NAT batch (F_NAT), its own instantiation so the RX / TX waves
+// carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for datagrams whose
+// transport follows the 40-byte header (descriptor seed 0; RX next header TCP / UDP / ICMPv6 --
+// anything else needs the extension-header walk: the sorted rounds).  ETH: the Ethernet batch
+// (MODE 3) for IPv4 behind the 14-byte header (ARP / dropped frames need no sums; a wave holding
+// an IPv6 frame falls back after the loop).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
 template <bool NATM, bool V6 = false, bool ETH = false>
-__device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane,
-                                             uint64_t f0) {
+__device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<true>* lds_all, uint32_t lane,
+                                             uint32_t wv, uint64_t f0) {
+    // the workgroup table lives in wave 0's stage until the third barrier below (after it nothing
+    // reads it; the stages -- or a fallback's sorted-rounds state -- are written only after it):
+    // 4 workgroups of 4 waves keep fitting a CU's 160 KiB of LDS
+    static_assert(sizeof(StreamWg) <= sizeof(StreamLds), "workgroup table must fit a stage");
+    StreamWg& W = *reinterpret_cast<StreamWg*>(&lds_all[0]);
     constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
     if (!ETH && (p.flags & F_MACF)) return false;
-    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    StreamLds& S = lds_all[wv].st;
+    const uint32_t cnt = f0 < p.n ? (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0) : 0u;
     const bool tx = (p.flags & 2u) != 0;
     constexpr bool natm = NATM;
     uint4 dcur = make_uint4(0, 0, 0, 0);
@@ -874,32 +889,91 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     if (NATM && lane < cnt)
         rw = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo) +
                                              8ull * (f0 + lane));
-    uint64_t off = ((uint64_t)dcur.y << 32) | dcur.x;
+    uint64_t off0 = ((uint64_t)dcur.y << 32) | dcur.x;
     uint32_t len = lane < cnt ? dcur.z : 0u;
-    const bool oob = lane < cnt && (off > p.base_len || len > p.base_len - off);
-    if (oob || lane >= cnt) { len = 0; off = 0; }
+    const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
+    if (oob || lane >= cnt) { len = 0; off0 = 0; }
     const bool valid = len >= (V6 ? 40u : ETH ? 14u : 20u);  // shorter: MALFORMED, nothing to sum
-    if (V6 && __builtin_amdgcn_ballot_w64(valid && dcur.w != 0u)) return false;   // a stack-walked seed
-    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off;
-    // the span, relative to the first valid frame's line (a frame more than 512 MiB away:
-    // not one span)
-    const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
-    if (vb == 0) return false;
-    const int fv = __builtin_ffsll((long long)vb) - 1;
+    const uint32_t blen = valid ? len : 0u;
+    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
-    const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+    // ---- the workgroup's span: anchor, frame-order byte prefix, ranges
+    {
+        const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
+        const int fv = vb ? __builtin_ffsll((long long)vb) - 1 : 0;
+        const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+        // a stack-walked IPv6 seed, or a frame over 1 MiB (the 32-bit byte sums): no stream
+        const bool no = __builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20))) != 0;
+        const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
+        if (lane == 0) {
+            W.anc[wv] = vb ? a : ~0ull;
+            W.wsum[wv] = ws;
+            W.flag[wv] = no ? 1u : 0u;
+        }
+        if (wv == 0 && lane < WPB) {
+            W.rmin[lane] = 0x7FFFFFFF;
+            W.rmax[lane] = -0x7FFFFFFF;
+            W.rsum[lane] = 0u;
+            if (lane == 0) W.far = 0u;
+        }
+    }
+    __syncthreads();
+    uint64_t anchor = ~0ull;
+    uint32_t bad = 0u, exw = 0u, total = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < WPB; ++k) {
+        const uint64_t a = W.anc[k];
+        if (anchor == ~0ull) anchor = a;
+        bad |= W.flag[k];
+        exw += k < wv ? W.wsum[k] : 0u;
+        total += W.wsum[k];
+    }
+    if (anchor == ~0ull || bad) {                      // workgroup-uniform (the same LDS for all)
+        __syncthreads();                               // (the table is read by every wave first)
+        return false;
+    }
     const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
-    if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
-    const int mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0), 63);
-    const int mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : 0), 63);
-    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(valid ? (int)len : 0), 63);
-    const uint64_t lo = anchor + (int64_t)mn;
+    const bool far = valid && (dl < -(1ll << 29) || dh > (1ll << 29));
+    // range of frame j: its frame-order byte prefix in WPB equal parts (whole frames)
+    const uint32_t inc = (uint32_t)wave_incl<0>((int)blen);
+    const uint32_t ex = exw + inc - blen;
+    const uint32_t rg = valid ? min(WPB - 1u, (uint32_t)(((uint64_t)ex * WPB) / total)) : 0u;
+    if (valid && !far) {
+        atomicMin(&W.rmin[rg], (int)dl);
+        atomicMax(&W.rmax[rg], (int)dh);
+        atomicAdd(&W.rsum[rg], len);
+    }
+    if (__builtin_amdgcn_ballot_w64(far) && lane == 0) W.far = 1u;
+    __syncthreads();
+    int mn = 0x7FFFFFFF, mx = -0x7FFFFFFF;
+    bool dense = W.far == 0u;
+    uint32_t nsteps = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < WPB; ++k) {
+        const uint32_t rs = W.rsum[k];
+        const int a = W.rmin[k], b = W.rmax[k];
+        if (rs) {
+            mn = min(mn, a);
+            mx = max(mx, b);
+            const uint32_t ext = (uint32_t)(((int64_t)b + 15 - a) & ~(int64_t)15);
+            dense = dense && (uint64_t)ext <= 2ull * rs + 4096u;
+            nsteps = max(nsteps, ((ext >> 4) + SQ - 1u) / SQ);
+        }
+    }
+    // this wave's range [q0, q1) in chunks of the window; frame j's owner's range start
+    const bool mine = W.rsum[wv] != 0u;
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(mine ? (int)((uint32_t)(W.rmin[wv] - mn) >> 4) : 0);
+    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readfirstlane(mine ? (int)((uint32_t)(W.rmax[wv] + 15 - mn) >> 4) : 0);
+    nsteps = (uint32_t)__builtin_amdgcn_readfirstlane((int)nsteps);
+    const uint32_t q0o = valid ? (uint32_t)(W.rmin[rg] - mn) >> 4 : 0u;
+    __syncthreads();                                   // the table is dead from here on
+    if (!dense) return false;                          // workgroup-uniform
+    // (wave-uniform values read from LDS: in SGPRs, not kept in VGPRs across the loop)
+    const uint64_t lo = uniform64(anchor + (int64_t)mn);
     const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
-    if (!(extent <= 2ull * sum + 4096u)) return false;
-
     const Window w = make_window(lo, (uint32_t)extent);
-    const uint32_t nq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(extent >> 4));
+    const StreamLds& So = lds_all[rg].st;
     const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
     const uint32_t r = rel & 15u, hq = rel >> 4;
     constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
@@ -916,21 +990,17 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     uint4 v[SCPL];
 #pragma unroll
     for (uint32_t c = 0; c < SCPL; ++c) {
-        const uint32_t q = 64u * c + lane;
-        v[c] = load_win<PICO_STREAM_NT != 0>(w, q < nq ? 16u * q : WIN_OOB);
+        const uint32_t q = q0 + 64u * c + lane;
+        v[c] = load_win<true>(w, q < q1 ? 16u * q : WIN_OOB);
     }
     STAMP(1);
-    for (uint32_t qb = 0; qb < nq; qb += SQ) {
+    for (uint32_t st = 0; st < nsteps; ++st) {
+        const uint32_t qb = q0 + st * SQ;
         uint4 vn[SCPL];
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) {
-            const uint32_t q = (PICO_STREAM_DB ? qb + SQ : qb) + 64u * c + lane;
-            if (PICO_STREAM_DB || qb != 0) vn[c] = load_win<PICO_STREAM_NT != 0>(w, q < nq ? 16u * q : WIN_OOB);
-            else vn[c] = v[c];
-        }
-        if (!PICO_STREAM_DB) {
-#pragma unroll
-            for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+            const uint32_t q = qb + SQ + 64u * c + lane;
+            vn[c] = load_win<true>(w, q < q1 ? 16u * q : WIN_OOB);
         }
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -944,23 +1014,24 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
             loc[k] = t;
             t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
         }
-        const uint32_t inc = (uint32_t)wave_incl<0>((int)t);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        const uint32_t ex = base + inc - t;
+        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
+        const uint32_t exs = base + incs - t;
 #pragma unroll
         for (uint32_t k = 0; k < SCPL; k += 4)
             *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
-                make_uint4(ex + loc[k], ex + loc[k + 1], ex + loc[k + 2], ex + loc[k + 3]);
-        __builtin_amdgcn_wave_barrier();
-        // frame j's head window chunks that are in this step
+                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
+        __syncthreads();                               // every wave's step is staged
+        // frame j's head window chunks that are in its range's stage
+        const uint32_t qbo = q0o + st * SQ;
 #pragma unroll
         for (uint32_t i = 0; i < HS; ++i) {
-            const uint32_t qi = hq + i - qb;
-            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
+            const uint32_t qi = hq + i - qbo;
+            if (i < nlh && qi < SQ) hw[i] = So.raw[sslot(qi)];
         }
         // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
         // fails the header checks below never reads them)
-        if (V6 && !pre && hq + 1u < qb + SQ) {
+        if (V6 && !pre && hq + 1u < qbo + SQ) {
             pre = true;
             uint32_t H[2];
             window_words<2, false>(hw, r, H);
@@ -970,7 +1041,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
             b2 = rel + min(40u + plen, len);
             if (tx && nh == 6u && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }   // TCP crc: past the head chunks
         }
-        if (!V6 && !pre && hq + (ETH ? 2u : 1u) < qb + SQ) {
+        if (!V6 && !pre && hq + (ETH ? 2u : 1u) < qbo + SQ) {
             pre = true;
             uint32_t H[3];
             window_words<3, ETH>(hw, r + L2, H);
@@ -991,22 +1062,24 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
                 x1 = x0 + 2u;
             }
         }
-        const uint32_t byte0 = 16u * qb;
-        stream_point(S, b1, byte0, P1);
-        stream_point(S, b2, byte0, P2);
+        const uint32_t byte0 = 16u * qbo;
+        stream_point(So, b1, byte0, P1);
+        stream_point(So, b2, byte0, P2);
         if (__builtin_amdgcn_ballot_w64(b0 != 0u || x0 != 0u)) {
-            stream_point(S, b0, byte0, P0);
-            stream_point(S, x0, byte0, P3);
-            stream_point(S, x1, byte0, P4);
+            stream_point(So, b0, byte0, P0);
+            stream_point(So, x0, byte0, P3);
+            stream_point(So, x1, byte0, P4);
         }
         base += tot;
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
         asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();                               // every stage read before the next is written
     }
 
     STAMP(2);
+    // the frame's offset again, from the span (a 64-bit value less to keep across the loop)
+    const uint64_t off = valid ? lo + rel - reinterpret_cast<uintptr_t>(p.base) : 0u;
     if constexpr (V6) {
         // pico_ipv6_process_in / pico_transport_crc_check as sorted_batch's MODE 2 (seed 0, no
         // extension header): lengths, byte-9 dispatch (ipcrc), the field, the pseudo header
@@ -1192,36 +1265,28 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     STAMP(3);
     return true;
 }
-#endif
 
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
-#ifndef PICO_SORTED_WPB
-#define PICO_SORTED_WPB 4    // waves per workgroup (A/B builds: 8)
-#endif
 // The product shape (measured): 8 chunks per lane per round, the 1-lane class for
 // frames of <= 8 chunks, non-temporal loads in the >= 16-lane rounds; 4 waves per SIMD.
 template <int MODE, bool NT = true, int CPL = 8, bool SMALL = true>
-__global__ __launch_bounds__(64 * PICO_SORTED_WPB, 4) void csum_sorted_kernel(FlatArgs p) {
-    __shared__ SortedWaveSmem<MODE != 0> lds_all[PICO_SORTED_WPB];
-    const uint32_t lane = threadIdx.x & 63u;
-    SortedWaveSmem<MODE != 0>& S = lds_all[threadIdx.x >> 6];
-    const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * p.fpw;
+__global__ __launch_bounds__(64 * WPB, 4) void csum_sorted_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<MODE != 0> lds_all[WPB];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    SortedWaveSmem<MODE != 0>& S = lds_all[wv];
+    const uint64_t f0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wv) * p.fpw;
     STAMP(0);
-    if (f0 < p.n) {
-#if PICO_STREAM
-        if constexpr (MODE == 2) {
-            if (stream_batch<false, true>(p, S.st, lane, f0)) return;
+    if ((uint64_t)blockIdx.x * (blockDim.x >> 6) * p.fpw < p.n) {     // workgroup-uniform
+        if constexpr (MODE != 0) {
+            bool done;
+            if constexpr (MODE == 2) done = stream_batch<false, true>(p, lds_all, lane, wv, f0);
+            else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, lds_all, lane, wv, f0);
+            else done = (p.flags & F_NAT) ? stream_batch<true>(p, lds_all, lane, wv, f0)
+                                          : stream_batch<false>(p, lds_all, lane, wv, f0);
+            if (done) return;
         }
-        if constexpr (MODE == 3) {
-            if (stream_batch<false, false, true>(p, S.st, lane, f0)) return;
-        }
-        if constexpr (MODE == 1) {
-            if ((p.flags & F_NAT) ? stream_batch<true>(p, S.st, lane, f0) : stream_batch<false>(p, S.st, lane, f0))
-                return;
-        }
-#endif
-        sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
+        if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
     }
     STAMP(3);
 }
@@ -1411,8 +1476,8 @@ int SORTED_LAUNCH(const void* args, void* stream);
 int SORTED_LAUNCH(const void* args, void* stream) {
     const FlatArgs& a = *static_cast<const FlatArgs*>(args);
     const uint64_t waves = ((uint64_t)a.n + a.fpw - 1) / a.fpw;
-    hipLaunchKernelGGL(csum_sorted_kernel<SORTED_MODE>, dim3((unsigned)((waves + PICO_SORTED_WPB - 1) / PICO_SORTED_WPB)),
-                       dim3(64 * PICO_SORTED_WPB), 0, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(csum_sorted_kernel<SORTED_MODE>, dim3((unsigned)((waves + WPB - 1) / WPB)),
+                       dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
 
