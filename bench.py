@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2slot|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
   c1 (default, the metric's config): 256K x 1500 B frames, raw pico_checksum per frame
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
+  c2slot: the same datagrams each in its own 2 KiB slot (a driver's slot ring), RX verify
   c2tx: the same datagrams, fused TX (checksums computed and written in place)
   c2tx_nw: fused TX computed and returned only (F_TX without F_WRITE: the driver's header write-out)
   c2nat: the same datagrams through the NAT batch (address / port rewrite + full checksum recompute)
@@ -63,6 +64,11 @@ CONFIGS = {
     "c2": dict(kind="ipv4", frames=262144,
                workload="C2: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams (14 B Ethernet header in front), "
                         "fused IPv4 header + TCP pseudo-header RX verify"),
+    "c2slot": dict(kind="ipv4", frames=262144, slot=2048,
+                   workload="C2 on a slot ring: the 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams each "
+                            "in its own 2 KiB slot (14 B Ethernet header first), as a batching TAP driver lays "
+                            "out a burst (modules/pico_dev_tap.c:63-75), fused IPv4 header + TCP pseudo-header "
+                            "RX verify"),
     "c2v6": dict(kind="ipv6", frames=262144,
                  workload="C2 (IPv6, SURVEY 8f row 3): 256K simple-IMIX {64,576,1500}+20 B IPv6/TCP datagrams "
                           "(14 B Ethernet header in front), fused IPv6 pseudo-header TCP RX verify"),
@@ -136,9 +142,9 @@ def rotation(batch_bytes: int) -> int:
     return max(3, -(-(1 << 30) // max(1, batch_bytes)))
 
 
-def make_c2(n, device, seed, frame_bytes=0, keep_host=True):
+def make_c2(n, device, seed, frame_bytes=0, keep_host=True, slot=0):
     lens = synth.imix_lengths(n, seed) if not frame_bytes else np.full(n, frame_bytes, dtype=np.uint32)
-    buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
+    buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True, slot=slot)
     desc = batch.make_desc(net, avail)
     d_buf = torch.from_numpy(buf).to(device)
     d_desc = batch.desc_to_device(desc, device)
@@ -593,8 +599,8 @@ def main():
     elif cfg["kind"] == "ipv4":
         n = cfg["frames"]
         ln = cfg.get("frame_bytes", 0)
-        rot = a.rotate or rotation(n * ((ln or IMIX_MEAN) + 14))
-        sets = [make_c2(n, dev, 500 + 13 * rank + i, ln, keep_host=i == 0) for i in range(rot)]
+        rot = a.rotate or rotation(n * (cfg.get("slot") or (ln or IMIX_MEAN) + 14))
+        sets = [make_c2(n, dev, 500 + 13 * rank + i, ln, keep_host=i == 0, slot=cfg.get("slot", 0)) for i in range(rot)]
         wr = cfg.get("tx") and cfg.get("write", True)
         fl = (batch.F_TX | (batch.F_WRITE if wr else 0)) if cfg.get("tx") else 0
         outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
@@ -776,7 +782,8 @@ def main():
         if not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline_fused(sets[0][3], cfg["kind"], bool(cfg.get("tx")),
                                                      a.cpu_seconds / 2, nat=cfg.get("_nat_host"))
-        if not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not cfg.get("nat") and not ln:
+        if (not a.no_e2e and cfg["kind"] == "ipv4" and not cfg.get("tx") and not cfg.get("nat") and not ln
+                and not cfg.get("slot")):
             out["e2e_host_to_host"] = e2e_rate_desc(sets[0][3])
     elif rank == 0 and world == 1 and cfg["kind"] == "frag":
         if not a.no_cpu:

@@ -844,15 +844,48 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
 // finish): at every step the workgroup's stages sit in LDS together (two barriers a step) and lane j
 // reads the stage of the wave that streams its frame's range.  A frame never straddles two ranges,
 // so every prefix it needs comes from one wave's running sum.
+// Two layouts: DENSE -- the range's frames lie back to back (a TAP / ring burst): the wave reads its
+// range's span in address order; COMPACT -- anything else within +-512 MiB (frames in fixed slots of
+// a batching driver's ring, modules/pico_dev_tap.c:63-75, or scattered): the wave reads only its
+// frames' own lines, frame after frame, as one compacted chunk sequence (chunk q of the range ->
+// frame i, the last with cs_i <= q, by a binary search over the range's (cs, line) table held in
+// the wave's registers); every frame position is then a compacted position, and the rest of the
+// stream is the same.
+constexpr uint32_t CMAXF = 128;   // COMPACT: frames per range (two table entries per lane)
 struct StreamWg {
     uint64_t anc[WPB];     // each wave's first valid frame's line (the workgroup anchor)
-    uint32_t wsum[WPB];    // each wave's valid bytes (frame order prefix)
+    uint32_t wsum[WPB];    // each wave's valid bytes, chunks, frames (frame-order prefixes)
+    uint32_t wch[WPB];
+    uint32_t wcnt[WPB];
     uint32_t flag[WPB];    // a wave that rules the stream out (stack-walked seed, huge frame)
     int rmin[WPB];         // range r: first line, end, bytes (relative to the anchor)
     int rmax[WPB];
     uint32_t rsum[WPB];
+    uint32_t rnc[WPB];     // range r: its frames' chunks and count, its first frame's prefixes
+    uint32_t rcnt[WPB];
+    uint32_t rc0[WPB];
+    uint32_t rn0[WPB];
     uint32_t far;                      // a frame more than 512 MiB from the anchor
 };
+
+// COMPACT: the window line of compacted chunk q of a range whose frame i (i < n) starts at compacted
+// chunk cs_i and window line line_i -- entries i and 64 + i in lane i (csab = cs_i | cs_64+i << 16,
+// la / lb = the lines), cs64 = cs_64.  Every lane of the wave must call it (ds_bpermute).
+__device__ __forceinline__ uint32_t compact_line(uint32_t q, uint32_t csab, uint32_t la, uint32_t lb, uint32_t n,
+                                                 uint32_t cs64) {
+    uint32_t i = (n > 64u && cs64 <= q) ? 64u : 0u;
+    uint32_t ci = i ? cs64 : 0u;
+#pragma unroll
+    for (uint32_t st = 32; st >= 1; st >>= 1) {
+        const uint32_t c = i + st;
+        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c & 63u) << 2), (int)csab);
+        const uint32_t cv = c >= 64u ? v >> 16 : v & 0xFFFFu;
+        if (c < n && cv <= q) { i = c; ci = cv; }
+    }
+    const uint32_t l0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((i & 63u) << 2), (int)la);
+    const uint32_t l1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((i & 63u) << 2), (int)lb);
+    return (i >= 64u ? l1 : l0) + (q - ci);
+}
 
 // Returns false (nothing written) for a wave whose frames are not streamed: the workgroup's
 // frames are not one dense span (every wave), or after the loop, this wave holds a frame the
@@ -897,6 +930,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint32_t blen = valid ? len : 0u;
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
+    const uint32_t cch = valid ? ((uint32_t)(addr & 15u) + len + 15u) >> 4 : 0u;   // the frame's lines
     // ---- the workgroup's span: anchor, frame-order byte prefix, ranges
     {
         const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
@@ -906,27 +940,36 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         // a stack-walked IPv6 seed, or a frame over 1 MiB (the 32-bit byte sums): no stream
         const bool no = __builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20))) != 0;
         const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
+        const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)cch), 63);
         if (lane == 0) {
             W.anc[wv] = vb ? a : ~0ull;
             W.wsum[wv] = ws;
+            W.wch[wv] = wc;
+            W.wcnt[wv] = (uint32_t)__builtin_popcountll(vb);
             W.flag[wv] = no ? 1u : 0u;
         }
         if (wv == 0 && lane < WPB) {
             W.rmin[lane] = 0x7FFFFFFF;
             W.rmax[lane] = -0x7FFFFFFF;
             W.rsum[lane] = 0u;
+            W.rnc[lane] = 0u;
+            W.rcnt[lane] = 0u;
+            W.rc0[lane] = 0xFFFFFFFFu;
+            W.rn0[lane] = 0xFFFFFFFFu;
             if (lane == 0) W.far = 0u;
         }
     }
     __syncthreads();
     uint64_t anchor = ~0ull;
-    uint32_t bad = 0u, exw = 0u, total = 0u;
+    uint32_t bad = 0u, exw = 0u, total = 0u, exc = 0u, exn = 0u;
 #pragma unroll
     for (uint32_t k = 0; k < WPB; ++k) {
         const uint64_t a = W.anc[k];
         if (anchor == ~0ull) anchor = a;
         bad |= W.flag[k];
         exw += k < wv ? W.wsum[k] : 0u;
+        exc += k < wv ? W.wch[k] : 0u;
+        exn += k < wv ? W.wcnt[k] : 0u;
         total += W.wsum[k];
     }
     if (anchor == ~0ull || bad) {                      // workgroup-uniform (the same LDS for all)
@@ -939,16 +982,24 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint32_t inc = (uint32_t)wave_incl<0>((int)blen);
     const uint32_t ex = exw + inc - blen;
     const uint32_t rg = valid ? min(WPB - 1u, (uint32_t)(((uint64_t)ex * WPB) / total)) : 0u;
+    // frame-order prefixes of the frames' lines and of the valid frames (COMPACT)
+    const uint32_t exch = exc + (uint32_t)wave_incl<0>((int)cch) - cch;
+    const uint64_t vbm = __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t exfn = exn + __builtin_amdgcn_mbcnt_hi((uint32_t)(vbm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vbm, 0u));
     if (valid && !far) {
         atomicMin(&W.rmin[rg], (int)dl);
         atomicMax(&W.rmax[rg], (int)dh);
         atomicAdd(&W.rsum[rg], len);
+        atomicAdd(&W.rnc[rg], cch);
+        atomicAdd(&W.rcnt[rg], 1u);
+        atomicMin(&W.rc0[rg], exch);
+        atomicMin(&W.rn0[rg], exfn);
     }
     if (__builtin_amdgcn_ballot_w64(far) && lane == 0) W.far = 1u;
     __syncthreads();
     int mn = 0x7FFFFFFF, mx = -0x7FFFFFFF;
-    bool dense = W.far == 0u;
-    uint32_t nsteps = 0;
+    bool dense = W.far == 0u, compact = W.far == 0u;
+    uint32_t nsteps = 0, csteps = 0;
 #pragma unroll
     for (uint32_t k = 0; k < WPB; ++k) {
         const uint32_t rs = W.rsum[k];
@@ -959,23 +1010,52 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             const uint32_t ext = (uint32_t)(((int64_t)b + 15 - a) & ~(int64_t)15);
             dense = dense && (uint64_t)ext <= 2ull * rs + 4096u;
             nsteps = max(nsteps, ((ext >> 4) + SQ - 1u) / SQ);
+            compact = compact && W.rcnt[k] <= CMAXF && W.rnc[k] < 0x10000u;
+            csteps = max(csteps, (W.rnc[k] + SQ - 1u) / SQ);
         }
     }
-    // this wave's range [q0, q1) in chunks of the window; frame j's owner's range start
+    compact = compact && !dense;
+    // this wave's range [q0, q1) in chunks of the window (COMPACT: of its compacted sequence);
+    // frame j's owner's range start, its compacted start and its index in the range
     const bool mine = W.rsum[wv] != 0u;
-    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(mine ? (int)((uint32_t)(W.rmin[wv] - mn) >> 4) : 0);
-    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readfirstlane(mine ? (int)((uint32_t)(W.rmax[wv] + 15 - mn) >> 4) : 0);
-    nsteps = (uint32_t)__builtin_amdgcn_readfirstlane((int)nsteps);
-    const uint32_t q0o = valid ? (uint32_t)(W.rmin[rg] - mn) >> 4 : 0u;
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(mine && !compact ? (int)((uint32_t)(W.rmin[wv] - mn) >> 4) : 0);
+    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        !mine ? 0 : compact ? (int)W.rnc[wv] : (int)((uint32_t)(W.rmax[wv] + 15 - mn) >> 4));
+    const uint32_t ncf = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.rcnt[wv]);
+    nsteps = (uint32_t)__builtin_amdgcn_readfirstlane((int)(compact ? csteps : nsteps));
+    const uint32_t q0o = valid && !compact ? (uint32_t)(W.rmin[rg] - mn) >> 4 : 0u;
+    const uint32_t csj = valid ? exch - W.rc0[rg] : 0u, idx = valid ? exfn - W.rn0[rg] : 0u;
     __syncthreads();                                   // the table is dead from here on
-    if (!dense) return false;                          // workgroup-uniform
+    if (!dense && !compact) return false;              // workgroup-uniform
     // (wave-uniform values read from LDS: in SGPRs, not kept in VGPRs across the loop)
     const uint64_t lo = uniform64(anchor + (int64_t)mn);
     const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
     const Window w = make_window(lo, (uint32_t)extent);
     const StreamLds& So = lds_all[rg].st;
-    const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
+    const uint32_t relw = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
+    // COMPACT: every position of the frame in its range's compacted sequence
+    const uint32_t rel = compact ? 16u * csj + (relw & 15u) : relw;
     const uint32_t r = rel & 15u, hq = rel >> 4;
+    // COMPACT: the range's (cs, line) table into the loading wave's registers, through LDS (wave 0's
+    // stage, free until the loop)
+    uint32_t csab = 0u, lna = 0u, lnb = 0u, cs64 = 0u;
+    if (compact) {                                     // workgroup-uniform
+        uint2* T = reinterpret_cast<uint2*>(&lds_all[0]);
+        static_assert(WPB * CMAXF * sizeof(uint2) <= sizeof(StreamLds), "range tables must fit a stage");
+        if (valid) T[rg * CMAXF + idx] = make_uint2(csj, relw >> 4);
+        __syncthreads();
+        const uint2 e0 = T[wv * CMAXF + lane], e1 = T[wv * CMAXF + 64u + lane];
+        csab = (e0.x & 0xFFFFu) | (e1.x << 16);
+        lna = e0.y;
+        lnb = e1.y;
+        cs64 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e1.x);
+        __syncthreads();
+    }
+    // the window offset of chunk q of this wave's range (WIN_OOB past its end)
+    auto chunk_off = [&](uint32_t q) -> uint32_t {
+        const uint32_t ln = compact ? compact_line(q, csab, lna, lnb, ncf, cs64) : q;
+        return q < q1 ? 16u * ln : WIN_OOB;
+    };
     constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
     const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
     uint4 hw[HW];
@@ -990,8 +1070,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     uint4 v[SCPL];
 #pragma unroll
     for (uint32_t c = 0; c < SCPL; ++c) {
-        const uint32_t q = q0 + 64u * c + lane;
-        v[c] = load_win<true>(w, q < q1 ? 16u * q : WIN_OOB);
+        v[c] = load_win<true>(w, chunk_off(q0 + 64u * c + lane));
     }
     STAMP(1);
     for (uint32_t st = 0; st < nsteps; ++st) {
@@ -999,8 +1078,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         uint4 vn[SCPL];
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) {
-            const uint32_t q = qb + SQ + 64u * c + lane;
-            vn[c] = load_win<true>(w, q < q1 ? 16u * q : WIN_OOB);
+            vn[c] = load_win<true>(w, chunk_off(qb + SQ + 64u * c + lane));
         }
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -1079,7 +1157,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
 
     STAMP(2);
     // the frame's offset again, from the span (a 64-bit value less to keep across the loop)
-    const uint64_t off = valid ? lo + rel - reinterpret_cast<uintptr_t>(p.base) : 0u;
+    const uint64_t off = valid ? lo + relw - reinterpret_cast<uintptr_t>(p.base) : 0u;
     if constexpr (V6) {
         // pico_ipv6_process_in / pico_transport_crc_check as sorted_batch's MODE 2 (seed 0, no
         // extension header): lengths, byte-9 dispatch (ipcrc), the field, the pseudo header

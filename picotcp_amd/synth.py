@@ -48,7 +48,7 @@ def imix_lengths(n: int, seed: int, mix=SIMPLE_IMIX) -> np.ndarray:
 
 
 def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = True, ihl: int = 5,
-               frag=None):
+               frag=None, slot: int = 0):
     """IPv4 datagrams of the given total lengths, packed back to back, each with a
     valid header (vhl = 0x40|ihl, len, ttl 64, proto, random id/addresses/ports/payload)
     and a transport header (TCP 20 B, UDP 8 B, ICMP 8 B).  frag = the flags / offset field
@@ -57,15 +57,22 @@ def ipv4_batch(lengths: np.ndarray, seed: int = 2, proto: int = 6, eth: bool = T
     make them valid with the TX kernel (PICO_CSUM_F_TX | F_WRITE) or a host checker.
     eth=True puts a 14-byte Ethernet header in front of each datagram (pico_ethernet.c:183),
     so the IPv4 headers are 2-byte aligned as in the reference RX path.
+    slot > 0: frame k starts at k * slot instead (a driver's ring of fixed slots; the rest of each
+    slot holds random bytes).
     Returns (buffer uint8, net offsets uint64, available bytes uint32)."""
     lengths = np.asarray(lengths, dtype=np.uint32)
     n = lengths.size
     pre = 14 if eth else 0
     frame_len = lengths.astype(np.uint64) + pre
     starts = np.zeros(n, dtype=np.uint64)
-    if n:
-        starts[1:] = np.cumsum(frame_len)[:-1]
-    total = int(frame_len.sum())
+    if slot:
+        assert int(frame_len.max(initial=0)) <= slot, "frame larger than its slot"
+        starts = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+        total = n * slot
+    else:
+        if n:
+            starts[1:] = np.cumsum(frame_len)[:-1]
+        total = int(frame_len.sum())
     buf = random_bytes(seed, total)
     net = starts + np.uint64(pre)
     hl = 4 * ihl
