@@ -263,10 +263,20 @@ def cpu_model() -> str:
 
 def cpu_threads() -> tuple[int, int]:
     """(threads used, usable cores).  The GPU box gives one GPU's job a 16-core share of
-    the host (OMP_NUM_THREADS=16 there; sched_getaffinity shows the whole machine), so
+    the host (OMP_NUM_THREADS=16 there; sched_getaffinity shows the whole machine, whose
+    other cores run other jobs, and the box's rules size worker pools to that share), so
     the multi-thread leg runs on that share, capped at the usable cores."""
     cores = len(os.sched_getaffinity(0))
     return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))), cores
+
+
+def cgroup_cpu() -> str | None:
+    """The CPU quota of this job's cgroup (cgroup v2 cpu.max: "<quota> <period>" or "max ...")."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
@@ -295,7 +305,9 @@ def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
         "sample": f"{n} x {ln} B frames ({n * ln / 2**20:.0f} MiB, DRAM-resident), reference stack/pico_frame.c "
                   f"pico_checksum built -O3 (PERF=1), pthreads over contiguous frame ranges; "
                   f"{res[(threads, False)][1]} passes on {threads} threads, {res[(1, False)][1]} on 1 thread",
-        "cpu_model": cpu_model(), "usable_cores": cores,
+        "cpu_model": cpu_model(), "usable_cores": cores, "cgroup_cpu_max": cgroup_cpu(),
+        "share": f"{threads} threads = the host share the GPU box grants one GPU's job (OMP_NUM_THREADS); "
+                 f"sched_getaffinity shows {cores} cores of a machine other jobs share",
     }
     if (1, True) in res:
         out["Os_value"] = round(res[(threads, True)][0], 3)
