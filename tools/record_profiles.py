@@ -17,7 +17,7 @@ import shutil
 import statistics
 import sys
 
-CFGS = ("c1", "c2", "c2tx", "c2tx_nw", "c2nat", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3", "c3_64k", "c3_frag", "c4")
+CFGS = ("c1", "c2", "c2slot", "c2tx", "c2tx_nw", "c2nat", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3", "c3_64k", "c3_frag", "c4")
 
 
 def timed_kernel_rows(path):
@@ -39,6 +39,59 @@ def counter_medians(path):
     return kern, {k: statistics.median(v) for k, v in by.items()}
 
 
+def bench_line(path):
+    """The bench JSON line printed in a log (the profiled process's own line)."""
+    line = None
+    if os.path.exists(path):
+        for x in open(path, errors="replace"):
+            x = x.strip()
+            if x.startswith("{") and '"metric"' in x:
+                line = json.loads(x)
+    return line
+
+
+def timed_trace(src, tcfg, tag, bench, dst):
+    """Timed-region statistics of one rocprofv3 kernel trace (prof_<tcfg>_<tag>/): the last `steps`
+    dispatches of the timed kernel, against the bench line printed by the SAME traced process (its
+    HIP events ran under the profiler too) and against the unprofiled bench line of the round.
+    Writes <tcfg>_timed.txt (JSON) and <tcfg>_kernel_stats.csv; returns the trace mean (us)."""
+    d = os.path.join(src, f"prof_{tcfg}_{tag}")
+    if not os.path.isdir(d):
+        return None
+    shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{tcfg}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
+    rows = [r for r in rows if "csum" in r["Name"] or "reassemble" in r["Name"]]
+    tr = os.path.join(d, "run_kernel_trace.csv")
+    same = bench_line(os.path.join(src, f"prof_{tcfg}_{tag}.log"))
+    ref = same or bench
+    if not (rows and os.path.exists(tr) and ref):
+        return None
+    # the timed region: the last `steps` dispatches of the timed kernel (the stats file's average
+    # also holds the setup and verification launches of the same kernel)
+    top = max(rows, key=lambda r: int(r["Calls"]))["Name"]
+    ts = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]))
+                for x in csv.DictReader(open(tr)) if x["Kernel_Name"] == top)
+    last = ts[-ref["steps"]:]
+    trace_us = sum(e - b for b, e in last) / len(last) / 1e3
+    bracket_us = (last[-1][1] - last[0][0]) / len(last) / 1e3
+    algo = ref["roofline"]["algorithmic_bytes_per_launch"]
+    peak = ref["roofline"]["peak"]
+    out = {"kernel": top, "timed_dispatches": len(last), "dispatches_total": len(ts),
+           "trace_avg_us": round(trace_us, 3), "trace_bracket_us": round(bracket_us, 3),
+           "frac_from_trace": round(algo / (trace_us * 1e3) / peak, 4),
+           "frac_from_trace_bracket": round(algo / (bracket_us * 1e3) / peak, 4),
+           "algorithmic_bytes_per_launch": algo}
+    if same:
+        out["same_process_line_kernel_avg_us"] = same["roofline"]["kernel_avg_us"]
+        out["same_process_line_frac"] = same["roofline"]["frac"]
+        out["same_process_launch"] = same["config"]["launch"]
+    if bench:
+        out["unprofiled_line_kernel_avg_us"] = bench["roofline"]["kernel_avg_us"]
+        out["unprofiled_line_frac"] = bench["roofline"]["frac"]
+    open(os.path.join(dst, f"{tcfg}_timed.txt"), "w").write(json.dumps(out, indent=1) + "\n")
+    return trace_us
+
+
 def main() -> None:
     tag, rnd = sys.argv[1], sys.argv[2]
     src = "gpurun_out"
@@ -53,24 +106,11 @@ def main() -> None:
         if os.path.exists(f):
             shutil.copy(f, os.path.join(dst, f"bench_{cfg}.json"))
             bench = json.loads(open(f).read().strip().splitlines()[-1])
-        d = os.path.join(src, f"prof_{cfg}_{tag}")
         trace_us = None
-        if os.path.isdir(d):
-            shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{cfg}_kernel_stats.csv"))
-            rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
-            rows = [r for r in rows if "csum" in r["Name"] or "reassemble" in r["Name"]]
-            tr = os.path.join(d, "run_kernel_trace.csv")
-            if rows and os.path.exists(tr) and bench:
-                # the timed region: the last `steps` dispatches of the timed kernel (the stats file's
-                # average also holds the setup and verification launches of the same kernel)
-                top = max(rows, key=lambda r: int(r["Calls"]))["Name"]
-                ts = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]))
-                            for x in csv.DictReader(open(tr)) if x["Kernel_Name"] == top)
-                last = ts[-bench["steps"]:]
-                trace_us = sum(e - b for b, e in last) / len(last) / 1e3
-                open(os.path.join(dst, f"{cfg}_timed.txt"), "w").write(
-                    f"{top}\nlast {len(last)} dispatches of {len(ts)} in run_kernel_trace.csv: mean {trace_us:.3f} us "
-                    f"(bench.py HIP events, same run type: {bench['roofline']['kernel_avg_us']} us)\n")
+        for tcfg in ((cfg, "c1ng") if cfg == "c1" else (cfg,)):
+            t = timed_trace(src, tcfg, tag, bench, dst)
+            if tcfg == cfg:
+                trace_us = t
         r = {}
         for kind, c in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
             f = os.path.join(src, f"pmc_{kind}_{cfg}_{tag}", "run_counter_collection.csv")
