@@ -161,3 +161,23 @@ def test_range_over_128_frames_falls_back():
         np.testing.assert_array_equal(v.cpu().numpy(), wv)
         np.testing.assert_array_equal(u16(net_), wn)
         np.testing.assert_array_equal(u16(l4), wl)
+
+
+@pytest.mark.parametrize("n", [1, 3, 63, 65, 255, 257, 1000])
+@pytest.mark.parametrize("slot", [0, 2048])
+def test_partial_workgroups(n, slot):
+    """Batches that end inside a workgroup (waves with no frames take part in its barriers), dense
+    and COMPACT, with invalid and out-of-bounds descriptors mixed in."""
+    rng = np.random.default_rng(n + slot)
+    buf, desc = imix_v4(n, 40 + n)
+    if slot:
+        buf, desc = relayout(buf, desc, rng, slot=slot, jitter=3)
+    desc["len"][::7] = 10                               # too short: MALFORMED, not part of any range
+    desc["off"][5::11] = buf.size + 100                 # out of bounds
+    batch.set_launch_override(2, fpw=64)
+    for fl in (batch.F_TX, 0):
+        net, l4, v = batch.ipv4_checksum_batch(to_dev(buf), batch.desc_to_device(desc, "cuda:0"), n, flags=fl)
+        wn, wl, wv = O.batch_ipv4(buf, desc, tx=bool(fl))
+        np.testing.assert_array_equal(v.cpu().numpy(), wv)
+        np.testing.assert_array_equal(u16(net), wn)
+        np.testing.assert_array_equal(u16(l4), wl)
