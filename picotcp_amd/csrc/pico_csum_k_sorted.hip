@@ -1036,12 +1036,12 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // COMPACT: every position of the frame in its range's compacted sequence
     const uint32_t rel = compact ? 16u * csj + (relw & 15u) : relw;
     const uint32_t r = rel & 15u, hq = rel >> 4;
-    // COMPACT: the range's (cs, line) table into the loading wave's registers, through LDS (wave 0's
-    // stage, free until the loop)
+    // COMPACT: the range's (cs, line) table into the loading wave's registers, through LDS (the
+    // stages, free until the loop)
     uint32_t csab = 0u, lna = 0u, lnb = 0u, cs64 = 0u;
     if (compact) {                                     // workgroup-uniform
-        uint2* T = reinterpret_cast<uint2*>(&lds_all[0]);
-        static_assert(WPB * CMAXF * sizeof(uint2) <= sizeof(StreamLds), "range tables must fit a stage");
+        uint2* T = reinterpret_cast<uint2*>(&lds_all[0]);        // (over the stages, all free here)
+        static_assert(WPB * CMAXF * sizeof(uint2) <= WPB * sizeof(SortedWaveSmem<true>), "range tables must fit");
         if (valid) T[rg * CMAXF + idx] = make_uint2(csj, relw >> 4);
         __syncthreads();
         const uint2 e0 = T[wv * CMAXF + lane], e1 = T[wv * CMAXF + 64u + lane];
