@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2slot|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2slot|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c2ethmix|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
@@ -13,6 +13,7 @@ A step = one pass of the hot path over one batch resident in HBM:
   c2nat: the same datagrams through the NAT batch (address / port rewrite + full checksum recompute)
   c2v6: 256K IMIX+20 B IPv6/TCP datagrams, fused IPv6 pseudo-header RX verify
   c2eth: the C2 frames through the Ethernet front end (one launch: ethertype dispatch + RX verify)
+  c2ethmix: a mixed IPv4 / IPv6 Ethernet burst through the same front end
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
   c3_reasm: 4K x 64512 B datagrams reassembled from 1480 B fragments + TCP check in the same pass
   c3_reasm6: the same for IPv6 (1448 B fragments behind a fragment header)
@@ -90,6 +91,11 @@ CONFIGS = {
                   workload="C2 through the Ethernet front end (SURVEY 8f row 1): the 256K simple-IMIX IPv4/TCP "
                            "frames, descriptors at the Ethernet header, ethertype dispatch + destination-MAC filter "
                            "+ fused IPv4 / TCP RX verify in one launch"),
+    "c2ethmix": dict(kind="eth", frames=262144, mix=True,
+                     workload="C2 as a mixed Ethernet burst (SURVEY 8f rows 1 and 3): 256K frames, IPv4/TCP "
+                              "(simple IMIX {64,576,1500} B) and IPv6/TCP (IMIX + 20 B) in seeded random order "
+                              "back to back, one launch: ethertype dispatch + destination-MAC filter + fused "
+                              "IPv4 / IPv6 / TCP RX verify"),
     "c3_reasm": dict(kind="frag", frames=4096, frame_bytes=64512,
                      workload="C3 reassembly (SURVEY 8f row 4): 4K x 64512 B IPv4/TCP datagrams arriving as 1480 B "
                               "fragments (44 per datagram, 14 B Ethernet gap each), gathered into reassembled "
@@ -168,10 +174,18 @@ def make_c2v6(n, device, seed, keep_host=True):
 MAC = bytes.fromhex("02005e0a0b0c")
 
 
-def make_c2eth(n, device, seed, keep_host=True):
-    """The C2 datagrams as Ethernet frames addressed to MAC (descriptors at the frame start)."""
+def make_c2eth(n, device, seed, keep_host=True, mix=False):
+    """The C2 datagrams as Ethernet frames addressed to MAC (descriptors at the frame start); mix:
+    IPv4 and IPv6 (IMIX + 20 B) frames in seeded random order, back to back."""
     lens = synth.imix_lengths(n, seed)
     buf, net, avail = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
+    if mix:
+        b6, n6, a6, _ = synth.ipv6_batch((lens + 20).astype(np.uint32), seed=seed + 2, proto=6, eth=True)
+        kinds = np.random.default_rng(seed).integers(0, 2, n)
+        buf, st, fl = synth.interleave([(buf, net - np.uint64(14), avail + 14), (b6, n6 - np.uint64(14), a6 + 14)],
+                                       kinds)
+        net, avail = st + np.uint64(14), fl - 14
+        lens = avail
     e = net.astype(np.int64) - 14
     for k, b in enumerate(MAC):
         buf[e + k] = b
@@ -645,7 +659,8 @@ def main():
         n = cfg["frames"]
         ln = 0
         rot = a.rotate or rotation(n * (IMIX_MEAN + 14))
-        sets = [make_c2eth(n, dev, 500 + 13 * rank + i, keep_host=i == 0) for i in range(rot)]
+        sets = [make_c2eth(n, dev, 500 + 13 * rank + i, keep_host=i == 0, mix=bool(cfg.get("mix")))
+                for i in range(rot)]
         outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                  torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 

@@ -894,8 +894,22 @@ __device__ __forceinline__ uint32_t compact_line(uint32_t q, uint32_t csab, uint
 // carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for datagrams whose
 // transport follows the 40-byte header (descriptor seed 0; RX next header TCP / UDP / ICMPv6 --
 // anything else needs the extension-header walk: the sorted rounds).  ETH: the Ethernet batch
-// (MODE 3) for IPv4 behind the 14-byte header (ARP / dropped frames need no sums; a wave holding
-// an IPv6 frame falls back after the loop).
+// (MODE 3): IPv4 and IPv6 behind the 14-byte header (ARP / dropped frames need no sums; a wave
+// holding an IPv6 datagram that needs the extension-header walk falls back after the loop).
+// MODE 3 stream, an IPv6 frame: where the transport field the finish reads lies (relative to the
+// transport start; NONE = none) -- RX: the UDP crc (present?) when byte 9 (the reference's dispatch,
+// or with F_NXD the next header) says UDP, the ICMPv6 type; TX: the crc field to compute
+// (sorted_batch's MODE 2 rules)
+__device__ __forceinline__ uint32_t eth6_field(bool tx, uint32_t nh, uint32_t b9, bool nxd) {
+    if (!tx) {
+        const bool ref17 = !nxd && b9 == 17u;
+        if (nh == 6u && !ref17) return NONE;
+        if (nh == 17u || nh == 6u) return 6u;
+        return nh == 58u ? 0u : NONE;
+    }
+    return nh == 6u ? 16u : nh == 17u ? 6u : nh == 58u ? 2u : NONE;
+}
+
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
@@ -927,6 +941,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
     if (oob || lane >= cnt) { len = 0; off0 = 0; }
     const bool valid = len >= (V6 ? 40u : ETH ? 14u : 20u);  // shorter: MALFORMED, nothing to sum
+    const bool seeded = ETH && dcur.w != 0u;     // MODE 3 IPv6 with a stack-walked net_len: sorted rounds
     const uint32_t blen = valid ? len : 0u;
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
@@ -1119,6 +1134,30 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             b2 = rel + min(40u + plen, len);
             if (tx && nh == 6u && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }   // TCP crc: past the head chunks
         }
+        if (ETH && !pre && hq + 2u < qbo + SQ) {
+            // MODE 3: an IPv6 frame (ethertype 0x86DD) -- its addresses (the pseudo header), the
+            // transport and the field, all by prefixes (they lie past the head chunks)
+            uint32_t T[1];
+            window_words<1, true>(hw, r + 12u, T);
+            if ((T[0] & 0xFFFFu) == 0xDD86u) {
+                pre = true;
+                uint32_t H[3];
+                window_words<3, true>(hw, r + 14u, H);
+                const uint32_t ilen = len - 14u;
+                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+                const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
+                if (ilen >= 40u) {
+                    b0 = rel + 14u + 8u;
+                    b1 = rel + 54u;
+                    b2 = rel + 14u + min(40u + plen, ilen);
+                    const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);
+                    if (xo != NONE && 40u + xo < ilen) {
+                        x0 = rel + 54u + xo;
+                        x1 = x0 + min(2u, ilen - 40u - xo);
+                    }
+                }
+            }
+        }
         if (!V6 && !pre && hq + (ETH ? 2u : 1u) < qbo + SQ) {
             pre = true;
             uint32_t H[3];
@@ -1222,7 +1261,11 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     uint32_t verdict = V_MALFORMED, hl = 0, tl = 0, proto = 0, ipcrc = 0, pseudo = 0, hdr20 = 0, post = 0;
     uint32_t l2v = natm ? NS_SKIP : 0u, nop = 0, nnw = 0;   // NAT: state, old / new port (frame pairing)
     bool parsed = false, l4_needed = false, hasx = false, nat_opt = false, ip4 = valid, eth6 = false;
+    bool walk6 = false;
     const uint32_t ilen = len - L2;
+    // MODE 3 IPv6 frames (as sorted_batch's MODE 3 -> MODE 2 path, seed 0, no extension header):
+    // transport sum, field, pseudo header from the prefixes
+    uint32_t v6sum = 0u, v6x = 0u;
     if constexpr (ETH) {
         // pico_ethernet_receive (pico_ethernet.c:180-235): destination filter, ethertype, version
         ip4 = false;
@@ -1236,13 +1279,53 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                               (m0 == 0xFFFFFFFFu && m1 == 0xFFFFu);
             if (!mine) l2v = V_DROP_L2;
             else if (et == 0x0608u) l2v = V_ARP;
-            else if (et == 0xDD86u) eth6 = true;         // IPv6: the sorted rounds
+            else if (et == 0xDD86u) {                    // IPv6 (pico_ethernet.c:162-176)
+                if (ilen != 0u) {
+                    uint32_t V[1];
+                    window_words<1, true>(hw, r + 14u, V);
+                    if ((V[0] & 0xF0u) != 0x60u) l2v = V_DROP_L2;
+                    else eth6 = true;
+                }
+            }
             else if (et != 0x0008u) l2v = V_DROP_L2;
             else if (ilen != 0u) {
                 uint32_t V[1];
                 window_words<1, true>(hw, r + 14u, V);
                 if ((V[0] & 0xF0u) != 0x40u) l2v = V_DROP_L2;
                 else ip4 = true;
+            }
+        }
+    }
+    walk6 = eth6 && seeded;
+    if (ETH && eth6 && ilen >= 40u && !seeded) {
+        uint32_t H[3];
+        window_words<3, true>(hw, r + 14u, H);
+        tl = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+        proto = (H[1] >> 16) & 0xFFu;
+        const uint32_t b9 = (H[2] >> 8) & 0xFFu;
+        if (!tx && proto != 6u && proto != 17u && proto != 58u) {
+            walk6 = true;                                // extension headers: the sorted rounds
+        } else if (40u + tl <= ilen) {
+            const bool odd6 = r & 1u;
+            pseudo = pairing(P1 - P0, odd6) + (((tl & 0xFFu) << 8) | (tl >> 8)) + (proto << 8);
+            parsed = true;
+            verdict = 0;
+            const uint32_t xo = eth6_field(tx, proto, b9, (p.flags & F_NXD) != 0u);
+            if (!tx) {
+                ipcrc = b9;
+                if (xo == 6u && 48u > ilen) { parsed = false; verdict = V_MALFORMED; }
+                else if (xo == 0u && 41u > ilen) { parsed = false; verdict = V_MALFORMED; }
+                else l4_needed = proto == 6u || proto == 17u || proto == 58u;
+            } else if (xo != NONE) {
+                if (tl < (proto == 6u ? 20u : proto == 17u ? 8u : 4u)) { parsed = false; verdict = V_MALFORMED; }
+                else l4_needed = true;
+            }
+            if (xo != NONE) {
+                const uint32_t xe6 = P4 - P3;
+                v6x = odd6 ? ((xe6 >> 8) | (xe6 << 8)) & 0xFFFFu : xe6;
+                v6sum = tx ? pairing(P2 - P1 - xe6, odd6) + v6x : pairing(P2 - P1, odd6);
+            } else {
+                v6sum = pairing(P2 - P1, odd6);
             }
         }
     }
@@ -1310,7 +1393,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             }
         }
     }
-    if (__builtin_amdgcn_ballot_w64(ETH ? eth6 : nat_opt)) return false;
+    if (__builtin_amdgcn_ballot_w64(ETH ? walk6 : nat_opt)) return false;
     const bool odd = r & 1u;
     // the field (frame pairing xp, even domain xe): from the head window, or with options by prefixes
     uint32_t xe = 0, xp = 0;
@@ -1331,13 +1414,14 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint32_t tsum = tx ? pairing(P2 - P1 - xe - noe, odd) + xp + nnw : pairing(P2 - P1, odd);
     const uint32_t opt = hl > 20u ? pairing(P1 - P0, odd) : 0u;
     // the IPv4 header's line and offset (finish stores relative to it)
-    const uint32_t ri = (r + L2) & 15u;
-    const uint64_t a0off = valid ? off + L2 - ri : 0u;
+    // (MODE 3 IPv6: the transport's line and offset; finish stores the field relative to it)
+    const uint32_t ri = (r + (eth6 ? 54u : L2)) & 15u;
+    const uint64_t a0off = valid ? off + (eth6 ? 54u : L2) - ri : 0u;
     if (lane < cnt)
-        finish_frame<ETH ? 3 : 1>(p, f0 + lane, tx, hdr20 + opt + tsum, xp, opt,
+        finish_frame<ETH ? 3 : 1>(p, f0 + lane, tx, eth6 ? v6sum : hdr20 + opt + tsum, eth6 ? v6x : xp, opt,
                         make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, ri),
                         make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
-                                       (proto << 8) | (tl << 16),
+                                       (eth6 ? 128u : 0u) | (proto << 8) | (tl << 16),
                                    hl | (l2v << 8) | (ipcrc << 16), pseudo, hdr20),
                         NONE);
     STAMP(3);

@@ -198,6 +198,28 @@ ETH_KINDS = ("ipv4_tcp", "ipv4_udp", "ipv4_icmp", "ipv6_tcp", "ipv6_udp", "ipv6_
              "ipv6_dst_tcp")
 
 
+def interleave(parts, kinds: np.ndarray):
+    """One burst from several packed ones: parts[k] = (buffer, frame starts, frame bytes); frame i of
+    the result is the next unused frame of parts[kinds[i]], back to back.  Returns (buffer, starts
+    uint64, bytes uint32)."""
+    kinds = np.asarray(kinds)
+    n = kinds.size
+    lens = np.zeros(n, np.int64)
+    src = np.zeros(n, np.int64)                      # source start, in the concatenated parts
+    base = 0
+    for k, (b, st, ln) in enumerate(parts):
+        sel = np.flatnonzero(kinds == k)
+        assert sel.size <= st.size
+        lens[sel] = np.asarray(ln, np.int64)[:sel.size]
+        src[sel] = np.asarray(st, np.int64)[:sel.size] + base
+        base += b.size
+    cat = np.concatenate([b for b, _, _ in parts])
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    seg = np.repeat(np.arange(n), lens)
+    idx = (src - starts)[seg] + np.arange(int(lens.sum()))
+    return cat[idx], starts.astype(np.uint64), lens.astype(np.uint32)
+
+
 def eth_batch(n: int, seed: int = 11, mac: bytes = bytes.fromhex("02005e0a0b0c")):
     """A mixed Ethernet burst as a TAP / pico_device RX ring delivers it: n frames, each
     with a 14-byte Ethernet header, of the kinds in ETH_KINDS (IPv4 / IPv6 datagrams in

@@ -8,7 +8,7 @@ O=$R/gpurun_out
 TAG=${1:-run}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for c in ${CFGS:-c1 c2 c2slot c2tx c2tx_nw c2nat c2v6 c2eth c3_reasm c3_reasm6}; do
+for c in ${CFGS:-c1 c2 c2slot c2tx c2tx_nw c2nat c2v6 c2eth c2ethmix c3_reasm c3_reasm6}; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_${c}_$TAG -o run --output-format csv -- python3 $R/bench.py --config $c --steps 20 --warmup 2 --no-cpu --no-e2e --no-verify > $O/pmc_fetch_${c}_$TAG.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_${c}_$TAG -o run --output-format csv -- python3 $R/bench.py --config $c --steps 20 --warmup 2 --no-cpu --no-e2e --no-verify > $O/pmc_write_${c}_$TAG.log 2>&1
   echo "pmc $c ok"

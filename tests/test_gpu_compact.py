@@ -181,3 +181,52 @@ def test_partial_workgroups(n, slot):
         np.testing.assert_array_equal(v.cpu().numpy(), wv)
         np.testing.assert_array_equal(u16(net), wn)
         np.testing.assert_array_equal(u16(l4), wl)
+
+
+def mixed_eth(n, seed, mac):
+    """IPv4/TCP and IPv6/TCP (or UDP / ICMPv6) Ethernet frames in random order, back to back."""
+    rng = np.random.default_rng(seed)
+    lens = synth.imix_lengths(n, seed)
+    b4, n4, a4 = synth.ipv4_batch(lens, seed=seed + 1, proto=6, eth=True)
+    parts = [(b4, n4 - np.uint64(14), a4 + 14)]
+    for k, (pr, kw) in enumerate(((6, {}), (17, {}), (58, dict(icmp_type=135)))):
+        b6, n6, a6, _ = synth.ipv6_batch((lens + 20).astype(np.uint32), seed=seed + 2 + k, proto=pr, eth=True, **kw)
+        parts.append((b6, n6 - np.uint64(14), a6 + 14))
+    kinds = rng.choice(4, n, p=[0.5, 0.3, 0.1, 0.1])
+    buf, st, fl = synth.interleave(parts, kinds)
+    for k, b in enumerate(mac):
+        buf[st.astype(np.int64) + k] = b
+    buf[st[::97].astype(np.int64) + 23] = 17            # some IPv6 byte-9 = 17 (the reference's UDP dispatch)
+    return buf, batch.make_desc(st, fl)
+
+
+@pytest.mark.parametrize("layout", [None, dict(slot=2048, jitter=1)])
+@pytest.mark.parametrize("fpw", [0, 64, 17])
+def test_mixed_ethernet_stream(layout, fpw):
+    """A mixed IPv4 / IPv6 Ethernet burst in one launch: the IPv6 frames are streamed too (their
+    addresses, transport and field by prefixes) -- TX written in place, then RX with both dispatches."""
+    mac = bytes.fromhex("02005e0a0b0c")
+    rng = np.random.default_rng(fpw + 5)
+    buf, desc = mixed_eth(20000, 71 + fpw, mac)
+    if layout:
+        buf, desc = relayout(buf, desc, rng, **layout)
+    if fpw:
+        batch.set_launch_override(2, fpw=fpw)
+    d_desc = batch.desc_to_device(desc, "cuda:0")
+    d_buf = to_dev(buf)
+    net, l4, v = batch.eth_checksum_batch(d_buf, d_desc, desc.size, flags=batch.F_TX | batch.F_WRITE)
+    torch.cuda.synchronize()
+    wn, wl, wv = O.batch_eth(buf, desc, tx=True)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    np.testing.assert_array_equal(u16(net), wn)
+    np.testing.assert_array_equal(u16(l4), wl)
+    got = d_buf.cpu().numpy()
+    got[rng.integers(0, got.size, 2000)] ^= 0x04
+    for nx in (False, True):
+        net, l4, v = batch.eth_checksum_batch(to_dev(got), d_desc, desc.size, mac=mac,
+                                              flags=batch.F_NXTHDR_DISPATCH if nx else 0)
+        wn, wl, wv = O.batch_eth(got, desc, mac=mac, nxthdr_dispatch=nx)
+        np.testing.assert_array_equal(v.cpu().numpy(), wv)
+        np.testing.assert_array_equal(u16(net), wn)
+        np.testing.assert_array_equal(u16(l4), wl)
+        assert ((wv & 0x7F) == 1).sum() > 15000 and (wv & 128).sum() > 0
