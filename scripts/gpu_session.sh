@@ -8,7 +8,7 @@ O=$R/gpurun_out
 TAG=${1:-r04a}
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1
 echo "tests ok"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1
 echo "smoke ok"
