@@ -387,6 +387,12 @@ int pico_eth_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, ui
                                  uint16_t *out_net, uint16_t *out_transport, uint8_t *verdict);
 int pico_csum_host_register(void *ptr, uint64_t bytes);
 int pico_csum_host_unregister(void *ptr);
+/* Zero-copy ingress (the batch form of pico_stack_recv_zerocopy, stack/pico_stack.c:479-527: the
+ * driver's buffer is used where it lies): the device's address of registered host memory (NULL and
+ * pico_csum_last_error() if ptr is not registered).  Any layer-2 batch takes it as d_base -- and as
+ * d_desc / the outputs, registered the same way -- and the kernel then reads the frames over PCIe in
+ * place, with no staging copy. */
+void *pico_csum_host_device_pointer(void *ptr);
 
 /* ---------------------------------------------------------------- misc */
 

@@ -41,6 +41,7 @@ EXPORTED = (
     "pico_eth_checksum_batch_host",
     "pico_csum_host_register",
     "pico_csum_host_unregister",
+    "pico_csum_host_device_pointer",
     "pico_csum_abi_version",
     "pico_csum_last_error",
     "pico_csum_set_launch_override",
@@ -109,6 +110,7 @@ def load() -> ctypes.CDLL:
     sig("pico_eth_checksum_batch_host", ctypes.c_int, vp, vp, u64, vp, u32, u32, vp, vp, vp, vp)
     sig("pico_csum_host_register", ctypes.c_int, vp, u64)
     sig("pico_csum_host_unregister", ctypes.c_int, vp)
+    sig("pico_csum_host_device_pointer", vp, vp)
     sig("pico_csum_abi_version", ctypes.c_int)
     sig("pico_csum_last_error", ctypes.c_char_p)
     sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32, u32, u32, u32)

@@ -583,6 +583,17 @@ int pico_csum_host_register(void *ptr, uint64_t bytes)
     return 0;
 }
 
+void *pico_csum_host_device_pointer(void *ptr)
+{
+    void *d = NULL;
+    hipError_t e = hipHostGetDevicePointer(&d, ptr, 0);
+    if (e != hipSuccess) {
+        fail(PICO_CSUM_EINVAL, "hipHostGetDevicePointer: %s (register the memory first)", hipGetErrorString(e));
+        return NULL;
+    }
+    return d;
+}
+
 int pico_csum_host_unregister(void *ptr)
 {
     hipError_t e = hipHostUnregister(ptr);
