@@ -1077,7 +1077,10 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
 #pragma unroll
     for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
     // boundaries (span byte positions, 0 = none): options start, transport start / end, field
-    uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    // MODE 3: b0 starts at an IPv6 datagram's addresses (frame + 22), which can lie in the step
+    // before the one that completes the header parse -- taken for every frame until the parse says
+    // IPv4 (then the options start, or none)
+    uint32_t b0 = ETH && valid ? rel + 22u : 0u, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
     uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
     bool pre = !valid;
     uint32_t base = 0;
@@ -1170,6 +1173,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             const uint32_t pr = (H[2] >> 8) & 0xFFu;
             b1 = rel + L2 + min(hl, ilen);
             b2 = rel + L2 + min(hl + tl, ilen);
+            b0 = 0u;
             if (hl > 20u) {                  // options: their sum and the field, by prefixes too
                 b0 = rel + L2 + 20u;
                 const uint32_t xo = !tx ? (pr == 17u ? 6u : 0u) : pr == 6u ? 16u : pr == 1u ? 2u : 0u;
