@@ -232,16 +232,6 @@ static int desc_fpw(uint32_t n, uint32_t *fpw)
     return 0;
 }
 
-/* Ablation bits for measurement builds of the sorted-rounds kernel (-DPICO_CSUM_AB, see
- * pico_csum_dev.h): PICO_CSUM_ABLATE bit 1 = skip the rounds, 2 = skip the head-window loads,
- * 4 = skip the IPv4 TX crc writes; passed in flags bits 8+, which the public API rejects.  The
- * product library compiles them out. */
-static uint32_t ablate_flags(void)
-{
-    const char *e = getenv("PICO_CSUM_ABLATE");
-    return e ? ((uint32_t)strtoul(e, NULL, 0) & 0xFFu) << 8 : 0u;
-}
-
 /* Device discovery runs once per process (pthread_once); compute-unit counts are read
  * per device, for the device current on the calling thread at launch. */
 #define MAX_DEVS 64
@@ -304,7 +294,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
         return fail(PICO_CSUM_EINVAL, "F_WRITE needs crc_off >= 0");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags | ablate_flags(),
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags,
                                                  d_out, d_bad, NULL, NULL, NULL, fpw, 0, stream),
                          "pico_checksum_batch_dev");
 }
@@ -353,7 +343,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags | ablate_flags(), NULL,
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv4_checksum_batch_dev");
 }
@@ -375,7 +365,7 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     /* the IPv4 kernel in TX + in-place mode with the NAT stage; the records' address rides in the
      * launcher's 64-bit MAC argument (used as a MAC by the Ethernet mode only) */
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1,
-                                                 PICO_CSUM_F_TX | PICO_CSUM_F_WRITE | KF_NAT | ablate_flags(), NULL,
+                                                 PICO_CSUM_F_TX | PICO_CSUM_F_WRITE | KF_NAT, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw,
                                                  (uint64_t)(uintptr_t)d_nat, stream),
                          "pico_ipv4_nat_batch_dev");
@@ -401,7 +391,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_NXTHDR_DISPATCH is an RX option");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags | ablate_flags(), NULL,
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL,
                                                  NULL, NULL, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv6_checksum_batch_dev");
 }
@@ -432,7 +422,7 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
             mac48 |= (uint64_t)mac[i] << (8 * i);
         flags |= KF_MACF;
     }
-    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags | ablate_flags(), NULL, NULL,
+    return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags, NULL, NULL,
                                                  d_out_net, d_out_transport, d_verdict, fpw, mac48, stream),
                          "pico_eth_checksum_batch_dev");
 }

@@ -248,14 +248,6 @@ constexpr uint32_t F_NXD = 0x8u;        // PICO_CSUM_F_NXTHDR_DISPATCH (IPv6 RX)
 // phase-1 outcomes applied after the IPv4 header check (sorted kernel)
 constexpr uint32_t PV_DROP = 1u, PV_FRAG = 2u;
 
-// Phase ablations for measurement builds only (-DPICO_CSUM_AB, flags bits 8-10 from the
-// PICO_CSUM_ABLATE environment variable); the product library compiles them out.
-#ifdef PICO_CSUM_AB
-#define ABLATE(p, bit) (((p).flags & (bit)) != 0u)
-#else
-#define ABLATE(p, bit) false
-#endif
-
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
 }

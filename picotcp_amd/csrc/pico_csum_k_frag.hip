@@ -28,8 +28,7 @@
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
 //      16-byte units on the output's 16-byte lines, 3 x 64 units per wave per step (two 1480-byte
 //      payloads): one byte-unaligned 16-byte load per unit through one buffer window over both
-//      payloads (out-of-range slots read zeros, no branches; FRAG_UNALIGNED 0 builds load two
-//      aligned lines and shift, the second taken from the next lane by DPP); v_dot2 sums on the
+//      payloads (out-of-range slots read zeros, no branches); v_dot2 sums on the
 //      fly (every unit is a whole number of checksum words); a
 //      workgroup reduction at the end.  Software-pipelined over two register sets: the next
 //      step's loads are issued before this step's stores, and the stores are a fixed sequence
@@ -40,7 +39,7 @@
 //      Measured (profiles/r03): one fragment per step 154.6 / 171.9 us (c3_reasm / c3_reasm6),
 //      pairs 148.9 / 162.0 us (ab_frag2.txt), pipelined 144.8 / 153.4 us (ab_frag_pipe.txt);
 //      without the stores 89.5 / 97.6 us, without the gather 18.2 / 26.2 us (ab_frag_ablate.txt,
-//      FRAG_AB measurement builds); one wave per datagram at 4096 datagrams 145.6 / 154.8 us vs
+//      measurement builds of round 3); one wave per datagram at 4096 datagrams 145.6 / 154.8 us vs
 //      149.0 / 157.9 at four (ab_frag_wpd.txt).  Stores keep the default cache policy: nt 194 /
 //      201 us, sc1 244 / 255 us (ab_frag_saux.txt).  Units on the output's 16-byte lines (every
 //      interior unit one aligned b128 store, 5 store instructions per slot instead of 8): 130.6 /
@@ -70,18 +69,6 @@ __device__ __forceinline__ uint32_t sel4s(uint32_t q, uint32_t a, uint32_t b, ui
     return (q & 2u) ? hi : lo;
 }
 
-#ifndef FRAG_WPD_FORCE
-#define FRAG_WPD_FORCE 0   // measurement builds only: waves per datagram (1, 4) regardless of batch size
-#endif
-#ifndef FRAG_C1DPP
-#define FRAG_C1DPP 1    // a unit's second input line from the next lane's first (DPP) instead of a second load
-#endif
-#ifndef FRAG_UNALIGNED
-#define FRAG_UNALIGNED 1   // one byte-unaligned 16-byte load per unit (0: two aligned loads + shift)
-#endif
-#ifndef FRAG_AB
-#define FRAG_AB 0       // measurement builds only: 1 = no gather stores, 2 = no gather
-#endif
 #ifndef FRAG_MAX_N
 #define FRAG_MAX_N 512
 #endif
@@ -300,12 +287,13 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
         constexpr int U = 3;                   // 64-unit slots per step: two 1480 B payloads
         struct Step {                          // plain scalars (a buffer resource inside a copied
             uint64_t wlo;                      // struct ends up in an LDS-promoted alloca)
-            uint32_t wsz, i, i2, va, vb, na, nt, ta, tb, ata, atb, sa, sb, oa, ob, u0, valid;
+            uint32_t wsz, i, i2, va, vb, na, nt, ta, tb, ata, atb, oa, ob, u0, valid;
         };
         // Units follow the OUTPUT's 16-byte lines: a fragment whose place starts o = (t + offset) & 15
         // bytes into a line has units [0, (o + tl + 15) / 16), unit u = its bytes [16 u - o, 16 u - o + 16),
         // so every unit but its first and last is one aligned 16-byte store (units on the payload's own
-        // grid gave dword stores for every unit of a fragment at 8 mod 16).  The loads take the shift.
+        // grid gave dword stores for every unit of a fragment at 8 mod 16).  The loads take the shift:
+        // one byte-unaligned 16-byte load per unit.
         // fragment A = i and (if any) B = i2: units [0, na) are A's, [na, nt) B's, read through
         // one buffer window over both payloads' 16-byte lines when they lie within 1 GiB of each
         // other (else B waits for the next step)
@@ -317,7 +305,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
             st.i = st.i2 = i;
             st.wlo = tb;
             st.wsz = 0;
-            st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.sa = st.sb = st.oa = st.ob = 0;
+            st.va = st.vb = st.na = st.nt = st.ta = st.tb = st.ata = st.atb = st.oa = st.ob = 0;
             if (!st.valid) return st;
             st.ata = field(ck, i) & 0xFFFFu;
             st.oa = (uint32_t)((tb + st.ata) & 15u);
@@ -348,8 +336,6 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
             st.wsz = (uint32_t)(((whi + 15u) & ~15ull) - wlo + 16u);
             st.va = (uint32_t)(sa - wlo);
             st.vb = (uint32_t)(sb - wlo);
-            st.sa = (uint32_t)(sa & 15u);
-            st.sb = (uint32_t)(sb & 15u);
             st.nt = st.na + nb;
             return st;
         };
@@ -359,57 +345,26 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
             else n = make_pair((c.i2 == c.i ? c.i : c.i2) + 1u);
             return n;
         };
-        auto issue = [&](const Step& st, uint4 (&c0)[U], uint4 (&c1)[U]) {
+        auto issue = [&](const Step& st, uint4 (&c0)[U]) {
             const Window win = make_window(st.wlo, st.wsz);   // empty for an invalid step
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const uint32_t x = st.u0 + 64u * k + lane;
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x, v = inb ? st.vb : st.va;
-                const bool ok = st.valid && x < st.nt, sh = (inb ? st.sb : st.sa) != 0u;
-                c0[k] = load_win<true>(win, ok ? v - (v & 15u) + 16u * u : WIN_OOB);
-#if FRAG_UNALIGNED
-                c0[k] = load_win<true>(win, ok ? v + 16u * u : WIN_OOB);   // A/B only: byte-unaligned loads
-                c1[k] = make_uint4(0, 0, 0, 0);
-                continue;
-#endif
-#if FRAG_C1DPP
-                // the unit's second line is the next lane's first (process() takes it by DPP), except
-                // in lane 63 and in a fragment's last unit: only those lanes load it
-                const bool own = lane == 63u || x + 1u == st.na || x + 1u == st.nt;
-                c1[k] = load_win<true>(win, ok && sh && own ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
-#else
-                c1[k] = load_win<true>(win, ok && sh ? v - (v & 15u) + 16u * u + 16u : WIN_OOB);
-#endif
+                const bool ok = st.valid && x < st.nt;
+                c0[k] = load_win<true>(win, ok ? v + 16u * u : WIN_OOB);   // byte-unaligned: the unit's 16 bytes
             }
         };
-        auto process = [&](const Step& st, const uint4 (&c0)[U], const uint4 (&c1)[U]) {
+        auto process = [&](const Step& st, const uint4 (&c0)[U]) {
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const uint32_t x = st.u0 + 64u * k + lane;
                 const bool ok = x < st.nt;
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x;
-                const uint32_t s = FRAG_UNALIGNED ? 0u : inb ? st.sb : st.sa, q = s >> 2, sbb = s & 3u;
                 const uint32_t tl = inb ? st.tb : st.ta, at = inb ? st.atb : st.ata, o = inb ? st.ob : st.oa;
-#if FRAG_UNALIGNED
-                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, 0u, 0u, 0u, 0u};
-#elif FRAG_C1DPP
-                const bool own = lane == 63u || x + 1u == st.na || x + 1u == st.nt;
-                auto shl1 = [](uint32_t v) {            // DPP wave_shl:1 -- lane l gets lane l + 1's v
-                    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-                };
-                const uint4 nx = make_uint4(shl1(c0[k].x), shl1(c0[k].y), shl1(c0[k].z), shl1(c0[k].w));
-                const uint4 e1 = own ? c1[k] : nx;
-                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, e1.x, e1.y, e1.z, e1.w};
-#else
-                const uint32_t D[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-#endif
-                uint32_t xw[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w)                 // bytes [s, s + 16) of the 32 loaded
-                    xw[w] = __builtin_amdgcn_alignbyte(sel4s(q, D[w + 1], D[w + 2], D[w + 3], D[w + 4]),
-                                                       sel4s(q, D[w], D[w + 1], D[w + 2], D[w + 3]), sbb);
+                uint32_t xw[4] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w};
                 // the unit's fragment bytes are [lo, hi) of its 16 (lo = o in unit 0, a multiple of 4;
                 // hi < 16 only in the last unit); the rest is the neighbours' and reads as zero
                 const uint32_t lo = ok && u == 0u ? o : 0u, hi = ok ? min(16u, o + tl - 16u * u) : 0u;
@@ -422,7 +377,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 // one aligned 16-byte store; else its whole dwords [a, a + c) as a b64 and / or a b32,
                 // then a last partial dword's bytes as a b16 and / or a b8
                 const uint32_t ou = at + 16u * u - o;       // the unit's place (16-byte aligned in t)
-                const uint32_t so = FRAG_AB == 1 ? ou | WIN_OOB : ou;   // (measurement builds: no stores)
+                const uint32_t so = ou;
                 const bool whole = lo == 0u && hi == 16u;
                 const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
                 const uint32_t nr = hi > lo ? hi & 3u : 0u;
@@ -450,23 +405,20 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 }
             }
         };
-        uint4 a0[U], a1[U], b0[U], b1[U];
+        uint4 a0[U], b0[U];
         Step cur = make_pair(0u);
-#if FRAG_AB == 2
-        cur.valid = 0;
-#endif
         if (cur.valid) {
-            issue(cur, a0, a1);
+            issue(cur, a0);
             for (;;) {                         // two steps per trip, alternating register sets
                 const Step n1 = next_step(cur);
-                issue(n1, b0, b1);
+                issue(n1, b0);
                 __builtin_amdgcn_sched_barrier(0);   // the next step's loads stay ahead of these stores
-                process(cur, a0, a1);
+                process(cur, a0);
                 if (!n1.valid) break;
                 const Step n2 = next_step(n1);
-                issue(n2, a0, a1);
+                issue(n2, a0);
                 __builtin_amdgcn_sched_barrier(0);
-                process(n1, b0, b1);
+                process(n1, b0);
                 if (!n2.valid) break;
                 cur = n2;
             }
@@ -540,7 +492,7 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     // waves per datagram: 4 each while the batch is small, 1 each once the batch fills the chip's
     // one-wave workgroup slots (16 per CU, LDS-bound): c3_reasm (4096 datagrams) 145.6 vs 149.0 us
     // at 4 waves, 2 waves 165.0 us (2560 slots: a partial second round), ab_frag_wpd.txt
-    const int wpd = FRAG_WPD_FORCE ? FRAG_WPD_FORCE : n_dgram >= 3072u ? 1 : 4;
+    const int wpd = n_dgram >= 3072u ? 1 : 4;
     const dim3 grid(n_dgram), block(64 * wpd);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (wpd == 1) {

@@ -265,7 +265,7 @@ __device__ __forceinline__ void finish_frame(const FlatArgs& p, uint64_t idx, bo
                         store_le(fp + hl + (ndir == 1u ? 0u : 2u), rw.y, 2);
                     }
                 }
-            } else if (tx && (p.flags & 1u) && !ABLATE(p, 0x400u)) {
+            } else if (tx && (p.flags & 1u)) {
                 if (verdict == V_ACCEPT) {
                     store_crc(fp + 10, net);
                     if ((proto == 6u || proto == 1u) && l4_needed) store_crc(fp + hl + (proto == 6u ? 16u : 2u), l4);
@@ -357,7 +357,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
         // (64-byte IMIX frames), the whole datagram: their sums are taken here and the
         // rounds start behind the window (or are skipped).
         constexpr uint32_t HDR = IPV6 ? 40u : IPV4 ? 20u : 14u;
-        nlh = len >= HDR && !ABLATE(p, 0x200u) ? min(HW, (r + len + 15u) >> 4) : 0u;
+        nlh = len >= HDR ? min(HW, (r + len + 15u) >> 4) : 0u;
         {
             // Buffer loads through a window over the batch (from base's 16-byte line to
             // base_len rounded up -- the bytes load_chunk may touch -- at most 2 GiB, from
@@ -741,10 +741,7 @@ __device__ __forceinline__ void sorted_batch(const FlatArgs& p, SortedWaveLds& L
 
     // ---- 3. rounds over the sorted frames
     RawArgs ra{p.base, p.base_len, nullptr, 0, 0, 0, 0, -1, 0u, 0u, nullptr, nullptr};
-    // measurement builds only (ABLATE, -DPICO_CSUM_AB): bit 8 skips the rounds (times phases 1,
-    // 2, 4); bit 9 skips the head-window loads (then nothing parses: descriptors + stores
-    // alone); bit 10 skips the IPv4 TX in-place crc writes
-    if (m && !ABLATE(p, 0x100u)) {
+    if (m) {
         if (any_odd) {
             if (any_xo) sorted_rounds<CPL, true, NT, true, SMALL>(ra, L, e, m);
             else sorted_rounds<CPL, true, NT, false, SMALL>(ra, L, e, m);
