@@ -993,19 +993,40 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // range of frame j: its frame-order byte prefix in WPB equal parts (whole frames)
     const uint32_t inc = (uint32_t)wave_incl<0>((int)blen);
     const uint32_t ex = exw + inc - blen;
-    const uint32_t rg = valid ? min(WPB - 1u, (uint32_t)(((uint64_t)ex * WPB) / total)) : 0u;
+    uint32_t rg = 0u;                                   // floor(WPB * ex / total), by compares
+#pragma unroll
+    for (uint32_t k = 1; k < WPB; ++k) rg += valid && (uint64_t)ex * WPB >= (uint64_t)k * total ? 1u : 0u;
     // frame-order prefixes of the frames' lines and of the valid frames (COMPACT)
     const uint32_t exch = exc + (uint32_t)wave_incl<0>((int)cch) - cch;
     const uint64_t vbm = __builtin_amdgcn_ballot_w64(valid);
     const uint32_t exfn = exn + __builtin_amdgcn_mbcnt_hi((uint32_t)(vbm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vbm, 0u));
-    if (valid && !far) {
-        atomicMin(&W.rmin[rg], (int)dl);
-        atomicMax(&W.rmax[rg], (int)dh);
-        atomicAdd(&W.rsum[rg], len);
-        atomicAdd(&W.rnc[rg], cch);
-        atomicAdd(&W.rcnt[rg], 1u);
-        atomicMin(&W.rc0[rg], exch);
-        atomicMin(&W.rn0[rg], exfn);
+    // per range: wave reductions, then one lane's LDS atomics (the LDS is the CU's: 64 lanes'
+    // atomics on one address from each of 16 waves serialise for microseconds). rg rises with
+    // the frame index, so the wave's frames touch the ranges of its first to its last valid frame.
+    if (vbm) {
+        const uint32_t kf = (uint32_t)__builtin_amdgcn_readlane((int)rg, __builtin_ffsll((long long)vbm) - 1);
+        const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)rg, 63 - __builtin_clzll(vbm));
+        for (uint32_t k = kf; k <= kl; ++k) {
+            const bool m = valid && rg == k;
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(m);
+            if (!bm) continue;
+            const int first = __builtin_ffsll((long long)bm) - 1;
+            const int mn_k = __builtin_amdgcn_readlane(wave_incl<1>(m ? (int)dl : 0x7FFFFFFF), 63);
+            const int mx_k = __builtin_amdgcn_readlane(wave_incl<2>(m ? (int)dh : -0x7FFFFFFF), 63);
+            const uint32_t rs_k = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(m ? (int)len : 0), 63);
+            const uint32_t nc_k = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(m ? (int)cch : 0), 63);
+            const uint32_t c0_k = (uint32_t)__builtin_amdgcn_readlane((int)exch, first);
+            const uint32_t n0_k = (uint32_t)__builtin_amdgcn_readlane((int)exfn, first);
+            if (lane == 0) {
+                atomicMin(&W.rmin[k], mn_k);
+                atomicMax(&W.rmax[k], mx_k);
+                atomicAdd(&W.rsum[k], rs_k);
+                atomicAdd(&W.rnc[k], nc_k);
+                atomicAdd(&W.rcnt[k], (uint32_t)__builtin_popcountll(bm));
+                atomicMin(&W.rc0[k], c0_k);
+                atomicMin(&W.rn0[k], n0_k);
+            }
+        }
     }
     if (__builtin_amdgcn_ballot_w64(far) && lane == 0) W.far = 1u;
     __syncthreads();

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=["c2", "c2tx", "c2v6", "c2raw"])
     ap.add_argument("--n", type=int, default=262144)
     ap.add_argument("--rotate", type=int, default=12)
+    ap.add_argument("--wpb", type=int, default=4, help="waves per workgroup of the kernel")
     a = ap.parse_args()
     lib = _lib.load()
     lib.pico_csum_diag_set_stamps.restype = ctypes.c_int
@@ -72,11 +73,11 @@ def main():
         launch(100 + rep)
         torch.cuda.synchronize()
         t = st.cpu().numpy().reshape(-1, 4)
-        t = t[t[:, 0] > 0]
-        res.append(t)
+        wid = np.nonzero(t[:, 0] > 0)[0]
+        res.append((t[t[:, 0] > 0], wid))
     lib.pico_csum_diag_set_stamps(ctypes.c_void_p(0), 0)
     out = []
-    for t in res:
+    for t, wid in res:
         t0 = t[:, 0].min()
         rel = (t - t0) * 10.0 / 1000.0          # 100 MHz ticks -> us
         span = rel[:, 3].max()
@@ -86,6 +87,16 @@ def main():
                     "end_pctl": q(rel[:, 3]), "phase1_dur_pctl": q(rel[:, 1] - rel[:, 0]),
                     "rounds_dur_pctl": q(rel[:, 2] - rel[:, 1]), "finish_dur_pctl": q(rel[:, 3] - rel[:, 2]),
                     "waves_done_at_90pct_span": round(float((rel[:, 3] <= 0.9 * span).mean()), 3)})
+        # per XCD (workgroups go round-robin over the 8 XCDs; 4 waves a workgroup): medians of the
+        # start, the streaming phase and the end, and each XCD's share of the last 5 % of waves
+        xcd = (wid // a.wpb) % 8
+        late = rel[:, 3] >= np.percentile(rel[:, 3], 95)
+        out[-1]["per_xcd"] = [{"xcd": x, "start_med": round(float(np.median(rel[xcd == x, 0])), 2),
+                               "rounds_med": round(float(np.median(rel[xcd == x, 2] - rel[xcd == x, 1])), 2),
+                               "end_med": round(float(np.median(rel[xcd == x, 3])), 2),
+                               "end_max": round(float(rel[xcd == x, 3].max()), 2),
+                               "late_share": round(float((late & (xcd == x)).sum() / max(1, late.sum())), 3)}
+                              for x in range(8)]
     for o in out:
         print(json.dumps({"config": a.config, **o}))
 
