@@ -777,20 +777,23 @@ __device__ __forceinline__ uint32_t sslot(uint32_t q) { return q ^ ((q >> 4) & (
 
 // The prefix at byte position b of the span (the sum of the span's bytes before b), taken when
 // b's last byte before it lies in the step starting at byte byte0.
-__device__ __forceinline__ void stream_point(const StreamLds& S, uint32_t b, uint32_t byte0, uint32_t& P) {
+__device__ __forceinline__ bool stream_point(const StreamLds& S, uint32_t b, uint32_t byte0, uint32_t& P) {
     const uint32_t t = b - 1u - byte0;
-    if (b != 0u && t < 16u * SQ) {
-        const uint32_t q = t >> 4, m = (t & 15u) + 1u;       // bytes of chunk q before b: 1..16
+    const bool in = b != 0u && t < 16u * SQ;
+    if (in) {
+        const uint32_t q = t >> 4, sh = 8u * (t & 15u) + 8u;  // bits of chunk q before b: 8..128
         const uint4 u = S.raw[sslot(q)];
         uint32_t a = S.pxc[q];
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (uint32_t d = 0; d < 4; ++d) {
-            const uint32_t nb = m > 4u * d ? min(m - 4u * d, 4u) : 0u;
-            a = dot2_add(w[d] & (nb >= 4u ? 0xFFFFFFFFu : (1u << (8u * nb)) - 1u), a);
-        }
+        // the chunk's first sh bits as two 64-bit masks (v_lshlrev_b64 takes the shift mod 64)
+        const uint64_t ml = sh >= 64u ? ~0ull : (1ull << (sh & 63u)) - 1ull;
+        const uint64_t mh = sh <= 64u ? 0ull : sh >= 128u ? ~0ull : (1ull << (sh & 63u)) - 1ull;
+        a = dot2_add(u.x & (uint32_t)ml, a);
+        a = dot2_add(u.y & (uint32_t)(ml >> 32), a);
+        a = dot2_add(u.z & (uint32_t)mh, a);
+        a = dot2_add(u.w & (uint32_t)(mh >> 32), a);
         P = a;
     }
+    return in;
 }
 
 template <int OP, int CTRL, int RM>
@@ -833,61 +836,27 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
     return ((v >> 8) | (v << 8)) & 0xFFFFu;
 }
 
-// Workgroup-wide stream (round 4): the workgroup's WPB x fpw frames are split into WPB ranges of
-// whole frames with equal bytes (a workgroup scan of the lengths in frame order), and wave w streams
-// range w -- so the waves of a workgroup read the same number of bytes whatever the size mix, where
-// a wave of 64 IMIX frames alone reads 64 frames' worth (+-14 %, the largest 1.5x the mean: the
-// launch's end).  Lane j still owns frame j (its header chunks, its prefixes, its
-// finish): at every step the workgroup's stages sit in LDS together (two barriers a step) and lane j
-// reads the stage of the wave that streams its frame's range.  A frame never straddles two ranges,
-// so every prefix it needs comes from one wave's running sum.
-// Two layouts: DENSE -- the range's frames lie back to back (a TAP / ring burst): the wave reads its
-// range's span in address order; COMPACT -- anything else within +-512 MiB (frames in fixed slots of
-// a batching driver's ring, modules/pico_dev_tap.c:63-75, or scattered): the wave reads only its
-// frames' own lines, frame after frame, as one compacted chunk sequence (chunk q of the range ->
-// frame i, the last with cs_i <= q, by a binary search over the range's (cs, line) table held in
-// the wave's registers); every frame position is then a compacted position, and the rest of the
-// stream is the same.
-constexpr uint32_t CMAXF = 128;   // COMPACT: frames per range (two table entries per lane)
-struct StreamWg {
-    uint64_t anc[WPB];     // each wave's first valid frame's line (the workgroup anchor)
-    uint32_t wsum[WPB];    // each wave's valid bytes, chunks, frames (frame-order prefixes)
-    uint32_t wch[WPB];
-    uint32_t wcnt[WPB];
-    uint32_t flag[WPB];    // a wave that rules the stream out (stack-walked seed, huge frame)
-    int rmin[WPB];         // range r: first line, end, bytes (relative to the anchor)
-    int rmax[WPB];
-    uint32_t rsum[WPB];
-    uint32_t rnc[WPB];     // range r: its frames' chunks and count, its first frame's prefixes
-    uint32_t rcnt[WPB];
-    uint32_t rc0[WPB];
-    uint32_t rn0[WPB];
-    uint32_t far;                      // a frame more than 512 MiB from the anchor
-};
-
-// COMPACT: the window line of compacted chunk q of a range whose frame i (i < n) starts at compacted
-// chunk cs_i and window line line_i -- entries i and 64 + i in lane i (csab = cs_i | cs_64+i << 16,
-// la / lb = the lines), cs64 = cs_64.  Every lane of the wave must call it (ds_bpermute).
-__device__ __forceinline__ uint32_t compact_line(uint32_t q, uint32_t csab, uint32_t la, uint32_t lb, uint32_t n,
-                                                 uint32_t cs64) {
-    uint32_t i = (n > 64u && cs64 <= q) ? 64u : 0u;
-    uint32_t ci = i ? cs64 : 0u;
+// Layouts of a wave's frames: DENSE -- back to back (a TAP / ring burst): the wave reads their span
+// in address order; COMPACT -- anything else within +-512 MiB (frames in fixed slots of a batching
+// driver's ring, modules/pico_dev_tap.c:63-75, or scattered): the wave reads only its frames' own
+// lines, frame after frame, as one compacted chunk sequence (chunk q -> frame i, the last with
+// cs_i <= q, by a binary search over the (cs, line) table held one entry per lane); every frame
+// position is then a compacted position, and the rest of the stream is the same.
+// (Round 4 also measured workgroup-balanced ranges -- the 4 waves of a workgroup splitting its 256
+// frames into equal-byte ranges, two barriers a step: slower on every config, DESIGN.md.)
+__device__ __forceinline__ uint32_t compact_line(uint32_t q, uint32_t cs, uint32_t ln, uint32_t n) {
+    uint32_t i = 0u, ci = 0u;
 #pragma unroll
     for (uint32_t st = 32; st >= 1; st >>= 1) {
         const uint32_t c = i + st;
-        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c & 63u) << 2), (int)csab);
-        const uint32_t cv = c >= 64u ? v >> 16 : v & 0xFFFFu;
+        const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c & 63u) << 2), (int)cs);
         if (c < n && cv <= q) { i = c; ci = cv; }
     }
-    const uint32_t l0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((i & 63u) << 2), (int)la);
-    const uint32_t l1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((i & 63u) << 2), (int)lb);
-    return (i >= 64u ? l1 : l0) + (q - ci);
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(i << 2), (int)ln) + (q - ci);
 }
 
-// Returns false (nothing written) for a wave whose frames are not streamed: the workgroup's
-// frames are not one dense span (every wave), or after the loop, this wave holds a frame the
-// stream does not finish (below).  Every wave of the workgroup must call it (barriers), whether or
-// not it has frames.  NATM: the NAT batch (F_NAT), its own instantiation so the RX / TX waves
+// Returns false (nothing written) for a wave whose frames are not streamed: they are neither DENSE
+// nor COMPACT, or after the loop, the wave holds a frame the stream does not finish (below).  NATM: the NAT batch (F_NAT), its own instantiation so the RX / TX waves
 // carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for datagrams whose
 // transport follows the 40-byte header (descriptor seed 0; RX next header TCP / UDP / ICMPv6 --
 // anything else needs the extension-header walk: the sorted rounds).  ETH: the Ethernet batch
@@ -907,6 +876,23 @@ __device__ __forceinline__ uint32_t eth6_field(bool tx, uint32_t nh, uint32_t b9
     return nh == 6u ? 16u : nh == 17u ? 6u : nh == 58u ? 2u : NONE;
 }
 
+// The even-domain sum of the head window's bytes [a, b) (window positions, b <= 16 * N): the
+// window starts on a 16-byte line of the span, so a byte's parity in the window is its parity there.
+template <uint32_t N>
+__device__ __forceinline__ uint32_t hw_range_sum(const uint4 (&hw)[HW], uint32_t a, uint32_t b) {
+    uint32_t s = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u * N; ++k) {
+        const uint4 c = hw[k >> 2];
+        const uint32_t d = (k & 3u) == 0 ? c.x : (k & 3u) == 1 ? c.y : (k & 3u) == 2 ? c.z : c.w;
+        const uint32_t lo = (uint32_t)min(max((int)a - (int)(4u * k), 0), 4);
+        const uint32_t hi = (uint32_t)min(max((int)b - (int)(4u * k), 0), 4);
+        const uint32_t mh = (uint32_t)((1ull << (8u * hi)) - 1ull), ml = (uint32_t)((1ull << (8u * lo)) - 1ull);
+        s = dot2_add(d & (mh & ~ml), s);
+    }
+    return s;
+}
+
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
@@ -915,11 +901,6 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 template <bool NATM, bool V6 = false, bool ETH = false>
 __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<true>* lds_all, uint32_t lane,
                                              uint32_t wv, uint64_t f0) {
-    // the workgroup table lives in wave 0's stage until the third barrier below (after it nothing
-    // reads it; the stages -- or a fallback's sorted-rounds state -- are written only after it):
-    // 4 workgroups of 4 waves keep fitting a CU's 160 KiB of LDS
-    static_assert(sizeof(StreamWg) <= sizeof(StreamLds), "workgroup table must fit a stage");
-    StreamWg& W = *reinterpret_cast<StreamWg*>(&lds_all[0]);
     constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
     if (!ETH && (p.flags & F_MACF)) return false;
     StreamLds& S = lds_all[wv].st;
@@ -943,150 +924,58 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
     const uint32_t cch = valid ? ((uint32_t)(addr & 15u) + len + 15u) >> 4 : 0u;   // the frame's lines
-    // ---- the workgroup's span: anchor, frame-order byte prefix, ranges
+    // ---- the span: anchor, extent, layout
+    uint64_t anchor = ~0ull;
+    int mn = 0, mx = 0;
+    bool dense = false, compact = false;
+    uint32_t q1 = 0u, ncf = 0u, nsteps = 0u, csj = 0u, idx = 0u;
     {
         const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
-        const int fv = vb ? __builtin_ffsll((long long)vb) - 1 : 0;
-        const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+        if (!vb) return false;
         // a stack-walked IPv6 seed, or a frame over 1 MiB (the 32-bit byte sums): no stream
-        const bool no = __builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20))) != 0;
-        const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
-        const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)cch), 63);
-        if (lane == 0) {
-            W.anc[wv] = vb ? a : ~0ull;
-            W.wsum[wv] = ws;
-            W.wch[wv] = wc;
-            W.wcnt[wv] = (uint32_t)__builtin_popcountll(vb);
-            W.flag[wv] = no ? 1u : 0u;
-        }
-        if (wv == 0 && lane < WPB) {
-            W.rmin[lane] = 0x7FFFFFFF;
-            W.rmax[lane] = -0x7FFFFFFF;
-            W.rsum[lane] = 0u;
-            W.rnc[lane] = 0u;
-            W.rcnt[lane] = 0u;
-            W.rc0[lane] = 0xFFFFFFFFu;
-            W.rn0[lane] = 0xFFFFFFFFu;
-            if (lane == 0) W.far = 0u;
-        }
+        if (__builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20)))) return false;
+        const int fv = __builtin_ffsll((long long)vb) - 1;
+        anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+        const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
+        if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
+        mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
+        mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
+        const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
+        const uint32_t incc = (uint32_t)wave_incl<0>((int)cch);
+        const uint32_t nc = (uint32_t)__builtin_amdgcn_readlane((int)incc, 63);
+        const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
+        dense = (uint64_t)ext <= 2ull * rs + 4096u;
+        compact = !dense && nc < (1u << 24);
+        if (!dense && !compact) return false;
+        ncf = (uint32_t)__builtin_popcountll(vb);
+        q1 = compact ? nc : ext >> 4;
+        nsteps = ((compact ? nc : ext >> 4) + SQ - 1u) / SQ;
+        csj = valid ? incc - cch : 0u;
+        idx = valid ? __builtin_amdgcn_mbcnt_hi((uint32_t)(vb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vb, 0u)) : 0u;
     }
-    __syncthreads();
-    uint64_t anchor = ~0ull;
-    uint32_t bad = 0u, exw = 0u, total = 0u, exc = 0u, exn = 0u;
-#pragma unroll
-    for (uint32_t k = 0; k < WPB; ++k) {
-        const uint64_t a = W.anc[k];
-        if (anchor == ~0ull) anchor = a;
-        bad |= W.flag[k];
-        exw += k < wv ? W.wsum[k] : 0u;
-        exc += k < wv ? W.wch[k] : 0u;
-        exn += k < wv ? W.wcnt[k] : 0u;
-        total += W.wsum[k];
-    }
-    if (anchor == ~0ull || bad) {                      // workgroup-uniform (the same LDS for all)
-        __syncthreads();                               // (the table is read by every wave first)
-        return false;
-    }
-    const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
-    const bool far = valid && (dl < -(1ll << 29) || dh > (1ll << 29));
-    // range of frame j: its frame-order byte prefix in WPB equal parts (whole frames)
-    const uint32_t inc = (uint32_t)wave_incl<0>((int)blen);
-    const uint32_t ex = exw + inc - blen;
-    uint32_t rg = 0u;                                   // floor(WPB * ex / total), by compares
-#pragma unroll
-    for (uint32_t k = 1; k < WPB; ++k) rg += valid && (uint64_t)ex * WPB >= (uint64_t)k * total ? 1u : 0u;
-    // frame-order prefixes of the frames' lines and of the valid frames (COMPACT)
-    const uint32_t exch = exc + (uint32_t)wave_incl<0>((int)cch) - cch;
-    const uint64_t vbm = __builtin_amdgcn_ballot_w64(valid);
-    const uint32_t exfn = exn + __builtin_amdgcn_mbcnt_hi((uint32_t)(vbm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vbm, 0u));
-    // per range: wave reductions, then one lane's LDS atomics (the LDS is the CU's: 64 lanes'
-    // atomics on one address from each of 16 waves serialise for microseconds). rg rises with
-    // the frame index, so the wave's frames touch the ranges of its first to its last valid frame.
-    if (vbm) {
-        const uint32_t kf = (uint32_t)__builtin_amdgcn_readlane((int)rg, __builtin_ffsll((long long)vbm) - 1);
-        const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)rg, 63 - __builtin_clzll(vbm));
-        for (uint32_t k = kf; k <= kl; ++k) {
-            const bool m = valid && rg == k;
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(m);
-            if (!bm) continue;
-            const int first = __builtin_ffsll((long long)bm) - 1;
-            const int mn_k = __builtin_amdgcn_readlane(wave_incl<1>(m ? (int)dl : 0x7FFFFFFF), 63);
-            const int mx_k = __builtin_amdgcn_readlane(wave_incl<2>(m ? (int)dh : -0x7FFFFFFF), 63);
-            const uint32_t rs_k = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(m ? (int)len : 0), 63);
-            const uint32_t nc_k = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>(m ? (int)cch : 0), 63);
-            const uint32_t c0_k = (uint32_t)__builtin_amdgcn_readlane((int)exch, first);
-            const uint32_t n0_k = (uint32_t)__builtin_amdgcn_readlane((int)exfn, first);
-            if (lane == 0) {
-                atomicMin(&W.rmin[k], mn_k);
-                atomicMax(&W.rmax[k], mx_k);
-                atomicAdd(&W.rsum[k], rs_k);
-                atomicAdd(&W.rnc[k], nc_k);
-                atomicAdd(&W.rcnt[k], (uint32_t)__builtin_popcountll(bm));
-                atomicMin(&W.rc0[k], c0_k);
-                atomicMin(&W.rn0[k], n0_k);
-            }
-        }
-    }
-    if (__builtin_amdgcn_ballot_w64(far) && lane == 0) W.far = 1u;
-    __syncthreads();
-    int mn = 0x7FFFFFFF, mx = -0x7FFFFFFF;
-    bool dense = W.far == 0u, compact = W.far == 0u;
-    uint32_t nsteps = 0, csteps = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < WPB; ++k) {
-        const uint32_t rs = W.rsum[k];
-        const int a = W.rmin[k], b = W.rmax[k];
-        if (rs) {
-            mn = min(mn, a);
-            mx = max(mx, b);
-            const uint32_t ext = (uint32_t)(((int64_t)b + 15 - a) & ~(int64_t)15);
-            dense = dense && (uint64_t)ext <= 2ull * rs + 4096u;
-            nsteps = max(nsteps, ((ext >> 4) + SQ - 1u) / SQ);
-            compact = compact && W.rcnt[k] <= CMAXF && W.rnc[k] < 0x10000u;
-            csteps = max(csteps, (W.rnc[k] + SQ - 1u) / SQ);
-        }
-    }
-    compact = compact && !dense;
-    // this wave's range [q0, q1) in chunks of the window (COMPACT: of its compacted sequence);
-    // frame j's owner's range start, its compacted start and its index in the range
-    const bool mine = W.rsum[wv] != 0u;
-    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(mine && !compact ? (int)((uint32_t)(W.rmin[wv] - mn) >> 4) : 0);
-    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readfirstlane(
-        !mine ? 0 : compact ? (int)W.rnc[wv] : (int)((uint32_t)(W.rmax[wv] + 15 - mn) >> 4));
-    const uint32_t ncf = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.rcnt[wv]);
-    nsteps = (uint32_t)__builtin_amdgcn_readfirstlane((int)(compact ? csteps : nsteps));
-    const uint32_t q0o = valid && !compact ? (uint32_t)(W.rmin[rg] - mn) >> 4 : 0u;
-    const uint32_t csj = valid ? exch - W.rc0[rg] : 0u, idx = valid ? exfn - W.rn0[rg] : 0u;
-    __syncthreads();                                   // the table is dead from here on
-    if (!dense && !compact) return false;              // workgroup-uniform
-    // (wave-uniform values read from LDS: in SGPRs, not kept in VGPRs across the loop)
     const uint64_t lo = uniform64(anchor + (int64_t)mn);
     const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
     const Window w = make_window(lo, (uint32_t)extent);
-    const StreamLds& So = lds_all[rg].st;
     const uint32_t relw = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
-    // COMPACT: every position of the frame in its range's compacted sequence
+    // COMPACT: every position of the frame in the wave's compacted sequence
     const uint32_t rel = compact ? 16u * csj + (relw & 15u) : relw;
     const uint32_t r = rel & 15u, hq = rel >> 4;
-    // COMPACT: the range's (cs, line) table into the loading wave's registers, through LDS (the
-    // stages, free until the loop)
-    uint32_t csab = 0u, lna = 0u, lnb = 0u, cs64 = 0u;
-    if (compact) {                                     // workgroup-uniform
-        uint2* T = reinterpret_cast<uint2*>(&lds_all[0]);        // (over the stages, all free here)
-        static_assert(WPB * CMAXF * sizeof(uint2) <= WPB * sizeof(SortedWaveSmem<true>), "range tables must fit");
-        if (valid) T[rg * CMAXF + idx] = make_uint2(csj, relw >> 4);
-        __syncthreads();
-        const uint2 e0 = T[wv * CMAXF + lane], e1 = T[wv * CMAXF + 64u + lane];
-        csab = (e0.x & 0xFFFFu) | (e1.x << 16);
-        lna = e0.y;
-        lnb = e1.y;
-        cs64 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e1.x);
-        __syncthreads();
+    // COMPACT: the (cs, line) table, lane i <- the i-th valid frame, through the wave's own stage
+    // (free until the loop)
+    uint32_t tcs = 0u, tln = 0u;
+    if (compact) {                                     // wave-uniform
+        uint2* T = reinterpret_cast<uint2*>(&S);
+        if (valid) T[idx] = make_uint2(csj, relw >> 4);
+        __builtin_amdgcn_wave_barrier();
+        const uint2 e = T[lane];
+        tcs = e.x;
+        tln = e.y;
+        __builtin_amdgcn_wave_barrier();
     }
-    // the window offset of chunk q of this wave's range (WIN_OOB past its end)
+    // the window offset of chunk q of the wave's sequence (WIN_OOB past its end)
     auto chunk_off = [&](uint32_t q) -> uint32_t {
-        const uint32_t ln = compact ? compact_line(q, csab, lna, lnb, ncf, cs64) : q;
+        const uint32_t ln = compact ? compact_line(q, tcs, tln, ncf) : q;
         return q < q1 ? 16u * ln : WIN_OOB;
     };
     constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
@@ -1099,26 +988,49 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // before the one that completes the header parse -- taken for every frame until the parse says
     // IPv4 (then the options start, or none)
     uint32_t b0 = ETH && valid ? rel + 22u : 0u, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    // MODE 1 / MODE 2: no parse in the loop -- the transport start as if there were no options
+    // (MODE 1: the options start), the frame's end, and (MODE 2 TX) the TCP crc field at 56; the
+    // finish corrects them from the head window (options, bytes past the datagram) or falls back
+    if constexpr (!ETH) {
+        if (valid) {
+            b1 = rel + (V6 ? 40u : 20u);
+            b2 = rel + len;
+            if (V6 && tx && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }
+        }
+    }
     uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
     bool pre = !valid;
     uint32_t base = 0;
     // two steps in flight: step k + 1's loads go out before step k is staged and summed
-    uint4 v[SCPL];
+    // (the offsets first, then the loads from one place: loads issued on two paths leave the
+    // compiler's wait counting at the join with a full vmcnt(0) -- the next step's loads waited on
+    // before this one is staged)
+    auto load_step = [&](uint32_t qs, uint4 (&dst)[SCPL]) {
+        uint32_t oc[SCPL];
+        if (compact) {                                 // wave-uniform
 #pragma unroll
-    for (uint32_t c = 0; c < SCPL; ++c) {
-        v[c] = load_win<true>(w, chunk_off(q0 + 64u * c + lane));
-    }
-    STAMP(1);
-    for (uint32_t st = 0; st < nsteps; ++st) {
-        const uint32_t qb = q0 + st * SQ;
-        uint4 vn[SCPL];
+            for (uint32_t c = 0; c < SCPL; ++c) oc[c] = chunk_off(qs + 64u * c + lane);
+        } else {
+            const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
 #pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) {
-            vn[c] = load_win<true>(w, chunk_off(qb + SQ + 64u * c + lane));
+            for (uint32_t c = 0; c < SCPL; ++c) oc[c] = o + 1024u * c < oe ? o + 1024u * c : WIN_OOB;
         }
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, oc[c]);
+    };
+    // NAT: the record is in before the loop (an older load still in flight at the loop leaves the
+    // compiler's wait counting with a vmcnt(0) at every stage write)
+    if constexpr (NATM) asm volatile("" ::"v"(rw.x), "v"(rw.y));
+    uint4 v[SCPL], vn[SCPL];
+    load_step(0u, v);
+    STAMP(1);
+    // one step: cur is staged and summed while nxt's loads (step st + 1) are in flight
+    auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
+        const uint32_t qb = st * SQ;
+        load_step(qb + SQ, nxt);
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = v[c];
+        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
         __builtin_amdgcn_wave_barrier();
         // lane-major: lane L's SCPL chunks, chunk prefixes, one wave scan of the lane totals
         uint32_t loc[SCPL];
@@ -1135,27 +1047,16 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         for (uint32_t k = 0; k < SCPL; k += 4)
             *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
                 make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
-        __syncthreads();                               // every wave's step is staged
-        // frame j's head window chunks that are in its range's stage
-        const uint32_t qbo = q0o + st * SQ;
+        __builtin_amdgcn_wave_barrier();
+        // frame j's head window chunks that are in this step
 #pragma unroll
         for (uint32_t i = 0; i < HS; ++i) {
-            const uint32_t qi = hq + i - qbo;
-            if (i < nlh && qi < SQ) hw[i] = So.raw[sslot(qi)];
+            const uint32_t qi = hq + i - qb;
+            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
         }
         // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
         // fails the header checks below never reads them)
-        if (V6 && !pre && hq + 1u < qbo + SQ) {
-            pre = true;
-            uint32_t H[2];
-            window_words<2, false>(hw, r, H);
-            const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
-            const uint32_t nh = (H[1] >> 16) & 0xFFu;
-            b1 = rel + 40u;
-            b2 = rel + min(40u + plen, len);
-            if (tx && nh == 6u && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }   // TCP crc: past the head chunks
-        }
-        if (ETH && !pre && hq + 2u < qbo + SQ) {
+        if (ETH && !pre && hq + 2u < qb + SQ) {
             // MODE 3: an IPv6 frame (ethertype 0x86DD) -- its addresses (the pseudo header), the
             // transport and the field, all by prefixes (they lie past the head chunks)
             uint32_t T[1];
@@ -1168,7 +1069,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
                 const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
                 if (ilen >= 40u) {
-                    b0 = rel + 14u + 8u;
+                    // (b0 = frame + 22 since the start: taken in this step or an earlier one)
                     b1 = rel + 54u;
                     b2 = rel + 14u + min(40u + plen, ilen);
                     const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);
@@ -1179,10 +1080,10 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 }
             }
         }
-        if (!V6 && !pre && hq + (ETH ? 2u : 1u) < qbo + SQ) {
+        if (ETH && !pre && hq + 2u < qb + SQ) {
             pre = true;
             uint32_t H[3];
-            window_words<3, ETH>(hw, r + L2, H);
+            window_words<3, true>(hw, r + L2, H);
             const uint32_t ilen = len - L2;
             const uint32_t ihl = H[0] & 0x0Fu;
             const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
@@ -1201,19 +1102,25 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 x1 = x0 + 2u;
             }
         }
-        const uint32_t byte0 = 16u * qbo;
-        stream_point(So, b1, byte0, P1);
-        stream_point(So, b2, byte0, P2);
-        if (__builtin_amdgcn_ballot_w64(b0 != 0u || x0 != 0u)) {
-            stream_point(So, b0, byte0, P0);
-            stream_point(So, x0, byte0, P3);
-            stream_point(So, x1, byte0, P4);
+        const uint32_t byte0 = 16u * qb;
+        stream_point(S, b1, byte0, P1);
+        stream_point(S, b2, byte0, P2);
+        // the optional points, each cleared once taken (the group is skipped once none is left)
+        if ((ETH || V6) && __builtin_amdgcn_ballot_w64((b0 | x0 | x1) != 0u)) {
+            b0 = stream_point(S, b0, byte0, P0) ? 0u : b0;
+            x0 = stream_point(S, x0, byte0, P3) ? 0u : x0;
+            x1 = stream_point(S, x1, byte0, P4) ? 0u : x1;
         }
         base += tot;
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();               // every stage read before the next is written
+    };
+    // one step a trip, the register sets copied (a two-step trip with the sets swapping roles
+    // spills in MODE 1 and MODE 3)
+    for (uint32_t st = 0; st < nsteps; ++st) {
+        step(st, v, vn);
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
-        asm volatile("" ::: "memory");
-        __syncthreads();                               // every stage read before the next is written
     }
 
     STAMP(2);
@@ -1256,7 +1163,11 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 }
             }
         }
-        if (__builtin_amdgcn_ballot_w64(walk)) return false;
+        // bytes past the datagram (P2 was taken at the frame's end): from the head window
+        const bool tail = parsed && 40u + tl < len;
+        if (__builtin_amdgcn_ballot_w64(walk || (tail && r + len > 16u * HS))) return false;
+        uint32_t P2d = P2;
+        if (__builtin_amdgcn_ballot_w64(tail) && tail) P2d = P2 - hw_range_sum<HS>(hw, r + 40u + tl, r + len);
         const bool odd = r & 1u;
         uint32_t xe = 0, xp = 0;
         if (xo == 16u) {                       // TX TCP: by prefixes
@@ -1266,7 +1177,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             xp = hw_pair<HS>(hw, r + 40u + xo);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         }
-        const uint32_t tsum = tx ? pairing(P2 - P1 - xe, odd) + xp : pairing(P2 - P1, odd);
+        const uint32_t tsum = tx ? pairing(P2d - P1 - xe, odd) + xp : pairing(P2d - P1, odd);
         // the transport's line and offset (finish stores the field relative to it)
         const uint32_t rt = (r + 40u) & 15u;
         const uint64_t a0t = valid ? off + 40u - rt : 0u;
@@ -1415,14 +1326,30 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             }
         }
     }
-    if (__builtin_amdgcn_ballot_w64(ETH ? walk6 : nat_opt)) return false;
+    // MODE 1 (no parse in the loop: P1 at the options start, P2 at the frame's end): the options,
+    // the field and any bytes past the datagram from the head window, else the sorted rounds
+    const uint32_t xo4 = (!tx || proto == 17u) ? 6u : proto == 6u ? 16u : 2u;
+    bool fb = false, tail = false;
+    if constexpr (!ETH) {
+        tail = parsed && hl + tl < ilen;
+        fb = (parsed && r + hl > 16u * HS) || (tail && r + len > 16u * HS) || (hasx && r + hl + xo4 + 2u > 16u * HS);
+    }
+    if (__builtin_amdgcn_ballot_w64(ETH ? walk6 : nat_opt || fb)) return false;
+    uint32_t optd = 0u, P1d = P1, P2d = P2;
+    if constexpr (!ETH) {
+        if (__builtin_amdgcn_ballot_w64(parsed && (hl > 20u || tail))) {
+            if (parsed && hl > 20u) optd = hw_range_sum<HS>(hw, r + 20u, r + hl);
+            if (tail) P2d = P2 - hw_range_sum<HS>(hw, r + hl + tl, r + len);
+        }
+        P1d = P1 + optd;
+    }
     const bool odd = r & 1u;
-    // the field (frame pairing xp, even domain xe): from the head window, or with options by prefixes
+    // the field (frame pairing xp, even domain xe): from the head window, or (MODE 3, options or
+    // the TX TCP crc past the head chunks) by prefixes
     uint32_t xe = 0, xp = 0;
     if (hasx) {
-        if (hl == 20u && !(ETH && tx && proto == 6u)) {
-            const uint32_t xo = (!tx || proto == 17u) ? 6u : proto == 6u ? 16u : 2u;
-            xp = hw_pair<HS>(hw, r + L2 + 20u + xo);
+        if (!ETH || (hl == 20u && !(tx && proto == 6u))) {
+            xp = hw_pair<HS>(hw, r + L2 + hl + xo4);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         } else {
             xe = P4 - P3;
@@ -1433,8 +1360,8 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // region), RX: the field only says "present" (a UDP crc may lie past a short region)
     // NAT: the old port leaves the region in the even domain (no wrap below zero), the new enters
     const uint32_t noe = odd ? ((nop >> 8) | (nop << 8)) & 0xFFFFu : nop;
-    const uint32_t tsum = tx ? pairing(P2 - P1 - xe - noe, odd) + xp + nnw : pairing(P2 - P1, odd);
-    const uint32_t opt = hl > 20u ? pairing(P1 - P0, odd) : 0u;
+    const uint32_t tsum = tx ? pairing(P2d - P1d - xe - noe, odd) + xp + nnw : pairing(P2d - P1d, odd);
+    const uint32_t opt = hl > 20u ? pairing(ETH ? P1 - P0 : optd, odd) : 0u;
     // the IPv4 header's line and offset (finish stores relative to it)
     // (MODE 3 IPv6: the transport's line and offset; finish stores the field relative to it)
     const uint32_t ri = (r + (eth6 ? 54u : L2)) & 15u;
