@@ -836,27 +836,15 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
     return ((v >> 8) | (v << 8)) & 0xFFFFu;
 }
 
-// Layouts of a wave's frames: DENSE -- back to back (a TAP / ring burst): the wave reads their span
-// in address order; COMPACT -- anything else within +-512 MiB (frames in fixed slots of a batching
-// driver's ring, modules/pico_dev_tap.c:63-75, or scattered): the wave reads only its frames' own
-// lines, frame after frame, as one compacted chunk sequence (chunk q -> frame i, the last with
-// cs_i <= q, by a binary search over the (cs, line) table held one entry per lane); every frame
-// position is then a compacted position, and the rest of the stream is the same.
-// (Round 4 also measured workgroup-balanced ranges -- the 4 waves of a workgroup splitting its 256
-// frames into equal-byte ranges, two barriers a step: slower on every config, DESIGN.md.)
-__device__ __forceinline__ uint32_t compact_line(uint32_t q, uint32_t cs, uint32_t ln, uint32_t n) {
-    uint32_t i = 0u, ci = 0u;
-#pragma unroll
-    for (uint32_t st = 32; st >= 1; st >>= 1) {
-        const uint32_t c = i + st;
-        const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((c & 63u) << 2), (int)cs);
-        if (c < n && cv <= q) { i = c; ci = cv; }
-    }
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(i << 2), (int)ln) + (q - ci);
-}
+// A wave streams its frames' span when they lie back to back (a TAP / ring burst: the span at
+// most 2 x their bytes + 4 KiB); anything else takes the sorted rounds, which read only the frames'
+// own lines. (Round 4 measured two alternatives, both slower and removed -- DESIGN.md 4: the 4 waves
+// of a workgroup splitting its 256 frames into equal-byte ranges, two barriers a step; and a
+// COMPACT stream over the frames' own lines in frame order for slot rings and scattered frames, its
+// chunk -> line map a binary search per chunk.)
 
-// Returns false (nothing written) for a wave whose frames are not streamed: they are neither DENSE
-// nor COMPACT, or after the loop, the wave holds a frame the stream does not finish (below).  NATM: the NAT batch (F_NAT), its own instantiation so the RX / TX waves
+// Returns false (nothing written) for a wave whose frames are not streamed: they are not back to
+// back, or after the loop, the wave holds a frame the stream does not finish (below).  NATM: the NAT batch (F_NAT), its own instantiation so the RX / TX waves
 // carry none of its registers or instructions.  V6: the IPv6 batch (MODE 2) for datagrams whose
 // transport follows the 40-byte header (descriptor seed 0; RX next header TCP / UDP / ICMPv6 --
 // anything else needs the extension-header walk: the sorted rounds).  ETH: the Ethernet batch
@@ -923,12 +911,10 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint32_t blen = valid ? len : 0u;
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
-    const uint32_t cch = valid ? ((uint32_t)(addr & 15u) + len + 15u) >> 4 : 0u;   // the frame's lines
     // ---- the span: anchor, extent, layout
     uint64_t anchor = ~0ull;
     int mn = 0, mx = 0;
-    bool dense = false, compact = false;
-    uint32_t q1 = 0u, ncf = 0u, nsteps = 0u, csj = 0u, idx = 0u;
+    uint32_t q1 = 0u, nsteps = 0u;
     {
         const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
         if (!vb) return false;
@@ -942,42 +928,16 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
         mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
         const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
-        const uint32_t incc = (uint32_t)wave_incl<0>((int)cch);
-        const uint32_t nc = (uint32_t)__builtin_amdgcn_readlane((int)incc, 63);
         const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
-        dense = (uint64_t)ext <= 2ull * rs + 4096u;
-        compact = !dense && nc < (1u << 24);
-        if (!dense && !compact) return false;
-        ncf = (uint32_t)__builtin_popcountll(vb);
-        q1 = compact ? nc : ext >> 4;
-        nsteps = ((compact ? nc : ext >> 4) + SQ - 1u) / SQ;
-        csj = valid ? incc - cch : 0u;
-        idx = valid ? __builtin_amdgcn_mbcnt_hi((uint32_t)(vb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vb, 0u)) : 0u;
+        if (!((uint64_t)ext <= 2ull * rs + 4096u)) return false;    // not back to back
+        q1 = ext >> 4;
+        nsteps = (q1 + SQ - 1u) / SQ;
     }
     const uint64_t lo = uniform64(anchor + (int64_t)mn);
     const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
     const Window w = make_window(lo, (uint32_t)extent);
-    const uint32_t relw = valid ? (uint32_t)(addr - lo) : 0u;  // frame start in the span
-    // COMPACT: every position of the frame in the wave's compacted sequence
-    const uint32_t rel = compact ? 16u * csj + (relw & 15u) : relw;
+    const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;   // frame start in the span
     const uint32_t r = rel & 15u, hq = rel >> 4;
-    // COMPACT: the (cs, line) table, lane i <- the i-th valid frame, through the wave's own stage
-    // (free until the loop)
-    uint32_t tcs = 0u, tln = 0u;
-    if (compact) {                                     // wave-uniform
-        uint2* T = reinterpret_cast<uint2*>(&S);
-        if (valid) T[idx] = make_uint2(csj, relw >> 4);
-        __builtin_amdgcn_wave_barrier();
-        const uint2 e = T[lane];
-        tcs = e.x;
-        tln = e.y;
-        __builtin_amdgcn_wave_barrier();
-    }
-    // the window offset of chunk q of the wave's sequence (WIN_OOB past its end)
-    auto chunk_off = [&](uint32_t q) -> uint32_t {
-        const uint32_t ln = compact ? compact_line(q, tcs, tln, ncf) : q;
-        return q < q1 ? 16u * ln : WIN_OOB;
-    };
     constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
     const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
     uint4 hw[HW];
@@ -1002,21 +962,12 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     bool pre = !valid;
     uint32_t base = 0;
     // two steps in flight: step k + 1's loads go out before step k is staged and summed
-    // (the offsets first, then the loads from one place: loads issued on two paths leave the
-    // compiler's wait counting at the join with a full vmcnt(0) -- the next step's loads waited on
-    // before this one is staged)
+    // (loads issued on two paths -- a layout branch -- leave the compiler's wait counting at the
+    // join with a full vmcnt(0): the next step's loads waited on before this one is staged)
     auto load_step = [&](uint32_t qs, uint4 (&dst)[SCPL]) {
-        uint32_t oc[SCPL];
-        if (compact) {                                 // wave-uniform
+        const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
 #pragma unroll
-            for (uint32_t c = 0; c < SCPL; ++c) oc[c] = chunk_off(qs + 64u * c + lane);
-        } else {
-            const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
-#pragma unroll
-            for (uint32_t c = 0; c < SCPL; ++c) oc[c] = o + 1024u * c < oe ? o + 1024u * c : WIN_OOB;
-        }
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, oc[c]);
+        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, o + 1024u * c < oe ? o + 1024u * c : WIN_OOB);
     };
     // NAT: the record is in before the loop (an older load still in flight at the loop leaves the
     // compiler's wait counting with a vmcnt(0) at every stage write)
@@ -1115,17 +1066,28 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();               // every stage read before the next is written
     };
-    // one step a trip, the register sets copied (a two-step trip with the sets swapping roles
-    // spills in MODE 1 and MODE 3)
-    for (uint32_t st = 0; st < nsteps; ++st) {
-        step(st, v, vn);
+    if constexpr (!ETH) {
+        // two steps a trip, the register sets swapping roles: each step's wait covers only its own
+        // loads (a copy of the next set into this one at the end of a trip would wait on them too,
+        // leaving one step in flight across the wait)
+        for (uint32_t st = 0; st < nsteps; st += 2) {
+            step(st, v, vn);
+            if (st + 1u >= nsteps) break;
+            step(st + 1u, vn, v);
+        }
+    } else {
+        // MODE 3 (both families' parse in the loop): one step a trip, the sets copied -- the
+        // two-step trip spills there
+        for (uint32_t st = 0; st < nsteps; ++st) {
+            step(st, v, vn);
 #pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+            for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+        }
     }
 
     STAMP(2);
     // the frame's offset again, from the span (a 64-bit value less to keep across the loop)
-    const uint64_t off = valid ? lo + relw - reinterpret_cast<uintptr_t>(p.base) : 0u;
+    const uint64_t off = valid ? lo + rel - reinterpret_cast<uintptr_t>(p.base) : 0u;
     if constexpr (V6) {
         // pico_ipv6_process_in / pico_transport_crc_check as sorted_batch's MODE 2 (seed 0, no
         // extension header): lengths, byte-9 dispatch (ipcrc), the field, the pseudo header

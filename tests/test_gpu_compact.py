@@ -1,9 +1,10 @@
-"""GPU: the stream's COMPACT layout (stream_batch in pico_csum_k_sorted.hip) -- frames that are not
-one dense span: each in a fixed slot of a driver's ring (modules/pico_dev_tap.c:63-75 reads one frame
-per slot-sized buffer), at a jitter inside the slot, or scattered with random gaps.  The workgroup
-reads only its frames' own lines as one compacted sequence per range.  IPv4 RX / TX (written in
-place) / NAT, IPv6, the Ethernet front end, and ranges of more than 128 frames (the sorted rounds
-take those), every output and byte against the oracle."""
+"""GPU: frame layouts that are not one dense span -- each frame in a fixed slot of a driver's ring
+(modules/pico_dev_tap.c:63-75 reads one frame per slot-sized buffer), at a jitter inside the slot,
+or scattered with random gaps: the waves holding them take the sorted rounds (a round-4 COMPACT
+stream over the frames' own lines measured slower and was removed), the dense ones in
+the same launch the stream.  IPv4 RX / TX (written in place) / NAT, IPv6, the Ethernet front end,
+batches ending inside a workgroup, mixed IPv4 / IPv6 Ethernet bursts, every output and byte against
+the oracle."""
 from __future__ import annotations
 
 import numpy as np
@@ -145,9 +146,9 @@ def test_eth_compact():
         np.testing.assert_array_equal(u16(l4), wl)
 
 
-def test_range_over_128_frames_falls_back():
-    """255 tiny datagrams and one large one per workgroup: a byte-balanced range holds more than
-    128 frames, so the workgroup takes the sorted rounds -- same results."""
+def test_tiny_and_huge_with_gaps():
+    """255 tiny datagrams and one of 20000 bytes per 256, with random gaps: waves whose frames are
+    not back to back take the sorted rounds, the others the stream -- same results."""
     rng = np.random.default_rng(3)
     n = 256 * 40
     lens = np.full(n, 40, np.uint32)
@@ -167,7 +168,7 @@ def test_range_over_128_frames_falls_back():
 @pytest.mark.parametrize("slot", [0, 2048])
 def test_partial_workgroups(n, slot):
     """Batches that end inside a workgroup (waves with no frames take part in its barriers), dense
-    and COMPACT, with invalid and out-of-bounds descriptors mixed in."""
+    and slotted, with invalid and out-of-bounds descriptors mixed in."""
     rng = np.random.default_rng(n + slot)
     buf, desc = imix_v4(n, 40 + n)
     if slot:
