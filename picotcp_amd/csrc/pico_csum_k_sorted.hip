@@ -886,6 +886,22 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
 
+// The head window as the stream's finish keeps it in LDS (wl: the lane's copy, dword-aligned, one
+// zero dword past it): NW words starting at byte pos, and the two bytes at pos, low byte first.
+template <int NW>
+__device__ __forceinline__ void lds_words(const uint32_t* wl, uint32_t pos, uint32_t (&H)[NW]) {
+    const uint32_t q = pos >> 2, sh = pos & 3u;
+    uint32_t E[NW + 1];
+#pragma unroll
+    for (int m = 0; m <= NW; ++m) E[m] = wl[q + m];
+#pragma unroll
+    for (int m = 0; m < NW; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
+}
+__device__ __forceinline__ uint32_t lds_pair(const uint32_t* wl, uint32_t pos) {
+    const uint32_t q = pos >> 2;
+    return __builtin_amdgcn_alignbyte(wl[q + 1], wl[q], pos & 3u) & 0xFFFFu;
+}
+
 template <bool NATM, bool V6 = false, bool ETH = false>
 __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<true>* lds_all, uint32_t lane,
                                              uint32_t wv, uint64_t f0) {
@@ -1086,6 +1102,14 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     }
 
     STAMP(2);
+    // the head window into the stage (free now), 144 bytes a lane: the finish takes its header
+    // words and fields with aligned LDS reads and one alignbyte each, not select chains over hw
+    static_assert(64u * 36u * sizeof(uint32_t) <= sizeof(StreamLds), "head windows must fit the stage");
+    uint32_t* const wl = reinterpret_cast<uint32_t*>(&S) + 36u * lane;
+#pragma unroll
+    for (uint32_t i = 0; i < HS; ++i) *reinterpret_cast<uint4*>(wl + 4u * i) = hw[i];
+    wl[4u * HS] = 0u;
+    __builtin_amdgcn_wave_barrier();
     // the frame's offset again, from the span (a 64-bit value less to keep across the loop)
     const uint64_t off = valid ? lo + rel - reinterpret_cast<uintptr_t>(p.base) : 0u;
     if constexpr (V6) {
@@ -1095,7 +1119,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         bool parsed = false, l4_needed = false, walk = false;
         if (valid) {
             uint32_t H[10];
-            window_words<10, false>(hw, r, H);
+            lds_words<10>(wl, r, H);
             tl = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
             proto = (H[1] >> 16) & 0xFFu;
             if (!tx && proto != 6u && proto != 17u && proto != 58u) {
@@ -1136,7 +1160,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             xe = P4 - P3;
             xp = odd ? ((xe >> 8) | (xe << 8)) & 0xFFFFu : xe;
         } else if (xo != NONE) {
-            xp = hw_pair<HS>(hw, r + 40u + xo);
+            xp = lds_pair(wl, r + 40u + xo);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         }
         const uint32_t tsum = tx ? pairing(P2d - P1 - xe, odd) + xp : pairing(P2d - P1, odd);
@@ -1166,8 +1190,8 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         ip4 = false;
         if (valid) {
             uint32_t M[2], T[1];
-            window_words<2, true>(hw, r, M);
-            window_words<1, true>(hw, r + 12u, T);
+            lds_words<2>(wl, r, M);
+            lds_words<1>(wl, r + 12u, T);
             const uint32_t m0 = M[0], m1 = M[1] & 0xFFFFu, et = T[0] & 0xFFFFu;
             const bool mine = !(p.flags & F_MACF) || tx || (m0 == p.mac_lo && m1 == p.mac_hi) ||
                               (m0 & 0xFFFFFFu) == 0x5E0001u || (m0 & 0xFFFFu) == 0x3333u ||
@@ -1177,7 +1201,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             else if (et == 0xDD86u) {                    // IPv6 (pico_ethernet.c:162-176)
                 if (ilen != 0u) {
                     uint32_t V[1];
-                    window_words<1, true>(hw, r + 14u, V);
+                    lds_words<1>(wl, r + 14u, V);
                     if ((V[0] & 0xF0u) != 0x60u) l2v = V_DROP_L2;
                     else eth6 = true;
                 }
@@ -1185,7 +1209,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
             else if (et != 0x0008u) l2v = V_DROP_L2;
             else if (ilen != 0u) {
                 uint32_t V[1];
-                window_words<1, true>(hw, r + 14u, V);
+                lds_words<1>(wl, r + 14u, V);
                 if ((V[0] & 0xF0u) != 0x40u) l2v = V_DROP_L2;
                 else ip4 = true;
             }
@@ -1194,7 +1218,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     walk6 = eth6 && seeded;
     if (ETH && eth6 && ilen >= 40u && !seeded) {
         uint32_t H[3];
-        window_words<3, true>(hw, r + 14u, H);
+        lds_words<3>(wl, r + 14u, H);
         tl = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
         proto = (H[1] >> 16) & 0xFFu;
         const uint32_t b9 = (H[2] >> 8) & 0xFFu;
@@ -1226,7 +1250,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     }
     if (ETH ? ip4 && ilen >= 20u : valid) {
         uint32_t H[5];
-        window_words<5, ETH>(hw, r + L2, H);
+        lds_words<5>(wl, r + L2, H);
         const uint32_t ihl = H[0] & 0x0Fu;
         hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
         const uint32_t tot = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
@@ -1277,7 +1301,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                         const uint32_t da = (rw.x & 0xFFFFu) + (rw.x >> 16) - (old & 0xFFFFu) - (old >> 16);
                         hdr20 += da;
                         pseudo += da;
-                        if (hl == 20u) nop = hw_pair<HS>(hw, r + 20u + (dir == 1u ? 0u : 2u));
+                        if (hl == 20u) nop = lds_pair(wl, r + 20u + (dir == 1u ? 0u : 2u));
                         else nat_opt = true;
                         nnw = rw.y & 0xFFFFu;
                         l2v = NS_XLATE | (dir << 4);
@@ -1311,7 +1335,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     uint32_t xe = 0, xp = 0;
     if (hasx) {
         if (!ETH || (hl == 20u && !(tx && proto == 6u))) {
-            xp = hw_pair<HS>(hw, r + L2 + hl + xo4);
+            xp = lds_pair(wl, r + L2 + hl + xo4);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         } else {
             xe = P4 - P3;
