@@ -960,10 +960,11 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
 #pragma unroll
     for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
     // boundaries (span byte positions, 0 = none): options start, transport start / end, field
-    // MODE 3: b0 starts at an IPv6 datagram's addresses (frame + 22), which can lie in the step
-    // before the one that completes the header parse -- taken for every frame until the parse says
-    // IPv4 (then the options start, or none)
-    uint32_t b0 = ETH && valid ? rel + 22u : 0u, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    // MODE 3: b0 = an IPv6 datagram's addresses (frame + 22), which can lie in the step before the
+    // one that completes the header parse: set once the ethertype is in (chunk 1), which is never
+    // later than the step holding frame + 21
+    uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    bool pre6 = !ETH || !valid;
     // MODE 1 / MODE 2: no parse in the loop -- the transport start as if there were no options
     // (MODE 1: the options start), the frame's end, and (MODE 2 TX) the TCP crc field at 56; the
     // finish corrects them from the head window (options, bytes past the datagram) or falls back
@@ -1023,6 +1024,12 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         }
         // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
         // fails the header checks below never reads them)
+        if (ETH && !pre6 && hq + 1u < qb + SQ) {
+            pre6 = true;
+            uint32_t T[1];
+            window_words<1, true>(hw, r + 12u, T);
+            if ((T[0] & 0xFFFFu) == 0xDD86u) b0 = rel + 22u;
+        }
         if (ETH && !pre && hq + 2u < qb + SQ) {
             // MODE 3: an IPv6 frame (ethertype 0x86DD) -- its addresses (the pseudo header), the
             // transport and the field, all by prefixes (they lie past the head chunks)
@@ -1036,7 +1043,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
                 const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
                 if (ilen >= 40u) {
-                    // (b0 = frame + 22 since the start: taken in this step or an earlier one)
+                    // (b0 = frame + 22 since the ethertype: taken in this step or an earlier one)
                     b1 = rel + 54u;
                     b2 = rel + 14u + min(40u + plen, ilen);
                     const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);

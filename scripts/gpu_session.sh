@@ -1,7 +1,7 @@
 # one GPU session (round 4): the GPU suite, smoke, bench lines of the main configs, kernel traces of
-# C1 (graph replay and launched one by one) / C2 / C2 slot ring, and short interleaved A/Bs against
-# the round-3 stream kernels (picotcp_amd/ab/libpicocsum_r03.so) and 8-wave workgroups.  Every GPU
-# step under its own time limit; the first failure ends the script.
+# C1 (graph replay and launched one by one) / C2 / C2 slot ring, a short interleaved A/B against the
+# round-3 stream kernels (picotcp_amd/ab/libpicocsum_r03.so), then the PMC passes of the round
+# (scripts/gpu_pmc_round.sh).  Every GPU step under its own time limit; the first failure ends it.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -26,7 +26,7 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c1ng_$TAG -o run --output-format csv -- python3 $R/bench.py --no-graph --no-cpu --no-e2e --no-verify > $O/prof_c1ng_$TAG.log 2>&1
 echo "trace c1 no-graph ok"
 cd $R
-A=r03 ROUNDS=2 CFGS="c2 c2ethmix" bash scripts/gpu_ab.sh wg_$TAG
+A=r03 ROUNDS=2 CFGS="c2 c2eth c2ethmix c2v6" bash scripts/gpu_ab.sh r03_$TAG
 echo "ab r03 ok"
-A=wpb8 ROUNDS=1 CFGS="c2 c2slot" bash scripts/gpu_ab.sh wpb8_$TAG
-echo "ab wpb8 ok"
+bash scripts/gpu_pmc_round.sh $TAG
+echo "pmc ok"
