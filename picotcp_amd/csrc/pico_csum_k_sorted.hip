@@ -41,7 +41,10 @@ __device__ uint32_t g_stamps_n;
 //      keeps its lanes busy; per-frame sums go to LDS;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
-constexpr uint32_t WPB = 4;  // waves per workgroup (8 measured the same on the sorted rounds, profiles/r02wpb)
+#ifndef PICO_SORTED_WPB
+#define PICO_SORTED_WPB 4
+#endif
+constexpr uint32_t WPB = PICO_SORTED_WPB;  // waves per workgroup (8 measured the same on the sorted rounds, profiles/r02wpb)
 constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1 (temporal loads:
                              // non-temporal ones measured 5 % slower, profiles/r02nt)
 
@@ -1375,7 +1378,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
 // The product shape (measured): 8 chunks per lane per round, the 1-lane class for
 // frames of <= 8 chunks, non-temporal loads in the >= 16-lane rounds; 4 waves per SIMD.
 template <int MODE, bool NT = true, int CPL = 8, bool SMALL = true>
-__global__ __launch_bounds__(64 * WPB, 4) void csum_sorted_kernel(FlatArgs p) {
+__global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArgs p) {
     __shared__ SortedWaveSmem<MODE != 0> lds_all[WPB];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     SortedWaveSmem<MODE != 0>& S = lds_all[wv];
