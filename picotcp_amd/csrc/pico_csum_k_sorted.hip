@@ -41,10 +41,9 @@ __device__ uint32_t g_stamps_n;
 //      keeps its lanes busy; per-frame sums go to LDS;
 //   4. lane j finalizes frame j (one coalesced store per output).
 
-#ifndef PICO_SORTED_WPB
-#define PICO_SORTED_WPB 4
-#endif
-constexpr uint32_t WPB = PICO_SORTED_WPB;  // waves per workgroup (8 measured the same on the sorted rounds, profiles/r02wpb)
+// waves per workgroup: 8 measured the same on the sorted rounds (profiles/r02wpb); 1 the same and
+// 2 slower on the stream (profiles/r04/ab_*_wave_workgroups.txt)
+constexpr uint32_t WPB = 4;
 constexpr uint32_t HW = 8;   // head-window chunks the fused modes load in phase 1 (temporal loads:
                              // non-temporal ones measured 5 % slower, profiles/r02nt)
 
@@ -944,8 +943,13 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
         const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
         if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
-        mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
-        mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
+        // frames in address order (a burst): the first valid frame's line (dl = 0) and the last
+        // one's end bound the span; a frame outside them makes the wave scan for both
+        mx = __builtin_amdgcn_readlane((int)dh, 63 - __builtin_clzll(vb));
+        if (__builtin_amdgcn_ballot_w64(valid && (dl < 0 || dh > (int64_t)mx))) {
+            mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
+            mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
+        }
         const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
         const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
         if (!((uint64_t)ext <= 2ull * rs + 4096u)) return false;    // not back to back
