@@ -961,7 +961,10 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const Window w = make_window(lo, (uint32_t)extent);
     const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;   // frame start in the span
     const uint32_t r = rel & 15u, hq = rel >> 4;
-    constexpr uint32_t HS = 4;      // the header and, without options, the crc field (r + 38 <= 64)
+    // head-window chunks: the header and, without options, the crc field (r + 38 <= 64). (MODE 3
+    // with a fifth -- a padded 60-byte frame's end at any start -- spills into its loop: a padded
+    // frame starting past byte 4 of its line sends the wave to the sorted rounds instead)
+    constexpr uint32_t HS = 4u;
     const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
     uint4 hw[HW];
 #pragma unroll
@@ -972,15 +975,16 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // later than the step holding frame + 21
     uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
     bool pre6 = !ETH || !valid;
-    // MODE 1 / MODE 2: no parse in the loop -- the transport start as if there were no options
-    // (MODE 1: the options start), the frame's end, and (MODE 2 TX) the TCP crc field at 56; the
-    // finish corrects them from the head window (options, bytes past the datagram) or falls back
-    if constexpr (!ETH) {
-        if (valid) {
-            b1 = rel + (V6 ? 40u : 20u);
-            b2 = rel + len;
-            if (V6 && tx && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }
-        }
+    // No IPv4 parse in the loop: the options start (where the transport starts without options),
+    // the frame's end and, for TX, the TCP crc field's place without options (MODE 2: the transport
+    // start and the TCP crc at 56); the finish corrects them from the head window (options, bytes
+    // past the datagram, the field with options) or falls back. MODE 3 moves an IPv6 frame's points
+    // once its ethertype is in, and parses IPv6 headers in the loop (their field depends on them).
+    if (valid) {
+        b1 = rel + min(V6 ? 40u : L2 + 20u, len);
+        b2 = rel + len;
+        if (V6 && tx && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }
+        if (ETH && tx && 52u <= len) { x0 = rel + 50u; x1 = x0 + 2u; }
     }
     uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
     bool pre = !valid;
@@ -1032,17 +1036,22 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
         // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
         // fails the header checks below never reads them)
         if (ETH && !pre6 && hq + 1u < qb + SQ) {
+            // the ethertype: an IPv6 frame's addresses, transport start (neither taken yet: both
+            // lie past chunk 1); anything else needs no parse in the loop
             pre6 = true;
             uint32_t T[1];
             window_words<1, true>(hw, r + 12u, T);
-            if ((T[0] & 0xFFFFu) == 0xDD86u) b0 = rel + 22u;
+            if ((T[0] & 0xFFFFu) == 0xDD86u) {
+                b0 = rel + 22u;
+                b1 = rel + min(54u, len);
+                x0 = x1 = 0u;
+            } else {
+                pre = true;
+            }
         }
         if (ETH && !pre && hq + 2u < qb + SQ) {
-            // MODE 3: an IPv6 frame (ethertype 0x86DD) -- its addresses (the pseudo header), the
-            // transport and the field, all by prefixes (they lie past the head chunks)
-            uint32_t T[1];
-            window_words<1, true>(hw, r + 12u, T);
-            if ((T[0] & 0xFFFFu) == 0xDD86u) {
+            // MODE 3: an IPv6 frame -- its transport end and field, by prefixes (past the head chunks)
+            {
                 pre = true;
                 uint32_t H[3];
                 window_words<3, true>(hw, r + 14u, H);
@@ -1050,8 +1059,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                 const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
                 const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
                 if (ilen >= 40u) {
-                    // (b0 = frame + 22 since the ethertype: taken in this step or an earlier one)
-                    b1 = rel + 54u;
+                    // (b0, b1 since the ethertype)
                     b2 = rel + 14u + min(40u + plen, ilen);
                     const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);
                     if (xo != NONE && 40u + xo < ilen) {
@@ -1059,28 +1067,6 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
                         x1 = x0 + min(2u, ilen - 40u - xo);
                     }
                 }
-            }
-        }
-        if (ETH && !pre && hq + 2u < qb + SQ) {
-            pre = true;
-            uint32_t H[3];
-            window_words<3, true>(hw, r + L2, H);
-            const uint32_t ilen = len - L2;
-            const uint32_t ihl = H[0] & 0x0Fu;
-            const uint32_t hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-            const uint32_t tot16 = (((H[0] >> 16) & 0xFFu) << 8) | (H[0] >> 24);
-            const uint32_t tl = (tot16 - hl) & 0xFFFFu;
-            const uint32_t pr = (H[2] >> 8) & 0xFFu;
-            b1 = rel + L2 + min(hl, ilen);
-            b2 = rel + L2 + min(hl + tl, ilen);
-            b0 = 0u;
-            if (hl > 20u) {                  // options: their sum and the field, by prefixes too
-                b0 = rel + L2 + 20u;
-                const uint32_t xo = !tx ? (pr == 17u ? 6u : 0u) : pr == 6u ? 16u : pr == 1u ? 2u : 0u;
-                if (xo && hl + xo + 2u <= ilen) { x0 = rel + L2 + hl + xo; x1 = x0 + 2u; }
-            } else if (ETH && tx && pr == 6u && 38u <= ilen) {   // TX TCP crc: past the head chunks
-                x0 = rel + L2 + 36u;
-                x1 = x0 + 2u;
             }
         }
         const uint32_t byte0 = 16u * qb;
@@ -1329,26 +1315,24 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // MODE 1 (no parse in the loop: P1 at the options start, P2 at the frame's end): the options,
     // the field and any bytes past the datagram from the head window, else the sorted rounds
     const uint32_t xo4 = (!tx || proto == 17u) ? 6u : proto == 6u ? 16u : 2u;
-    bool fb = false, tail = false;
-    if constexpr (!ETH) {
-        tail = parsed && hl + tl < ilen;
-        fb = (parsed && r + hl > 16u * HS) || (tail && r + len > 16u * HS) || (hasx && r + hl + xo4 + 2u > 16u * HS);
+    const bool v4 = parsed && !eth6;                   // an IPv4 datagram with sums to take
+    const bool fx = ETH && tx && proto == 6u && hl == 20u;   // MODE 3 TX TCP crc: by prefixes (50)
+    const bool tail = v4 && hl + tl < ilen;
+    const bool fb = (v4 && r + L2 + hl > 16u * HS) || (tail && r + len > 16u * HS) ||
+                    (v4 && hasx && !fx && r + L2 + hl + xo4 + 2u > 16u * HS);
+    if (__builtin_amdgcn_ballot_w64((ETH && walk6) || nat_opt || fb)) return false;
+    uint32_t optd = 0u, P2d = P2;
+    if (__builtin_amdgcn_ballot_w64(v4 && (hl > 20u || tail))) {
+        if (v4 && hl > 20u) optd = hw_range_sum<HS>(hw, r + L2 + 20u, r + L2 + hl);
+        if (tail) P2d = P2 - hw_range_sum<HS>(hw, r + L2 + hl + tl, r + len);
     }
-    if (__builtin_amdgcn_ballot_w64(ETH ? walk6 : nat_opt || fb)) return false;
-    uint32_t optd = 0u, P1d = P1, P2d = P2;
-    if constexpr (!ETH) {
-        if (__builtin_amdgcn_ballot_w64(parsed && (hl > 20u || tail))) {
-            if (parsed && hl > 20u) optd = hw_range_sum<HS>(hw, r + 20u, r + hl);
-            if (tail) P2d = P2 - hw_range_sum<HS>(hw, r + hl + tl, r + len);
-        }
-        P1d = P1 + optd;
-    }
+    const uint32_t P1d = P1 + optd;
     const bool odd = r & 1u;
-    // the field (frame pairing xp, even domain xe): from the head window, or (MODE 3, options or
-    // the TX TCP crc past the head chunks) by prefixes
+    // the field (frame pairing xp, even domain xe): from the head window, or (MODE 3 TX TCP without
+    // options: frame + 50, past the head chunks at some starts) by prefixes
     uint32_t xe = 0, xp = 0;
     if (hasx) {
-        if (!ETH || (hl == 20u && !(tx && proto == 6u))) {
+        if (!fx) {
             xp = lds_pair(wl, r + L2 + hl + xo4);
             xe = odd ? ((xp >> 8) | (xp << 8)) & 0xFFFFu : xp;
         } else {
@@ -1361,7 +1345,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // NAT: the old port leaves the region in the even domain (no wrap below zero), the new enters
     const uint32_t noe = odd ? ((nop >> 8) | (nop << 8)) & 0xFFFFu : nop;
     const uint32_t tsum = tx ? pairing(P2d - P1d - xe - noe, odd) + xp + nnw : pairing(P2d - P1d, odd);
-    const uint32_t opt = hl > 20u ? pairing(ETH ? P1 - P0 : optd, odd) : 0u;
+    const uint32_t opt = hl > 20u ? pairing(optd, odd) : 0u;
     // the IPv4 header's line and offset (finish stores relative to it)
     // (MODE 3 IPv6: the transport's line and offset; finish stores the field relative to it)
     const uint32_t ri = (r + (eth6 ? 54u : L2)) & 15u;
