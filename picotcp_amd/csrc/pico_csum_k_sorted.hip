@@ -905,11 +905,9 @@ __device__ __forceinline__ uint32_t lds_pair(const uint32_t* wl, uint32_t pos) {
 }
 
 template <bool NATM, bool V6 = false, bool ETH = false>
-__device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<true>* lds_all, uint32_t lane,
-                                             uint32_t wv, uint64_t f0) {
+__device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane, uint64_t f0) {
     constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
     if (!ETH && (p.flags & F_MACF)) return false;
-    StreamLds& S = lds_all[wv].st;
     const uint32_t cnt = f0 < p.n ? (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0) : 0u;
     const bool tx = (p.flags & 2u) != 0;
     constexpr bool natm = NATM;
@@ -929,6 +927,22 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     const uint32_t blen = valid ? len : 0u;
     const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
     const uint64_t la = addr & ~(uint64_t)15;
+    // MODE 3: the first step's loads go out before the span is worked out: 8 KiB from lane 0's
+    // frame's line (where a burst's span starts) through a window clamped to the batch buffer. They
+    // are kept when the span does start there -- bytes past the span's end only ever enter prefixes
+    // past every frame (a span longer than one step fills its first step) -- else the step is
+    // loaded again. (Measured: c2eth 23.3-23.5 against 24.5-24.7 us; C2 / C2-IPv6 no better, C2
+    // 21.5-21.8 against 21.2, so MODE 1 / MODE 2 load after the setup: profiles/r04/ab_spec_first_step.txt)
+    // (whole lines, as the span's own window: a buffer load partly past its window's end returns
+    // zeros for all of it, and a frame's last line can run past the batch buffer's end)
+    const uint64_t lo0 = uniform64(la);
+    const uint64_t bend = (reinterpret_cast<uintptr_t>(p.base) + p.base_len + 15u) & ~(uint64_t)15;
+    const Window w0 = make_window(lo0, (uint32_t)min((uint64_t)(16u * SQ), bend > lo0 ? bend - lo0 : 0ull));
+    uint4 v[SCPL], vn[SCPL];
+    if constexpr (ETH) {
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) v[c] = load_win<true>(w0, 16u * (64u * c + lane));
+    }
     // ---- the span: anchor, extent, layout
     uint64_t anchor = ~0ull;
     int mn = 0, mx = 0;
@@ -1000,8 +1014,7 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, SortedWaveSmem<t
     // NAT: the record is in before the loop (an older load still in flight at the loop leaves the
     // compiler's wait counting with a vmcnt(0) at every stage write)
     if constexpr (NATM) asm volatile("" ::"v"(rw.x), "v"(rw.y));
-    uint4 v[SCPL], vn[SCPL];
-    load_step(0u, v);
+    if (!ETH || lo != lo0) load_step(0u, v);             // MODE 3: the span starts elsewhere
     STAMP(1);
     // one step: cur is staged and summed while nxt's loads (step st + 1) are in flight
     auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
@@ -1375,10 +1388,9 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
     if ((uint64_t)blockIdx.x * (blockDim.x >> 6) * p.fpw < p.n) {     // workgroup-uniform
         if constexpr (MODE != 0) {
             bool done;
-            if constexpr (MODE == 2) done = stream_batch<false, true>(p, lds_all, lane, wv, f0);
-            else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, lds_all, lane, wv, f0);
-            else done = (p.flags & F_NAT) ? stream_batch<true>(p, lds_all, lane, wv, f0)
-                                          : stream_batch<false>(p, lds_all, lane, wv, f0);
+            if constexpr (MODE == 2) done = stream_batch<false, true>(p, S.st, lane, f0);
+            else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, S.st, lane, f0);
+            else done = (p.flags & F_NAT) ? stream_batch<true>(p, S.st, lane, f0) : stream_batch<false>(p, S.st, lane, f0);
             if (done) return;
         }
         if (f0 < p.n) sorted_batch<MODE, NT, CPL, SMALL>(p, S.s, S.stage, lane, f0);
