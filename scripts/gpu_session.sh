@@ -8,6 +8,10 @@ O=$R/gpurun_out
 TAG=${1:-r04a}
 mkdir -p $O
 cd $R
+# provenance: the library rebuilt from source on the box (make -B), build() then loads it
+timeout -k 10 600 make -s -B -j16 -C picotcp_amd/csrc > $O/build_$TAG.log 2>&1
+timeout -k 10 600 python -c "import __graft_entry__ as g; g.build(); print('build ok')" >> $O/build_$TAG.log 2>&1
+echo "build ok"
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1
 echo "tests ok"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1
