@@ -1,3 +1,7 @@
+#!/bin/bash
+# Per-wave stamps (tools/stamps.py) of the diagnostic builds (make -C picotcp_amd/csrc diag; the
+# round-3 one built from picotcp_amd/ab/r03): remove ./picotcp_amd/diag from .gpurunignore first,
+# so the libraries travel to the box.
 set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 for v in stamps stamps_r03; do
