@@ -255,7 +255,10 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
  * with an all-zero tuple is a duplicate).  NULL: a zero state, not kept.  Calls that share a d_state
  * must be ordered (one stream).  Regions past base_len or shorter than 20 bytes are V_MALFORMED,
  * untouched, and leave the state alone.  d_verdict is required (the batch order is resolved through
- * it).  Three kernel launches on `stream`. */
+ * it).  The descriptors of one batch must not overlap: each header is updated by one lane with a
+ * plain read-modify-write, so two descriptors on the same header would race on its TTL / crc
+ * (the reference, handed the same frame twice, would apply both decrements in sequence).  Three
+ * kernel launches on `stream`. */
 struct pico_csum_fwd_state {
     uint32_t src;       /* last_src, as stored */
     uint32_t dst;       /* last_dst */

@@ -29,19 +29,32 @@
 static uint32_t be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
 
 /* A datagram the stack would route on (pico_ipv4_process_finally_try_forward, pico_ipv4.c:467;
- * pico_ipv6_process_in's forward, pico_ipv6.c:845): its transport checksum is never checked. */
+ * pico_ipv6_process_in's forward, pico_ipv6.c:845-853): its transport checksum is never checked.
+ * IPv4: not a local address, broadcast or multicast (pico_ipv4.c:458-467) -- and no 0.0.0.0 link
+ * on the stack, which takes every such datagram into UDP's queue instead (:353-361, checked there).
+ * IPv6: unicast and not local; when the first header is hop-by-hop (nxthdr 0) the reference
+ * forwards only if `hbh->ext.routing.routtype` is 0 -- read through f->transport_hdr, which on RX
+ * still points at the frame buffer's start there (pico_frame.c:112; nothing on the path from
+ * pico_stack_recv sets it before pico_ipv6.c:789), so the byte is the Ethernet frame's byte 2,
+ * the destination MAC's third byte (0 for a 33:33:00:.. multicast MAC, not for the device's own
+ * 02:00:5e:..).  tests/test_burst_driver.py holds frames of both kinds. */
 static int forwarded4(const uint8_t *ip)
 {
-    struct pico_ip4 dst;
+    struct pico_ip4 dst, any;
     memcpy(&dst.addr, ip + 16, 4);
-    return !pico_ipv4_link_find(&dst) && !pico_ipv4_is_broadcast(dst.addr) && !pico_ipv4_is_multicast(dst.addr);
+    any.addr = 0u;
+    return !pico_ipv4_link_find(&dst) && !pico_ipv4_is_broadcast(dst.addr) && !pico_ipv4_is_multicast(dst.addr)
+           && !pico_ipv4_link_find(&any);
 }
 
-static int forwarded6(const uint8_t *ip)
+static int forwarded6(const uint8_t *frame)
 {
+    const uint8_t *ip = frame + 14;
     struct pico_ip6 dst;
     memcpy(dst.addr, ip + 24, 16);
-    return pico_ipv6_is_unicast(&dst) && !pico_ipv6_link_get(&dst);
+    if (!pico_ipv6_is_unicast(&dst) || pico_ipv6_link_get(&dst))
+        return 0;
+    return ip[6] != 0u || frame[2] == 0u;
 }
 
 /* The transport check of pico_transport_crc_check on `proto` (the network header's byte 9). */
@@ -104,7 +117,7 @@ static uint8_t burst_host_verdict(const uint8_t *f, uint32_t len)
         }
         plen = be16(ip + 4);
         tl = (plen - (off - 40u)) & 0xFFFFu;             /* pico_ipv6.c:790 */
-        if ((nh != 6u && nh != 17u) || off + tl > avail || forwarded6(ip))
+        if ((nh != 6u && nh != 17u) || off + tl > avail || forwarded6(f))
             return V_HAND_ON | PICO_CSUM_V_IPV6;
         memcpy(pseudo, ip + 8, 32);
         pseudo[32] = (uint8_t)(tl >> 24);
@@ -140,7 +153,7 @@ int pico_burst_hand_on(uint8_t verdict, const uint8_t *frame, uint32_t len)
     /* a transport checksum only matters to a datagram delivered here: one the stack routes on
      * goes on (a CRC=1 stack never checks it) */
     if (v == PICO_CSUM_V_L4_BAD)                   /* (an L4 verdict implies a whole IP header) */
-        return (verdict & PICO_CSUM_V_IPV6) ? len >= 54u && forwarded6(frame + 14)
+        return (verdict & PICO_CSUM_V_IPV6) ? len >= 54u && forwarded6(frame)
                                             : len >= 34u && forwarded4(frame + 14);
     return 0;
 }

@@ -56,6 +56,8 @@
  *   no-op variant, always 1).  rr_ipv6_link adds a non-tentative /64 IPv6 link (DAD done:
  *   pico_ipv6_link_add_no_dad) so unicast IPv6 to it is local.  The batched-driver test
  *   (tests/test_burst_driver.py) runs this in a CRC=1 and a CRC=0 build of the stack.
+ *   rr_take_forwarded: 1 when that frame was routed on instead (pico_ipv4_forward /
+ *   pico_ipv6_forward reached pico_datalink_send or an ICMP notice), 0 otherwise.
  * Callers (tests/golden/make_ref_rx.py, make_ref_reasm.py, make_ref_eth.py, make_ref_nat.py) only pass datagrams whose reference reads stay inside
  * avail and whose walk terminates (the oracle restatement decides which; the others are
  * restatement-only and documented so).
@@ -90,6 +92,15 @@ void __wrap_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame 
 void __wrap_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_frame *f, uint8_t proto);
 int32_t __wrap_pico_transport_receive(struct pico_frame *f, uint8_t proto);
 int __wrap_pico_arp_receive(struct pico_frame *f);
+int __real_pico_notify_dest_unreachable(struct pico_frame *f);
+int __real_pico_notify_ttl_expired(struct pico_frame *f);
+int __real_pico_notify_pkt_too_big(struct pico_frame *f);
+int32_t __real_pico_datalink_send(struct pico_frame *f);
+int __wrap_pico_notify_dest_unreachable(struct pico_frame *f);
+int __wrap_pico_notify_ttl_expired(struct pico_frame *f);
+int __wrap_pico_notify_pkt_too_big(struct pico_frame *f);
+int32_t __wrap_pico_datalink_send(struct pico_frame *f);
+int rr_take_forwarded(void);
 int32_t rr_ethernet_receive(struct pico_frame *f);
 int rr_eth_init(const uint8_t *mac);
 int rr_eth_rx(const uint8_t *d, uint32_t avail);
@@ -112,6 +123,7 @@ static int g_arp;
 static int g_frag, g_deliv_proto;
 static struct pico_frame *g_deliv;
 static int g_forward;          /* 1: call the real hand-offs (reassembly runs) */
+static int g_routed;           /* the frame entered a forwarding path (see the wrappers below) */
 
 void __wrap_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto)
 {
@@ -134,6 +146,34 @@ int32_t __wrap_pico_transport_receive(struct pico_frame *f, uint8_t proto)
     g_deliv = f;
     g_deliv_proto = proto;
     return 0;
+}
+
+/* Routing is observed where pico_ipv4_forward / pico_ipv6_forward (modules/pico_ipv4.c:1589-1617,
+ * modules/pico_ipv6.c:495-521) end: the datagram goes out (pico_datalink_send) or the stack gives
+ * up on it with an ICMP notification (no route, TTL / hop limit expired, too big).  The real
+ * functions still run; the wrappers only note that the frame was routed, not delivered. */
+int __wrap_pico_notify_dest_unreachable(struct pico_frame *f)
+{
+    g_routed = 1;
+    return __real_pico_notify_dest_unreachable(f);
+}
+
+int __wrap_pico_notify_ttl_expired(struct pico_frame *f)
+{
+    g_routed = 1;
+    return __real_pico_notify_ttl_expired(f);
+}
+
+int __wrap_pico_notify_pkt_too_big(struct pico_frame *f)
+{
+    g_routed = 1;
+    return __real_pico_notify_pkt_too_big(f);
+}
+
+int32_t __wrap_pico_datalink_send(struct pico_frame *f)
+{
+    g_routed = 1;
+    return __real_pico_datalink_send(f);
 }
 
 /* ARP frames the Ethernet layer hands on are counted, not processed */
@@ -463,6 +503,7 @@ int rr_stack_rx(const uint8_t *frame, uint32_t len)
     }
     g_frag = 0;
     g_arp = 0;
+    g_routed = 0;
     r = pico_stack_recv(g_edev, (uint8_t *)frame, len);
     for (k = 0; k < 3; k++) {
         pico_devices_loop(64, PICO_LOOP_DIR_IN);
@@ -500,4 +541,12 @@ int rr_take_delivered(int *check)
         g_deliv = NULL;
     }
     return proto;
+}
+
+/* 1 when the last rr_stack_rx frame was routed on (forwarded, or given up with an ICMP notice). */
+int rr_take_forwarded(void)
+{
+    int r = g_routed;
+    g_routed = 0;
+    return r;
 }

@@ -207,14 +207,17 @@ def fwd_state(device) -> torch.Tensor:
     return torch.zeros(FWD_STATE_BYTES, dtype=torch.uint8, device=device)
 
 
-def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, local=(), state: torch.Tensor | None = None,
+def ipv4_forward_batch(base: torch.Tensor, desc: torch.Tensor, n: int, *, state: torch.Tensor | None, local=(),
                        verdict: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """pico_ipv4_pre_forward_checks (pico_ipv4.c:1535-1574) in batch order, in place on n datagrams:
     ttl - 1, then unless the TTL expired the reference's crc++, the local-source check against
     `local` (the host's link addresses as stored: uint32 little-endian views, <= 32) and the
-    duplicate check against the last forwarded tuple, carried in `state` (fwd_state(); None = a
-    zero state not kept).  Returns the verdicts (V_ACCEPT = forwarded, V_EXPIRED, V_LOCAL_SRC,
-    V_DUPLICATE, V_MALFORMED)."""
+    duplicate check against the last forwarded tuple, carried in `state` (fwd_state()).  `state`
+    is required: a sequence split over several calls must pass the same state tensor to each, as
+    the reference's statics carry the last tuple; `state=None` is the explicit one-shot mode (the
+    reference's zero initial state, nothing kept).  Descriptors of one batch must not overlap
+    (two descriptors on one header would race on its TTL / crc).  Returns the verdicts (V_ACCEPT
+    = forwarded, V_EXPIRED, V_LOCAL_SRC, V_DUPLICATE, V_MALFORMED)."""
     _require_device(base, "base")
     _require_u8(base, "base")
     _require_device(desc, "desc")

@@ -8,7 +8,8 @@
  * burst.bin (little-endian): u32 n, u32 n4, u32 n6, u8 mac[6], u16 0, u64 ring_len,
  *   u32 ipv4_link[n4], u8 ipv6_link[n6][16], struct pico_csum_desc desc[n], u8 ring[ring_len].
  * out.bin: i32 used_gpu, u8 verdict[n], i32 delivered[n] (the protocol handed to the transport
- *   layer, -1 none), i32 check[n] (pico_transport_crc_check on it: the CRC=0 no-op, 1; -1 none).
+ *   layer, -1 none), i32 check[n] (pico_transport_crc_check on it: the CRC=0 no-op, 1; -1 none),
+ *   i32 routed[n] (1: the stack routed the frame on instead, rr_take_forwarded).
  *
  * The frames go on one by one as pico_burst_rx hands them on (pico_burst_hand_on), each through
  * rr_stack_rx (pico_stack_recv + the receive loops) so every transport hand-off is attributed to
@@ -28,6 +29,7 @@ int rr_ipv4_link(uint32_t addr);
 int rr_ipv6_link(const uint8_t *addr16);
 int rr_stack_rx(const uint8_t *frame, uint32_t len);
 int rr_take_delivered(int *check);
+int rr_take_forwarded(void);
 
 static void *slurp(const char *path, size_t *size)
 {
@@ -56,7 +58,7 @@ int main(int argc, char **argv)
     uint32_t n, n4, n6, i;
     uint64_t ring_len;
     struct pico_csum_desc *desc;
-    int32_t *deliv, *check, used;
+    int32_t *deliv, *check, *routed, used;
     struct pico_csum_ctx *ctx = NULL;
     FILE *out;
     if (argc < 3 || !(in = slurp(argv[1], &size)) || size < 24)
@@ -85,6 +87,7 @@ int main(int argc, char **argv)
     verdict = malloc(n + 1u);
     deliv = malloc(4u * n + 4u);
     check = malloc(4u * n + 4u);
+    routed = malloc(4u * n + 4u);
     if (!(argc > 3 && strcmp(argv[3], "--no-gpu") == 0))
         ctx = pico_csum_ctx_create(0, 16u << 20);
     used = pico_burst_verdicts(ctx, mac, ring, ring_len, desc, n, verdict);
@@ -93,10 +96,12 @@ int main(int argc, char **argv)
     for (i = 0; i < n; i++) {
         deliv[i] = -1;
         check[i] = -1;
+        routed[i] = 0;
         if (!pico_burst_hand_on(verdict[i], ring + desc[i].off, desc[i].len))
             continue;
         rr_stack_rx(ring + desc[i].off, desc[i].len);
         deliv[i] = rr_take_delivered(&check[i]);
+        routed[i] = rr_take_forwarded();
     }
     if (ctx)
         pico_csum_ctx_destroy(ctx);
@@ -107,6 +112,7 @@ int main(int argc, char **argv)
     fwrite(verdict, 1, n, out);
     fwrite(deliv, 4, n, out);
     fwrite(check, 4, n, out);
+    fwrite(routed, 4, n, out);
     fclose(out);
     return 0;
 }

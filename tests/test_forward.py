@@ -181,7 +181,7 @@ def _gpu_run(buf, desc, local, steps, dev="cuda:0"):
     vs = []
     for s in range(0, desc.size, steps):
         k = min(steps, desc.size - s)
-        vs.append(batch.ipv4_forward_batch(d_buf, d_desc[16 * s:16 * (s + k)], k, local, st).cpu().numpy())
+        vs.append(batch.ipv4_forward_batch(d_buf, d_desc[16 * s:16 * (s + k)], k, local=local, state=st).cpu().numpy())
     torch.cuda.synchronize()
     return d_buf.cpu().numpy(), np.concatenate(vs), st.cpu().numpy()
 
@@ -241,7 +241,7 @@ def test_gpu_forward_long_discard_runs():
     buf2[np.arange(1000) * 64 + 8] = 1
     d_buf = torch.from_numpy(buf2).to("cuda:0")
     s = torch.from_numpy(np.array([(1, 2, 3, 4, 0)], O.FWD_STATE_DTYPE).view(np.uint8)).to("cuda:0")
-    v2 = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(d2, "cuda:0"), 1000, (), s).cpu().numpy()
+    v2 = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(d2, "cuda:0"), 1000, state=s).cpu().numpy()
     assert (v2 == V_EXPIRED).all()
     assert s.cpu().numpy().view(O.FWD_STATE_DTYPE)[0].tolist() == (1, 2, 3, 4, 0)
 
@@ -254,6 +254,6 @@ def test_gpu_forward_out_of_bounds_untouched():
     want = buf.copy()
     wv = O.batch_ipv4_forward(want, desc[[0, 3]])
     d_buf = torch.from_numpy(buf).to("cuda:0")
-    v = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(desc, "cuda:0"), 4).cpu().numpy()
+    v = batch.ipv4_forward_batch(d_buf, batch.desc_to_device(desc, "cuda:0"), 4, state=None).cpu().numpy()
     np.testing.assert_array_equal(v, [wv[0], V_MALFORMED, V_MALFORMED, wv[1]])
     np.testing.assert_array_equal(d_buf.cpu().numpy(), want)
