@@ -126,6 +126,8 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-verify", action="store_true", help="skip the parity check of the timed outputs")
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
+    p.add_argument("--stream", default="", help="WPS,FPW persistent stream waves of the fused batches "
+                                                  "(pico_csum_set_stream_shape; 255 = off)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch the K timed steps one by one from Python instead of replaying them as one "
                         "captured HIP graph")
@@ -157,7 +159,8 @@ def make_c2(n, device, seed, frame_bytes=0, keep_host=True, slot=0):
     # make every datagram valid with the TX kernel (untimed setup), so RX verify accepts
     batch.ipv4_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
+    # the host copy is the batch as the timed steps see it (valid checksums), for the CPU leg
+    return d_buf, d_desc, int(lens.sum()), (d_buf.cpu().numpy(), desc) if keep_host else None
 
 
 def make_c2v6(n, device, seed, keep_host=True):
@@ -168,7 +171,7 @@ def make_c2v6(n, device, seed, keep_host=True):
     d_desc = batch.desc_to_device(desc, device)
     batch.ipv6_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum()), (buf, desc) if keep_host else None
+    return d_buf, d_desc, int(lens.sum()), (d_buf.cpu().numpy(), desc) if keep_host else None
 
 
 MAC = bytes.fromhex("02005e0a0b0c")
@@ -194,7 +197,7 @@ def make_c2eth(n, device, seed, keep_host=True, mix=False):
     d_desc = batch.desc_to_device(desc, device)
     batch.eth_checksum_batch(d_buf, d_desc, n, flags=batch.F_TX | batch.F_WRITE)
     torch.cuda.synchronize(device)
-    return d_buf, d_desc, int(lens.sum()) + 14 * n, (buf, desc) if keep_host else None
+    return d_buf, d_desc, int(lens.sum()) + 14 * n, (d_buf.cpu().numpy(), desc) if keep_host else None
 
 
 FRAG = 1480                 # IPv4 fragment payload (MTU 1500 - 20 B header)
@@ -330,14 +333,48 @@ def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
 
 
 def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float, nat=None):
-    """The oracle's fused IPv4/IPv6/Ethernet restatement (oracle/pico_csum_oracle.c, a port of
-    the reference's callers over its pico_checksum) on 1 host core over a bounded sample
-    of the same datagrams (the reference's own IPv4/TCP modules need the whole stack)."""
+    """The reference's own per-datagram work on the host cores: oracle/_ref/libref_callers.so
+    (rc_batch_mt over the compiled reference modules: pico_checksum of the IPv4 header +
+    pico_tcp_checksum_ipv4 / _ipv6, f->sock NULL on RX; TX zeroes the crc fields, computes with a
+    socket carrying the header's addresses and stores both, as tcp_send + pico_ipv4_frame_push do;
+    the Ethernet burst by ethertype) over the batch as the timed steps see it, on 1 thread and on
+    the job's host-core share.  Where that library is absent (or for NAT, which has no single
+    reference entry point), the oracle's fused restatement on 1 thread (kind "port")."""
     from oracle import oracle as O
     buf, desc = host
+    threads, cores = cpu_threads()
+    if nat is None and O.ref_callers_available():
+        mode = {"ipv4": O.RC_TX4 if tx else O.RC_RX4, "ipv6": O.RC_RX6, "eth": O.RC_ETH}[kind]
+        if not (tx and kind != "ipv4"):
+            nbytes = int(desc["len"].astype(np.int64).sum())
+            work = buf.copy() if tx else buf
+            res = {}
+            for t in (1, threads):
+                secs, on, ol = O.ref_callers_batch(work, desc, mode, t)        # page-in / warm
+                reps = max(1, int(target_s / max(secs, 1e-3)))
+                tot = 0.0
+                for _ in range(reps):
+                    secs, on, ol = O.ref_callers_batch(work, desc, mode, t)
+                    tot += secs
+                res[t] = (nbytes * reps / tot / GIB, reps)
+            # the reference's values on this batch: every datagram is valid, so an RX pass gives 0 / 0
+            ok = int(((on == 0) & (ol == 0)).sum()) if not tx else None
+            what = {"ipv4": "IPv4 TX (crc fields zeroed, pico_tcp_checksum_ipv4 + pico_checksum of the header, stored)"
+                    if tx else "IPv4 RX (pico_checksum of the header + pico_tcp_checksum_ipv4)",
+                    "ipv6": "IPv6 RX (pico_tcp_checksum_ipv6)",
+                    "eth": "Ethernet burst RX (ethertype, then the IPv4 / IPv6 RX work)"}[kind]
+            out = {"value": round(res[threads][0], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                   "single_core_value": round(res[1][0], 3),
+                   "sample": f"all {desc.size} datagrams of the batch ({nbytes / 2**20:.0f} MiB), the reference's "
+                             f"compiled modules (oracle/_ref/libref_callers.so, gcc -O3), {what}, a struct pico_frame "
+                             f"per thread on the datagram in place; {res[threads][1]} passes on {threads} threads, "
+                             f"{res[1][1]} on 1 thread",
+                   "cpu_model": cpu_model(), "usable_cores": cores, "cgroup_cpu_max": cgroup_cpu()}
+            if ok is not None:
+                out["reference_accepts"] = ok
+            return out
     k = min(desc.size, 65536)
     sample, nbytes = desc[:k], int(desc["len"][:k].astype(np.int64).sum())
-    ipv6 = kind == "ipv6"
     fn = {"ipv6": lambda: O.batch_ipv6(buf, sample, tx=tx), "ipv4": lambda: O.batch_ipv4(buf, sample, tx=tx),
           "eth": lambda: O.batch_eth(buf, sample, mac=MAC, tx=tx)}[kind]
     if nat is not None:                                  # in place on a copy (idempotent: same records)
@@ -632,6 +669,8 @@ def main():
     red_dev = dev if backend == "nccl" else torch.device("cpu")
     if a.shape:
         batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
+    if a.stream:
+        batch.set_stream_shape(*[int(x) for x in a.stream.split(",")])
     cfg = CONFIGS[a.config]
 
     # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)

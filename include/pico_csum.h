@@ -415,6 +415,13 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);
 
+/* Tuning knob (tests / bench sweeps), per calling thread: the fused IPv4 / IPv6 / Ethernet batches'
+ * persistent stream waves -- waves_per_simd 2 or 4 (0 = automatic, PICO_CSUM_STREAM_OFF = one wave
+ * per group of frames, the sorted-rounds kernel's grid), fpw frames per group (0 = automatic).
+ * Results never depend on it. */
+#define PICO_CSUM_STREAM_OFF 0xFFu
+int pico_csum_set_stream_shape(uint32_t waves_per_simd, uint32_t fpw);
+
 #ifdef __cplusplus
 }
 #endif

@@ -287,3 +287,33 @@ def uniform_mt(base: np.ndarray, stride: int, length: int, n: int, nthreads: int
         fn = ctypes.cast(lib().oracle_checksum, ctypes.c_void_p)
     secs = lib().oracle_uniform_mt(fn, _p(base), stride, length, n, _p(out), nthreads)
     return secs, out
+
+
+REF_CALLERS_SO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libref_callers.so")
+RC_RX4, RC_RX6, RC_TX4, RC_ETH = 0, 1, 2, 3
+
+
+def ref_callers_available() -> bool:
+    return os.path.exists(REF_CALLERS_SO)
+
+
+def ref_callers_batch(base: np.ndarray, desc: np.ndarray, mode: int, threads: int):
+    """The reference's own per-datagram work (oracle/ref_callers_shim.c rc_batch_mt: pico_checksum
+    of the IPv4 header + pico_tcp/udp_checksum_ipv4/_ipv6, the compiled reference modules) over a
+    batch on `threads` pthreads.  TX (RC_TX4) writes the values into `base`.  Returns (seconds,
+    out_net, out_l4)."""
+    import time
+    if "callers" not in _rlibs:
+        L = ctypes.CDLL(REF_CALLERS_SO)
+        L.rc_batch_mt.restype = ctypes.c_int
+        L.rc_batch_mt.argtypes = [_vp, _vp, _u32, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        _rlibs["callers"] = L
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    n = desc.shape[0]
+    on, ol = np.zeros(n, np.uint16), np.zeros(n, np.uint16)
+    t0 = time.perf_counter()
+    rc = _rlibs["callers"].rc_batch_mt(_p(base), _p(desc), n, mode, threads, _p(on), _p(ol))
+    secs = time.perf_counter() - t0
+    if rc != 0:
+        raise RuntimeError(f"rc_batch_mt failed ({rc})")
+    return secs, on, ol

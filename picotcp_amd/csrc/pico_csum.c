@@ -35,7 +35,8 @@ int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t st
 #define KF_NAT 0x20000u
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
-                            uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
+                            uint8_t *verdict, uint32_t fpw, uint64_t mac48, uint32_t pgrid, uint32_t pwps,
+                            void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
                                   uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
@@ -142,6 +143,19 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
 /* Launch-shape override: per calling thread (a test or sweep setting it cannot race a
  * launch from another thread). */
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
+static __thread uint32_t g_ovr_swps, g_ovr_sfpw;     /* persistent stream waves: 0 = automatic */
+
+int pico_csum_set_stream_shape(uint32_t waves_per_simd, uint32_t fpw)
+{
+    if (!(waves_per_simd == 0 || waves_per_simd == 2 || waves_per_simd == 4 ||
+          waves_per_simd == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "stream waves per SIMD must be 0 (auto), 2, 4 or PICO_CSUM_STREAM_OFF");
+    if (fpw > 64)
+        return fail(PICO_CSUM_EINVAL, "stream frames per group in [1, 64] (0 = auto)");
+    g_ovr_swps = waves_per_simd;
+    g_ovr_sfpw = fpw;
+    return 0;
+}
 
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline)
@@ -232,6 +246,26 @@ static int desc_fpw(uint32_t n, uint32_t *fpw)
     return 0;
 }
 
+static uint32_t cur_cus(void);
+
+/* The fused modes' persistent stream waves (pico_csum_k_sorted.hip, csum_stream_kernel): a grid of
+ * cus x wps workgroups (4 waves each) walking groups of sfpw frames, for batches with more groups
+ * than waves; *pgrid 0 = one wave per group (desc_fpw's shape). */
+static void desc_stream_shape(uint32_t n, uint32_t *fpw, uint32_t *pgrid, uint32_t *pwps)
+{
+    const uint32_t wps = g_ovr_swps ? g_ovr_swps : 2u, sf = g_ovr_sfpw ? g_ovr_sfpw : 64u;
+    const uint32_t cus = cur_cus();
+    *pgrid = 0;
+    *pwps = 0;
+    if (wps == PICO_CSUM_STREAM_OFF || g_ovr_group == 2)
+        return;
+    if (((uint64_t)n + sf - 1u) / sf > 4ull * cus * wps) {
+        *fpw = sf;
+        *pgrid = cus * wps;
+        *pwps = wps;
+    }
+}
+
 /* Device discovery runs once per process (pthread_once); compute-unit counts are read
  * per device, for the device current on the calling thread at launch. */
 #define MAX_DEVS 64
@@ -252,6 +286,15 @@ static void probe_devices(void)
                        cus > 0 ? (uint32_t)cus : 256u;
     }
     g_dev_count = count;
+}
+
+/* compute units of the device current on the calling thread */
+static uint32_t cur_cus(void)
+{
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= g_dev_count)
+        return 256u;
+    return g_dev_cus[d];
 }
 
 static int need_device(void)
@@ -295,7 +338,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags,
-                                                 d_out, d_bad, NULL, NULL, NULL, fpw, 0, stream),
+                                                 d_out, d_bad, NULL, NULL, NULL, fpw, 0, 0, 0, stream),
                          "pico_checksum_batch_dev");
 }
 
@@ -329,7 +372,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_net,
                                  uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
 {
-    uint32_t fpw = 0;
+    uint32_t fpw = 0, pgrid = 0, pwps = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -343,8 +386,10 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
+    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,
-                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
+                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, pgrid, pwps,
+                                                 stream),
                          "pico_ipv4_checksum_batch_dev");
 }
 
@@ -367,7 +412,7 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1,
                                                  PICO_CSUM_F_TX | PICO_CSUM_F_WRITE | KF_NAT, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw,
-                                                 (uint64_t)(uintptr_t)d_nat, stream),
+                                                 (uint64_t)(uintptr_t)d_nat, 0, 0, stream),
                          "pico_ipv4_nat_batch_dev");
 }
 
@@ -375,7 +420,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream)
 {
-    uint32_t fpw = 0;
+    uint32_t fpw = 0, pgrid = 0, pwps = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -391,8 +436,10 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_NXTHDR_DISPATCH is an RX option");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
+    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL,
-                                                 NULL, NULL, d_out_transport, d_verdict, fpw, 0, stream),
+                                                 NULL, NULL, d_out_transport, d_verdict, fpw, 0, pgrid, pwps,
+                                                 stream),
                          "pico_ipv6_checksum_batch_dev");
 }
 
@@ -401,7 +448,7 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
                                 uint8_t *d_verdict, void *stream)
 {
     uint64_t mac48 = 0;
-    uint32_t fpw = 0;
+    uint32_t fpw = 0, pgrid = 0, pwps = 0;
     int rc, i;
     if (n == 0)
         return 0;
@@ -422,8 +469,10 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
             mac48 |= (uint64_t)mac[i] << (8 * i);
         flags |= KF_MACF;
     }
+    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags, NULL, NULL,
-                                                 d_out_net, d_out_transport, d_verdict, fpw, mac48, stream),
+                                                 d_out_net, d_out_transport, d_verdict, fpw, mac48, pgrid, pwps,
+                                                 stream),
                          "pico_eth_checksum_batch_dev");
 }
 

@@ -3,6 +3,8 @@
 // Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
 #include "pico_csum_dev.h"
 
+#include <atomic>
+
 #ifndef SORTED_MODE
 #define SORTED_MODE 0
 #endif
@@ -1398,6 +1400,87 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
     STAMP(3);
 }
 
+// ---------------------------------------------------------------- persistent stream waves
+//
+// The kernel above runs one wave per 64-frame group: at 256K frames that is one residency round of
+// 4096 waves, every wave in the same phase at the same time -- descriptor round trips while HBM
+// idles at the start, a tail of late waves at the end (per-wave stamps).  Here a fixed
+// grid of waves (pwps per SIMD) walks the groups: group gw first, then groups claimed one at a time
+// from per-XCD heads (the dynamic groups split into 8 contiguous ranges; a wave claims from its
+// workgroup's XCD's range and moves on to the others once it is empty), each claim issued when the
+// previous group starts so its round trip hides behind that group's stream.  Waves drift apart, so
+// one wave's setup and finish overlap the others' streaming, and the dynamic claims end the
+// launch within about one group's time.  A group that is not streamed (not back to back, or
+// holding a frame the stream does not finish) takes the sorted rounds in the same wave.
+// The counters live in a slot of g_stream_ctl, one slot per launch (a ring the launcher walks);
+// the last wave to leave resets them, so a captured graph replays with the slot clean.
+struct StreamCtl {
+    uint32_t head[8];      // per-XCD claim counters
+    uint32_t done;         // waves that left
+    uint32_t pad[7];
+};
+constexpr uint32_t NCTL = 4096;
+__device__ StreamCtl g_stream_ctl[NCTL];
+
+__device__ __forceinline__ uint32_t ctl_add(uint32_t* a) {
+    return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MODE, int WPS>
+__global__ __launch_bounds__(64 * WPB, WPS) void csum_stream_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<true> lds_all[WPB];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    SortedWaveSmem<true>& S = lds_all[wv];
+    StreamCtl* const ctl = g_stream_ctl + p.ctl_slot;
+    const uint32_t P = gridDim.x * WPB;                        // persistent waves
+    const uint32_t ngroups = (uint32_t)(((uint64_t)p.n + p.fpw - 1u) / p.fpw);
+    const uint32_t dyn = ngroups > P ? ngroups - P : 0u;       // groups handed out by claims
+    const uint32_t R = (dyn + 7u) >> 3;                        // per XCD range
+    const uint32_t home = blockIdx.x & 7u;                     // workgroups go round-robin over the XCDs
+    uint32_t empty = dyn ? 0u : 0xFFu;                         // ranges found exhausted
+    uint32_t g = blockIdx.x * WPB + wv;
+    STAMP(0);
+    while (g < ngroups) {
+        // the next claim (home range) goes out before this group's loads
+        uint32_t k = 0xFFFFFFFFu;
+        const bool claim = !(empty & (1u << home));
+        if (claim && lane == 0) k = ctl_add(&ctl->head[home]);
+        const uint64_t f0 = (uint64_t)g * p.fpw;
+        bool done;
+        if constexpr (MODE == 2) done = stream_batch<false, true>(p, S.st, lane, f0);
+        else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, S.st, lane, f0);
+        else done = stream_batch<false>(p, S.st, lane, f0);
+        if (!done) sorted_batch<MODE, true, 8, true>(p, S.s, S.stage, lane, f0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // the claimed group, or the next range with groups left
+        g = ngroups;
+        if (claim) {
+            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+            const uint32_t sz = home * R < dyn ? min(R, dyn - home * R) : 0u;
+            if (k < sz) g = P + home * R + k;
+            else empty |= 1u << home;
+        }
+        for (uint32_t t = 1; g == ngroups && t < 8u; ++t) {
+            const uint32_t x = (home + t) & 7u;
+            if (empty & (1u << x)) continue;
+            uint32_t kx = 0;
+            if (lane == 0) kx = ctl_add(&ctl->head[x]);
+            kx = (uint32_t)__builtin_amdgcn_readfirstlane((int)kx);
+            const uint32_t sz = x * R < dyn ? min(R, dyn - x * R) : 0u;
+            if (kx < sz) g = P + x * R + kx;
+            else empty |= 1u << x;
+        }
+    }
+    // the last wave out resets the slot for the next launch that takes it
+    if (lane == 0 && ctl_add(&ctl->done) == P - 1u) {
+#pragma unroll
+        for (uint32_t x = 0; x < 8u; ++x) __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    STAMP(3);
+}
+
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- IPv4 forwarding step
 //
@@ -1583,6 +1666,16 @@ int SORTED_LAUNCH(const void* args, void* stream);
 int SORTED_LAUNCH(const void* args, void* stream) {
     const FlatArgs& a = *static_cast<const FlatArgs*>(args);
     const uint64_t waves = ((uint64_t)a.n + a.fpw - 1) / a.fpw;
+#if SORTED_MODE != 0
+    if (a.pgrid && !(a.flags & F_NAT) && waves > 4ull * a.pgrid) {
+        static std::atomic<uint32_t> slot{0};
+        FlatArgs b = a;
+        b.ctl_slot = slot.fetch_add(1u, std::memory_order_relaxed) % NCTL;
+        auto kern = a.pwps >= 4 ? csum_stream_kernel<SORTED_MODE, 4> : csum_stream_kernel<SORTED_MODE, 2>;
+        hipLaunchKernelGGL(kern, dim3(a.pgrid), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), b);
+        return (int)hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL(csum_sorted_kernel<SORTED_MODE>, dim3((unsigned)((waves + WPB - 1) / WPB)),
                        dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
@@ -1598,11 +1691,13 @@ int pico_csum_sorted_launch_mode3(const void* args, void* stream);
 // used when flags carry F_MACF (set by the host layer).
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t fpw, uint64_t mac48, void* stream) {
+                            uint8_t* verdict, uint32_t fpw, uint64_t mac48, uint32_t pgrid, uint32_t pwps,
+                            void* stream) {
     if (fpw < 1 || fpw > 64 || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
-               crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32)};
+               crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32),
+               pgrid, pwps, 0u};
     switch (mode) {
         case 0: return pico_csum_sorted_launch_mode0(&a, stream);
         case 1: return pico_csum_sorted_launch_mode1(&a, stream);
