@@ -77,6 +77,7 @@
 #include "pico_dev_null.h"
 #include "pico_nat.h"
 #include "pico_protocol.h"
+#include "pico_socket.h"
 
 int rr_ipv4_process_in(struct pico_frame *f);
 int rr_ipv4_crc_check(struct pico_frame *f);
@@ -101,6 +102,13 @@ int __wrap_pico_notify_ttl_expired(struct pico_frame *f);
 int __wrap_pico_notify_pkt_too_big(struct pico_frame *f);
 int32_t __wrap_pico_datalink_send(struct pico_frame *f);
 int rr_take_forwarded(void);
+int rr_tx_capture(uint8_t *buf, uint32_t cap, uint32_t *lens, uint32_t maxn);
+int rr_real_transport(int on);
+void *rr_socket(int proto, uint32_t addr, uint16_t port_be, int listen);
+int rr_sendto(void *s, const uint8_t *data, int len, uint32_t dst, uint16_t port_be);
+void *rr_accept(void *s);
+int rr_write(void *s, const uint8_t *data, int len);
+void rr_tick(int n);
 int32_t rr_ethernet_receive(struct pico_frame *f);
 int rr_eth_init(const uint8_t *mac);
 int rr_eth_rx(const uint8_t *d, uint32_t avail);
@@ -124,6 +132,9 @@ static int g_frag, g_deliv_proto;
 static struct pico_frame *g_deliv;
 static int g_forward;          /* 1: call the real hand-offs (reassembly runs) */
 static int g_routed;           /* the frame entered a forwarding path (see the wrappers below) */
+static int g_real_l4;          /* 1: pico_transport_receive runs for real (the TX capture) */
+static uint8_t *g_cap;         /* TX capture: datagrams handed to pico_datalink_send */
+static uint32_t g_cap_cap, g_cap_used, g_cap_n, g_cap_max, *g_cap_len;
 
 void __wrap_pico_ipv4_process_frag(struct pico_ipv4_hdr *hdr, struct pico_frame *f, uint8_t proto)
 {
@@ -141,6 +152,8 @@ void __wrap_pico_ipv6_process_frag(struct pico_ipv6_exthdr *frag, struct pico_fr
 
 int32_t __wrap_pico_transport_receive(struct pico_frame *f, uint8_t proto)
 {
+    if (g_real_l4)
+        return __real_pico_transport_receive(f, proto);
     if (g_deliv)
         pico_frame_discard(g_deliv);
     g_deliv = f;
@@ -173,6 +186,17 @@ int __wrap_pico_notify_pkt_too_big(struct pico_frame *f)
 int32_t __wrap_pico_datalink_send(struct pico_frame *f)
 {
     g_routed = 1;
+    if (g_cap && g_cap_n < g_cap_max && f->net_hdr) {
+        /* the IP datagram as the stack hands it to the link layer (its length from its own header) */
+        const uint8_t *ip = f->net_hdr;
+        const uint32_t v = ip[0] >> 4;
+        const uint32_t len = v == 4u ? ((uint32_t)ip[2] << 8 | ip[3]) : v == 6u ? 40u + ((uint32_t)ip[4] << 8 | ip[5]) : 0u;
+        if (len && g_cap_used + len <= g_cap_cap) {
+            memcpy(g_cap + g_cap_used, ip, len);
+            g_cap_used += len;
+            g_cap_len[g_cap_n++] = len;
+        }
+    }
     return __real_pico_datalink_send(f);
 }
 
@@ -549,4 +573,78 @@ int rr_take_forwarded(void)
     int r = g_routed;
     g_routed = 0;
     return r;
+}
+
+/*
+ * The TX capture (tests/test_ref_tx.py): the frames the CRC=1 stack itself emits -- TCP from
+ * tcp_send (modules/pico_tcp.c:968-985: SYN-ACKs, RSTs, data segments of an accepted connection),
+ * UDP from pico_udp_push (crc 0, :120), ICMPv4 echo replies (pico_icmp4_checksum, modules/
+ * pico_icmp4.c:30-41), each behind pico_ipv4_frame_push's header checksum (modules/pico_ipv4.c:1079)
+ * -- recorded where they reach pico_datalink_send.  rr_real_transport(1) lets received segments
+ * reach the real transport layer (the RX fixtures intercept it); rr_socket / rr_sendto /
+ * rr_accept / rr_write are the public socket API; rr_tick runs pico_stack_tick.
+ */
+int rr_tx_capture(uint8_t *buf, uint32_t cap, uint32_t *lens, uint32_t maxn)
+{
+    const int n = (int)g_cap_n;
+    g_cap = buf;
+    g_cap_cap = cap;
+    g_cap_len = lens;
+    g_cap_max = maxn;
+    g_cap_used = 0;
+    g_cap_n = 0;
+    return n;
+}
+
+int rr_real_transport(int on)
+{
+    g_real_l4 = on;
+    return 0;
+}
+
+static void rr_wakeup(uint16_t ev, struct pico_socket *s)
+{
+    (void)ev;
+    (void)s;
+}
+
+void *rr_socket(int proto, uint32_t addr, uint16_t port_be, int listen)
+{
+    struct pico_socket *s = pico_socket_open(PICO_PROTO_IPV4, (uint16_t)proto, rr_wakeup);
+    struct pico_ip4 a;
+    uint16_t port = port_be;
+    if (!s)
+        return NULL;
+    a.addr = addr;
+    if (pico_socket_bind(s, &a, &port) != 0 || (listen && pico_socket_listen(s, 8) != 0)) {
+        pico_socket_close(s);
+        return NULL;
+    }
+    return s;
+}
+
+int rr_sendto(void *s, const uint8_t *data, int len, uint32_t dst, uint16_t port_be)
+{
+    struct pico_ip4 a;
+    a.addr = dst;
+    return pico_socket_sendto((struct pico_socket *)s, data, len, &a, port_be);
+}
+
+void *rr_accept(void *s)
+{
+    struct pico_ip4 orig;
+    uint16_t port = 0;
+    return pico_socket_accept((struct pico_socket *)s, &orig, &port);
+}
+
+int rr_write(void *s, const uint8_t *data, int len)
+{
+    return pico_socket_write((struct pico_socket *)s, data, len);
+}
+
+void rr_tick(int n)
+{
+    int k;
+    for (k = 0; k < n; k++)
+        pico_stack_tick();
 }

@@ -37,6 +37,8 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, uint32_t pgrid, uint32_t pwps,
                             void *stream);
+int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
+                                    uint16_t *out, uint32_t fpw, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
                                   uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
@@ -147,11 +149,12 @@ static __thread uint32_t g_ovr_swps, g_ovr_sfpw;     /* persistent stream waves:
 
 int pico_csum_set_stream_shape(uint32_t waves_per_simd, uint32_t fpw)
 {
-    if (!(waves_per_simd == 0 || waves_per_simd == 2 || waves_per_simd == 4 ||
-          waves_per_simd == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "stream waves per SIMD must be 0 (auto), 2, 4 or PICO_CSUM_STREAM_OFF");
-    if (fpw > 64)
-        return fail(PICO_CSUM_EINVAL, "stream frames per group in [1, 64] (0 = auto)");
+    const uint32_t w = waves_per_simd & ~PICO_CSUM_STREAM_STATIC;
+    if (!(waves_per_simd == 0 || w == 2 || w == 4 || waves_per_simd == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "stream waves per SIMD must be 0 (auto), 2, 4 (| PICO_CSUM_STREAM_STATIC) or "
+                                        "PICO_CSUM_STREAM_OFF");
+    if (fpw > 65536)
+        return fail(PICO_CSUM_EINVAL, "stream frames per group / wave in [1, 65536] (0 = auto)");
     g_ovr_swps = waves_per_simd;
     g_ovr_sfpw = fpw;
     return 0;
@@ -253,16 +256,16 @@ static uint32_t cur_cus(void);
  * than waves; *pgrid 0 = one wave per group (desc_fpw's shape). */
 static void desc_stream_shape(uint32_t n, uint32_t *fpw, uint32_t *pgrid, uint32_t *pwps)
 {
-    const uint32_t wps = g_ovr_swps ? g_ovr_swps : 2u, sf = g_ovr_sfpw ? g_ovr_sfpw : 64u;
-    const uint32_t cus = cur_cus();
+    const uint32_t sw = g_ovr_swps ? g_ovr_swps : 2u, sf = g_ovr_sfpw && g_ovr_sfpw <= 64u ? g_ovr_sfpw : 64u;
+    const uint32_t cus = cur_cus(), wps = sw & 0xFFu;
     *pgrid = 0;
     *pwps = 0;
-    if (wps == PICO_CSUM_STREAM_OFF || g_ovr_group == 2)
+    if (sw == PICO_CSUM_STREAM_OFF || g_ovr_group == 2)
         return;
     if (((uint64_t)n + sf - 1u) / sf > 4ull * cus * wps) {
         *fpw = sf;
         *pgrid = cus * wps;
-        *pwps = wps;
+        *pwps = sw;
     }
 }
 
@@ -342,6 +345,23 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
                          "pico_checksum_batch_dev");
 }
 
+/* Uniform rings on the persistent stream waves (pico_csum_k_sorted.hip, csum_uniform_stream_kernel):
+ * densely packed frames (the span a wave reads is the frames' own bytes, give or take a small gap),
+ * no shape override, and -- where a frame can start at an odd address -- no carry out of 32 bits in
+ * the byte-swapped fold (len <= 65535, seed < 2^31).  Measured against uniform_shape's kernels:
+ * DESIGN.md 4. */
+static int uniform_stream_ok(const void *d_base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed)
+{
+    const uint64_t slack = len / 8u > 64u ? len / 8u : 64u;
+    if (g_ovr_group >= 4 || g_ovr_swps == PICO_CSUM_STREAM_OFF || n == 0 || len == 0)
+        return 0;
+    if (stride < len || stride > (uint64_t)len + slack || stride * 64u <= 2u * 8192u)
+        return 0;
+    if ((((uintptr_t)d_base | stride) & 1u) && (len > 65535u || seed >= 0x80000000u))
+        return 0;
+    return 1;
+}
+
 int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint64_t stride, uint32_t len,
                                     uint32_t n, uint32_t seed, uint16_t *d_out, void *stream)
 {
@@ -358,6 +378,17 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return rc;
     if (g_ovr_group == 2)
         return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
+    if (uniform_stream_ok(d_base, stride, len, n, seed)) {
+        /* frames per wave: a multiple of 64, one residency round of 4096 waves (16 per CU) where the
+         * batch fills it (C1: 64, C4: 1024) */
+        uint32_t fpw = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + 4u * 4u * cur_cus() - 1u) /
+                                                                (4u * 4u * cur_cus()));
+        if (!g_ovr_sfpw)
+            fpw = (fpw + 63u) & ~63u;
+        if ((uint64_t)(fpw - 1u) * stride + len + 32u < (1ull << 31))
+            return launch_status(pico_csum_launch_uniform_stream(d_base, stride, len, n, seed, d_out, fpw, stream),
+                                 "pico_checksum_batch_uniform_dev");
+    }
     s = uniform_shape(n, len);
     if (s.pipe && (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u)
         return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,

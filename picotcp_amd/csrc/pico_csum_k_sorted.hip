@@ -1416,8 +1416,9 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
 // the last wave to leave resets them, so a captured graph replays with the slot clean.
 struct StreamCtl {
     uint32_t head[8];      // per-XCD claim counters
-    uint32_t done;         // waves that left
-    uint32_t pad[7];
+    uint32_t done[8];      // per-XCD workgroups that left
+    uint32_t xcds;         // XCDs whose workgroups all left
+    uint32_t pad[15];
 };
 constexpr uint32_t NCTL = 4096;
 __device__ StreamCtl g_stream_ctl[NCTL];
@@ -1426,60 +1427,174 @@ __device__ __forceinline__ uint32_t ctl_add(uint32_t* a) {
     return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The persistent walk: group gw first, then (ctl != NULL) groups claimed from this workgroup's XCD's
+// range until it is empty, or (ctl NULL) every P-th group; process(g) runs one group on the whole
+// wave.  A range's claims come only from its XCD's waves (a wave whose range is empty leaves: no
+// cross-XCD stealing -- a failed claim on every other head was a serialised round trip per wave on
+// eight contended words, 7x the kernel's time in the first build).  Exit: one arrival per workgroup
+// on its XCD's counter, the XCD's last workgroup on the XCD counter, whose last arrival resets the
+// slot -- no wave waits on any of it.
+template <typename F>
+__device__ __forceinline__ void persistent_groups(StreamCtl* ctl, uint32_t ngroups, uint32_t lane, uint32_t wv,
+                                                  F&& process) {
+    const uint32_t P = gridDim.x * WPB;                        // persistent waves
+    uint32_t g = blockIdx.x * WPB + wv;
+    const uint32_t dyn = ctl && ngroups > P ? ngroups - P : 0u;   // groups handed out by claims
+    const uint32_t R = (dyn + 7u) >> 3;                        // per XCD range
+    const uint32_t home = blockIdx.x & 7u;                     // workgroups go round-robin over the XCDs
+    const uint32_t sz = home * R < dyn ? min(R, dyn - home * R) : 0u;
+    bool open = sz != 0u;
+    while (g < ngroups) {
+        // the next claim goes out before this group's loads
+        uint32_t k = 0xFFFFFFFFu;
+        if (open && lane == 0) k = ctl_add(&ctl->head[home]);
+        process(g);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (ctl) {
+            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+            open = open && k < sz;
+            g = open ? P + home * R + k : ngroups;
+        } else {
+            g += P;
+        }
+    }
+    if (!ctl) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t wgs = (gridDim.x - home + 7u) >> 3;                  // workgroups of this XCD
+        const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u;               // XCDs with workgroups
+        if (ctl_add(&ctl->done[home]) == wgs - 1u && ctl_add(&ctl->xcds) == nx - 1u) {
+#pragma unroll
+            for (uint32_t x = 0; x < 8u; ++x) {
+                __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->done[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_store(&ctl->xcds, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int MODE, int WPS>
 __global__ __launch_bounds__(64 * WPB, WPS) void csum_stream_kernel(FlatArgs p) {
     __shared__ SortedWaveSmem<true> lds_all[WPB];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     SortedWaveSmem<true>& S = lds_all[wv];
-    StreamCtl* const ctl = g_stream_ctl + p.ctl_slot;
-    const uint32_t P = gridDim.x * WPB;                        // persistent waves
     const uint32_t ngroups = (uint32_t)(((uint64_t)p.n + p.fpw - 1u) / p.fpw);
-    const uint32_t dyn = ngroups > P ? ngroups - P : 0u;       // groups handed out by claims
-    const uint32_t R = (dyn + 7u) >> 3;                        // per XCD range
-    const uint32_t home = blockIdx.x & 7u;                     // workgroups go round-robin over the XCDs
-    uint32_t empty = dyn ? 0u : 0xFFu;                         // ranges found exhausted
-    uint32_t g = blockIdx.x * WPB + wv;
     STAMP(0);
-    while (g < ngroups) {
-        // the next claim (home range) goes out before this group's loads
-        uint32_t k = 0xFFFFFFFFu;
-        const bool claim = !(empty & (1u << home));
-        if (claim && lane == 0) k = ctl_add(&ctl->head[home]);
+    persistent_groups(p.ctl_slot != NCTL ? g_stream_ctl + p.ctl_slot : nullptr, ngroups, lane, wv, [&](uint32_t g) {
         const uint64_t f0 = (uint64_t)g * p.fpw;
         bool done;
         if constexpr (MODE == 2) done = stream_batch<false, true>(p, S.st, lane, f0);
         else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, S.st, lane, f0);
         else done = stream_batch<false>(p, S.st, lane, f0);
         if (!done) sorted_batch<MODE, true, 8, true>(p, S.s, S.stage, lane, f0);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        // the claimed group, or the next range with groups left
-        g = ngroups;
-        if (claim) {
-            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
-            const uint32_t sz = home * R < dyn ? min(R, dyn - home * R) : 0u;
-            if (k < sz) g = P + home * R + k;
-            else empty |= 1u << home;
-        }
-        for (uint32_t t = 1; g == ngroups && t < 8u; ++t) {
-            const uint32_t x = (home + t) & 7u;
-            if (empty & (1u << x)) continue;
-            uint32_t kx = 0;
-            if (lane == 0) kx = ctl_add(&ctl->head[x]);
-            kx = (uint32_t)__builtin_amdgcn_readfirstlane((int)kx);
-            const uint32_t sz = x * R < dyn ? min(R, dyn - x * R) : 0u;
-            if (kx < sz) g = P + x * R + kx;
-            else empty |= 1u << x;
-        }
-    }
-    // the last wave out resets the slot for the next launch that takes it
-    if (lane == 0 && ctl_add(&ctl->done) == P - 1u) {
-#pragma unroll
-        for (uint32_t x = 0; x < 8u; ++x) __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    });
     STAMP(3);
 }
+
+#if SORTED_MODE == 0
+// ---------------------------------------------------------------- uniform rings: stream waves
+//
+// C1 / C3 / C4: frame i at base + i * stride, len bytes, densely packed (stride close to len).  Wave
+// w takes frames [w R, w R + R) and reads their span in address order, one continuous stream (64
+// lanes x SCPL coalesced 16-byte non-temporal buffer loads a step, the next step's loads in flight
+// while this one is summed -- stream_batch's loop, nothing parsed).  Lane j owns frames j, j + 64,
+// j + 128, ... of the range: it takes its frame's two prefixes (start, end) as their steps pass,
+// stores the frame's checksum and moves on to its next frame, so results leave during the stream
+// and no lane waits for the wave.  sum = end - start is exact mod 2^32 for an even start (the
+// reference's uint32 accumulator); an odd start is folded and byte-swapped, which the host allows
+// only where no carry can leave 32 bits (len <= 65535, seed < 2^31).  The host requires 64 frames
+// to span more than two steps, so a lane's next frame never starts in the step its last one ended.
+struct UniArgs {
+    uint8_t* base;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t n;
+    uint32_t seed;
+    uint32_t fpw;          // frames per wave (R)
+    uint16_t* out;
+};
+
+__device__ __forceinline__ void uniform_stream_range(const UniArgs& p, StreamLds& S, uint32_t lane, uint64_t f0) {
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    const uint64_t first = reinterpret_cast<uintptr_t>(p.base) + f0 * p.stride;
+    const uint64_t lo = first & ~(uint64_t)15;
+    const uint64_t end = first + (uint64_t)(cnt - 1u) * p.stride + p.len;
+    const uint32_t extent = (uint32_t)(((end + 15u) & ~(uint64_t)15) - lo);     // < 2^31 (host)
+    const Window w = make_window(lo, extent);
+    const uint32_t q1 = extent >> 4, nsteps = (q1 + SQ - 1u) / SQ;
+    const uint32_t r0 = (uint32_t)(first - lo);
+    const uint32_t nmine = lane < cnt ? (cnt - lane + 63u) >> 6 : 0u;   // this lane's frames
+    uint32_t m = 0;                                                   // its current one: lane + 64 m
+    uint32_t b1 = 0, b2 = 0, P1 = 0, P2 = 0;
+    bool t1 = false;                                                  // start prefix taken
+    auto frame_points = [&]() {
+        const uint32_t rel = r0 + (uint32_t)((uint64_t)(lane + 64u * m) * p.stride);
+        b1 = rel;
+        b2 = rel + p.len;
+        P1 = 0u;
+        t1 = rel == 0u;                                               // the span's first byte: prefix 0
+    };
+    if (nmine) frame_points();
+    uint32_t base = 0;
+    uint4 v[SCPL], vn[SCPL];
+    auto load_step = [&](uint32_t qs, uint4 (&dst)[SCPL]) {
+        const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, o + 1024u * c < oe ? o + 1024u * c : WIN_OOB);
+    };
+    load_step(0u, v);
+    auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
+        const uint32_t qb = st * SQ;
+        load_step(qb + SQ, nxt);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t loc[SCPL];
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; ++k) {
+            loc[k] = t;
+            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
+        }
+        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
+        const uint32_t exs = base + incs - t;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; k += 4)
+            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
+                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t byte0 = 16u * qb;
+        if (m < nmine) {
+            if (!t1) t1 = stream_point(S, b1, byte0, P1);
+            if (t1 && stream_point(S, b2, byte0, P2)) {
+                p.out[f0 + lane + 64u * m] = (uint16_t)finalize(p.seed + pairing(P2 - P1, (b1 & 1u) != 0u));
+                ++m;
+                if (m < nmine) frame_points();
+            }
+        }
+        base += tot;
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();               // every stage read before the next is written
+    };
+    for (uint32_t st = 0; st < nsteps; st += 2) {
+        step(st, v, vn);
+        if (st + 1u >= nsteps) break;
+        step(st + 1u, vn, v);
+    }
+}
+
+template <int WPS>
+__global__ __launch_bounds__(64 * WPB, WPS) void csum_uniform_stream_kernel(UniArgs p) {
+    __shared__ StreamLds lds_all[WPB];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t f0 = ((uint64_t)blockIdx.x * WPB + wv) * p.fpw;
+    if (f0 < p.n) uniform_stream_range(p, lds_all[wv], lane, f0);
+}
+#endif
 
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- IPv4 forwarding step
@@ -1670,8 +1785,8 @@ int SORTED_LAUNCH(const void* args, void* stream) {
     if (a.pgrid && !(a.flags & F_NAT) && waves > 4ull * a.pgrid) {
         static std::atomic<uint32_t> slot{0};
         FlatArgs b = a;
-        b.ctl_slot = slot.fetch_add(1u, std::memory_order_relaxed) % NCTL;
-        auto kern = a.pwps >= 4 ? csum_stream_kernel<SORTED_MODE, 4> : csum_stream_kernel<SORTED_MODE, 2>;
+        b.ctl_slot = (a.pwps & 0x100u) ? NCTL : slot.fetch_add(1u, std::memory_order_relaxed) % NCTL;
+        auto kern = (a.pwps & 0xFFu) >= 4 ? csum_stream_kernel<SORTED_MODE, 4> : csum_stream_kernel<SORTED_MODE, 2>;
         hipLaunchKernelGGL(kern, dim3(a.pgrid), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), b);
         return (int)hipGetLastError();
     }
@@ -1704,6 +1819,18 @@ int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uin
         case 2: return pico_csum_sorted_launch_mode2(&a, stream);
         default: return pico_csum_sorted_launch_mode3(&a, stream);
     }
+}
+
+// Uniform rings on the stream waves (pico_csum.c decides when: dense rings): fpw frames per wave.
+int pico_csum_launch_uniform_stream(const void* base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
+                                    uint16_t* out, uint32_t fpw, void* stream) {
+    if (n == 0) return (int)hipSuccess;
+    if (fpw < 1) return (int)hipErrorInvalidValue;
+    UniArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), stride, len, n, seed, fpw, out};
+    const uint64_t waves = ((uint64_t)n + fpw - 1u) / fpw;
+    hipLaunchKernelGGL(csum_uniform_stream_kernel<4>, dim3((unsigned)((waves + WPB - 1u) / WPB)), dim3(64 * WPB), 0,
+                       static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
 }
 
 int pico_csum_launch_ipv4_forward(void* base, uint64_t base_len, const void* desc, uint32_t n, const uint32_t* local,
