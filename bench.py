@@ -126,8 +126,8 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-verify", action="store_true", help="skip the parity check of the timed outputs")
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
-    p.add_argument("--stream", default="", help="WPS,FPW persistent stream waves of the fused batches "
-                                                  "(pico_csum_set_stream_shape; 255 = off)")
+    p.add_argument("--stream", default="", help="MODE,FPW the uniform rings' stream waves "
+                                                  "(pico_csum_set_uniform_stream: 1 on, 255 off; frames per wave)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch the K timed steps one by one from Python instead of replaying them as one "
                         "captured HIP graph")
@@ -670,7 +670,7 @@ def main():
     if a.shape:
         batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
     if a.stream:
-        batch.set_stream_shape(*[int(x) for x in a.stream.split(",")])
+        batch.set_uniform_stream(*[int(x) for x in a.stream.split(",")])
     cfg = CONFIGS[a.config]
 
     # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)

@@ -415,14 +415,12 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);
 
-/* Tuning knob (tests / bench sweeps), per calling thread: the persistent stream waves of the fused
- * IPv4 / IPv6 / Ethernet batches and of dense uniform rings -- waves_per_simd 2 or 4, optionally |
- * PICO_CSUM_STREAM_STATIC (every wave takes every P-th group instead of claiming them), 0 =
- * automatic, PICO_CSUM_STREAM_OFF = no persistent waves (one wave per group of frames / the
- * lane-group kernels); fpw frames per group (0 = automatic).  Results never depend on it. */
+/* Tuning knob (tests / bench sweeps), per calling thread: the uniform rings' stream waves
+ * (pico_checksum_batch_uniform_dev / _host on densely packed frames) -- mode 0 = automatic, 1 = on
+ * wherever the ring allows them, PICO_CSUM_STREAM_OFF = the lane-group kernels; frames_per_wave
+ * 0 = automatic.  Results never depend on it. */
 #define PICO_CSUM_STREAM_OFF 0xFFu
-#define PICO_CSUM_STREAM_STATIC 0x100u
-int pico_csum_set_stream_shape(uint32_t waves_per_simd, uint32_t fpw);
+int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
 
 #ifdef __cplusplus
 }

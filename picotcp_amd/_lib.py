@@ -45,7 +45,7 @@ EXPORTED = (
     "pico_csum_abi_version",
     "pico_csum_last_error",
     "pico_csum_set_launch_override",
-    "pico_csum_set_stream_shape",
+    "pico_csum_set_uniform_stream",
 )
 
 F_WRITE = 0x1
@@ -116,7 +116,7 @@ def load() -> ctypes.CDLL:
     sig("pico_csum_last_error", ctypes.c_char_p)
     sig("pico_csum_set_launch_override", ctypes.c_int, u32, u32, u32, u32, u32, u32)
     if hasattr(lib, "pico_csum_set_stream_shape"):       # (an A/B build of an older round may lack it)
-        sig("pico_csum_set_stream_shape", ctypes.c_int, u32, u32)
+        sig("pico_csum_set_uniform_stream", ctypes.c_int, u32, u32)
     del u8p
     if lib.pico_csum_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {lib.pico_csum_abi_version()}, this binding {ABI_VERSION}: rebuild it")

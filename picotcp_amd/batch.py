@@ -324,11 +324,11 @@ def _reassemble(v6, base, frag_desc, n_frag, groups, out, out_desc, flags, strea
 STREAM_OFF = 0xFF
 
 
-def set_stream_shape(waves_per_simd: int = 0, fpw: int = 0) -> None:
-    """The fused batches' persistent stream waves (tests / bench sweeps, this thread): waves per
-    SIMD 2 or 4, STREAM_OFF = one wave per frame group (the classic grid), 0 = automatic; fpw
-    frames per group (0 = automatic).  Results never depend on it (include/pico_csum.h)."""
-    _lib.check("pico_csum_set_stream_shape", _lib.load().pico_csum_set_stream_shape(waves_per_simd, fpw))
+def set_uniform_stream(mode: int = 0, frames_per_wave: int = 0) -> None:
+    """Uniform rings' stream waves (tests / bench sweeps, this thread): mode 0 automatic, 1 on where
+    the ring allows them, STREAM_OFF the lane-group kernels; frames per wave (0 = automatic).
+    Results never depend on it (include/pico_csum.h)."""
+    _lib.check("pico_csum_set_uniform_stream", _lib.load().pico_csum_set_uniform_stream(mode, frames_per_wave))
 
 
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,

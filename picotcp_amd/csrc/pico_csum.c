@@ -35,8 +35,7 @@ int pico_csum_launch_uniform_pf(const void *base, uint64_t base_len, uint64_t st
 #define KF_NAT 0x20000u
 int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t *out, uint32_t *bad, uint16_t *out_net, uint16_t *out_l4,
-                            uint8_t *verdict, uint32_t fpw, uint64_t mac48, uint32_t pgrid, uint32_t pwps,
-                            void *stream);
+                            uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t fpw, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
@@ -145,18 +144,16 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
 /* Launch-shape override: per calling thread (a test or sweep setting it cannot race a
  * launch from another thread). */
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
-static __thread uint32_t g_ovr_swps, g_ovr_sfpw;     /* persistent stream waves: 0 = automatic */
+static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 = automatic */
 
-int pico_csum_set_stream_shape(uint32_t waves_per_simd, uint32_t fpw)
+int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave)
 {
-    const uint32_t w = waves_per_simd & ~PICO_CSUM_STREAM_STATIC;
-    if (!(waves_per_simd == 0 || w == 2 || w == 4 || waves_per_simd == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "stream waves per SIMD must be 0 (auto), 2, 4 (| PICO_CSUM_STREAM_STATIC) or "
-                                        "PICO_CSUM_STREAM_OFF");
-    if (fpw > 65536)
-        return fail(PICO_CSUM_EINVAL, "stream frames per group / wave in [1, 65536] (0 = auto)");
-    g_ovr_swps = waves_per_simd;
-    g_ovr_sfpw = fpw;
+    if (!(mode == 0 || mode == 1 || mode == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "uniform stream mode must be 0 (auto), 1 (on) or PICO_CSUM_STREAM_OFF");
+    if (frames_per_wave > 65536)
+        return fail(PICO_CSUM_EINVAL, "frames per wave in [1, 65536] (0 = auto)");
+    g_ovr_smode = mode;
+    g_ovr_sfpw = frames_per_wave;
     return 0;
 }
 
@@ -251,24 +248,6 @@ static int desc_fpw(uint32_t n, uint32_t *fpw)
 
 static uint32_t cur_cus(void);
 
-/* The fused modes' persistent stream waves (pico_csum_k_sorted.hip, csum_stream_kernel): a grid of
- * cus x wps workgroups (4 waves each) walking groups of sfpw frames, for batches with more groups
- * than waves; *pgrid 0 = one wave per group (desc_fpw's shape). */
-static void desc_stream_shape(uint32_t n, uint32_t *fpw, uint32_t *pgrid, uint32_t *pwps)
-{
-    const uint32_t sw = g_ovr_swps ? g_ovr_swps : 2u, sf = g_ovr_sfpw && g_ovr_sfpw <= 64u ? g_ovr_sfpw : 64u;
-    const uint32_t cus = cur_cus(), wps = sw & 0xFFu;
-    *pgrid = 0;
-    *pwps = 0;
-    if (sw == PICO_CSUM_STREAM_OFF || g_ovr_group == 2)
-        return;
-    if (((uint64_t)n + sf - 1u) / sf > 4ull * cus * wps) {
-        *fpw = sf;
-        *pgrid = cus * wps;
-        *pwps = sw;
-    }
-}
-
 /* Device discovery runs once per process (pthread_once); compute-unit counts are read
  * per device, for the device current on the calling thread at launch. */
 #define MAX_DEVS 64
@@ -341,7 +320,7 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 0, crc_off, flags,
-                                                 d_out, d_bad, NULL, NULL, NULL, fpw, 0, 0, 0, stream),
+                                                 d_out, d_bad, NULL, NULL, NULL, fpw, 0, stream),
                          "pico_checksum_batch_dev");
 }
 
@@ -350,10 +329,12 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
  * no shape override, and -- where a frame can start at an odd address -- no carry out of 32 bits in
  * the byte-swapped fold (len <= 65535, seed < 2^31).  Measured against uniform_shape's kernels:
  * DESIGN.md 4. */
+#define UNIFORM_STREAM_MIN_LEN 4096u    /* automatic: frames of at least this many bytes (C3) */
+
 static int uniform_stream_ok(const void *d_base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed)
 {
     const uint64_t slack = len / 8u > 64u ? len / 8u : 64u;
-    if (g_ovr_group >= 4 || g_ovr_swps == PICO_CSUM_STREAM_OFF || n == 0 || len == 0)
+    if (g_ovr_group >= 4 || g_ovr_smode == PICO_CSUM_STREAM_OFF || n == 0 || len == 0)
         return 0;
     if (stride < len || stride > (uint64_t)len + slack || stride * 64u <= 2u * 8192u)
         return 0;
@@ -378,13 +359,10 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return rc;
     if (g_ovr_group == 2)
         return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
-    if (uniform_stream_ok(d_base, stride, len, n, seed)) {
-        /* frames per wave: a multiple of 64, one residency round of 4096 waves (16 per CU) where the
-         * batch fills it (C1: 64, C4: 1024) */
-        uint32_t fpw = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + 4u * 4u * cur_cus() - 1u) /
-                                                                (4u * 4u * cur_cus()));
-        if (!g_ovr_sfpw)
-            fpw = (fpw + 63u) & ~63u;
+    if (uniform_stream_ok(d_base, stride, len, n, seed) && (g_ovr_smode == 1 || len >= UNIFORM_STREAM_MIN_LEN)) {
+        /* frames per wave: one wave per SIMD over the whole batch (C3: 256 frames of 9000 B) */
+        const uint32_t waves = 4u * cur_cus();
+        const uint32_t fpw = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + waves - 1u) / waves);
         if ((uint64_t)(fpw - 1u) * stride + len + 32u < (1ull << 31))
             return launch_status(pico_csum_launch_uniform_stream(d_base, stride, len, n, seed, d_out, fpw, stream),
                                  "pico_checksum_batch_uniform_dev");
@@ -403,7 +381,7 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_net,
                                  uint16_t *d_out_transport, uint8_t *d_verdict, void *stream)
 {
-    uint32_t fpw = 0, pgrid = 0, pwps = 0;
+    uint32_t fpw = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -417,10 +395,8 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,
-                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, pgrid, pwps,
-                                                 stream),
+                                                 NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv4_checksum_batch_dev");
 }
 
@@ -443,7 +419,7 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1,
                                                  PICO_CSUM_F_TX | PICO_CSUM_F_WRITE | KF_NAT, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw,
-                                                 (uint64_t)(uintptr_t)d_nat, 0, 0, stream),
+                                                 (uint64_t)(uintptr_t)d_nat, stream),
                          "pico_ipv4_nat_batch_dev");
 }
 
@@ -451,7 +427,7 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
                                  uint32_t n, uint32_t flags, uint16_t *d_out_transport, uint8_t *d_verdict,
                                  void *stream)
 {
-    uint32_t fpw = 0, pgrid = 0, pwps = 0;
+    uint32_t fpw = 0;
     int rc;
     if (n == 0)
         return 0;
@@ -467,10 +443,8 @@ int pico_ipv6_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_NXTHDR_DISPATCH is an RX option");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 2, -1, flags, NULL,
-                                                 NULL, NULL, d_out_transport, d_verdict, fpw, 0, pgrid, pwps,
-                                                 stream),
+                                                 NULL, NULL, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv6_checksum_batch_dev");
 }
 
@@ -479,7 +453,7 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
                                 uint8_t *d_verdict, void *stream)
 {
     uint64_t mac48 = 0;
-    uint32_t fpw = 0, pgrid = 0, pwps = 0;
+    uint32_t fpw = 0;
     int rc, i;
     if (n == 0)
         return 0;
@@ -500,10 +474,8 @@ int pico_eth_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pi
             mac48 |= (uint64_t)mac[i] << (8 * i);
         flags |= KF_MACF;
     }
-    desc_stream_shape(n, &fpw, &pgrid, &pwps);
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 3, -1, flags, NULL, NULL,
-                                                 d_out_net, d_out_transport, d_verdict, fpw, mac48, pgrid, pwps,
-                                                 stream),
+                                                 d_out_net, d_out_transport, d_verdict, fpw, mac48, stream),
                          "pico_eth_checksum_batch_dev");
 }
 

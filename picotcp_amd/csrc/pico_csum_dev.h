@@ -460,9 +460,6 @@ struct FlatArgs {
     uint8_t* verdict;
     uint32_t mac_lo;      // ETH: the device's MAC as stored (bytes 0-3, 4-5), with F_MACF
     uint32_t mac_hi;
-    uint32_t pgrid;       // fused modes: persistent stream waves in workgroups (0: one wave per group)
-    uint32_t pwps;        // their waves per SIMD (1, 2, 4)
-    uint32_t ctl_slot;    // their claim counters (g_stream_ctl[ctl_slot], set by the launcher)
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;

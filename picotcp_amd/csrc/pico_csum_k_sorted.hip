@@ -3,8 +3,6 @@
 // Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
 #include "pico_csum_dev.h"
 
-#include <atomic>
-
 #ifndef SORTED_MODE
 #define SORTED_MODE 0
 #endif
@@ -1400,99 +1398,6 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
     STAMP(3);
 }
 
-// ---------------------------------------------------------------- persistent stream waves
-//
-// The kernel above runs one wave per 64-frame group: at 256K frames that is one residency round of
-// 4096 waves, every wave in the same phase at the same time -- descriptor round trips while HBM
-// idles at the start, a tail of late waves at the end (per-wave stamps).  Here a fixed
-// grid of waves (pwps per SIMD) walks the groups: group gw first, then groups claimed one at a time
-// from per-XCD heads (the dynamic groups split into 8 contiguous ranges; a wave claims from its
-// workgroup's XCD's range and moves on to the others once it is empty), each claim issued when the
-// previous group starts so its round trip hides behind that group's stream.  Waves drift apart, so
-// one wave's setup and finish overlap the others' streaming, and the dynamic claims end the
-// launch within about one group's time.  A group that is not streamed (not back to back, or
-// holding a frame the stream does not finish) takes the sorted rounds in the same wave.
-// The counters live in a slot of g_stream_ctl, one slot per launch (a ring the launcher walks);
-// the last wave to leave resets them, so a captured graph replays with the slot clean.
-struct StreamCtl {
-    uint32_t head[8];      // per-XCD claim counters
-    uint32_t done[8];      // per-XCD workgroups that left
-    uint32_t xcds;         // XCDs whose workgroups all left
-    uint32_t pad[15];
-};
-constexpr uint32_t NCTL = 4096;
-__device__ StreamCtl g_stream_ctl[NCTL];
-
-__device__ __forceinline__ uint32_t ctl_add(uint32_t* a) {
-    return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The persistent walk: group gw first, then (ctl != NULL) groups claimed from this workgroup's XCD's
-// range until it is empty, or (ctl NULL) every P-th group; process(g) runs one group on the whole
-// wave.  A range's claims come only from its XCD's waves (a wave whose range is empty leaves: no
-// cross-XCD stealing -- a failed claim on every other head was a serialised round trip per wave on
-// eight contended words, 7x the kernel's time in the first build).  Exit: one arrival per workgroup
-// on its XCD's counter, the XCD's last workgroup on the XCD counter, whose last arrival resets the
-// slot -- no wave waits on any of it.
-template <typename F>
-__device__ __forceinline__ void persistent_groups(StreamCtl* ctl, uint32_t ngroups, uint32_t lane, uint32_t wv,
-                                                  F&& process) {
-    const uint32_t P = gridDim.x * WPB;                        // persistent waves
-    uint32_t g = blockIdx.x * WPB + wv;
-    const uint32_t dyn = ctl && ngroups > P ? ngroups - P : 0u;   // groups handed out by claims
-    const uint32_t R = (dyn + 7u) >> 3;                        // per XCD range
-    const uint32_t home = blockIdx.x & 7u;                     // workgroups go round-robin over the XCDs
-    const uint32_t sz = home * R < dyn ? min(R, dyn - home * R) : 0u;
-    bool open = sz != 0u;
-    while (g < ngroups) {
-        // the next claim goes out before this group's loads
-        uint32_t k = 0xFFFFFFFFu;
-        if (open && lane == 0) k = ctl_add(&ctl->head[home]);
-        process(g);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (ctl) {
-            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
-            open = open && k < sz;
-            g = open ? P + home * R + k : ngroups;
-        } else {
-            g += P;
-        }
-    }
-    if (!ctl) return;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t wgs = (gridDim.x - home + 7u) >> 3;                  // workgroups of this XCD
-        const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u;               // XCDs with workgroups
-        if (ctl_add(&ctl->done[home]) == wgs - 1u && ctl_add(&ctl->xcds) == nx - 1u) {
-#pragma unroll
-            for (uint32_t x = 0; x < 8u; ++x) {
-                __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl->done[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __hip_atomic_store(&ctl->xcds, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-template <int MODE, int WPS>
-__global__ __launch_bounds__(64 * WPB, WPS) void csum_stream_kernel(FlatArgs p) {
-    __shared__ SortedWaveSmem<true> lds_all[WPB];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    SortedWaveSmem<true>& S = lds_all[wv];
-    const uint32_t ngroups = (uint32_t)(((uint64_t)p.n + p.fpw - 1u) / p.fpw);
-    STAMP(0);
-    persistent_groups(p.ctl_slot != NCTL ? g_stream_ctl + p.ctl_slot : nullptr, ngroups, lane, wv, [&](uint32_t g) {
-        const uint64_t f0 = (uint64_t)g * p.fpw;
-        bool done;
-        if constexpr (MODE == 2) done = stream_batch<false, true>(p, S.st, lane, f0);
-        else if constexpr (MODE == 3) done = stream_batch<false, false, true>(p, S.st, lane, f0);
-        else done = stream_batch<false>(p, S.st, lane, f0);
-        if (!done) sorted_batch<MODE, true, 8, true>(p, S.s, S.stage, lane, f0);
-    });
-    STAMP(3);
-}
-
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- uniform rings: stream waves
 //
@@ -1781,16 +1686,6 @@ int SORTED_LAUNCH(const void* args, void* stream);
 int SORTED_LAUNCH(const void* args, void* stream) {
     const FlatArgs& a = *static_cast<const FlatArgs*>(args);
     const uint64_t waves = ((uint64_t)a.n + a.fpw - 1) / a.fpw;
-#if SORTED_MODE != 0
-    if (a.pgrid && !(a.flags & F_NAT) && waves > 4ull * a.pgrid) {
-        static std::atomic<uint32_t> slot{0};
-        FlatArgs b = a;
-        b.ctl_slot = (a.pwps & 0x100u) ? NCTL : slot.fetch_add(1u, std::memory_order_relaxed) % NCTL;
-        auto kern = (a.pwps & 0xFFu) >= 4 ? csum_stream_kernel<SORTED_MODE, 4> : csum_stream_kernel<SORTED_MODE, 2>;
-        hipLaunchKernelGGL(kern, dim3(a.pgrid), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), b);
-        return (int)hipGetLastError();
-    }
-#endif
     hipLaunchKernelGGL(csum_sorted_kernel<SORTED_MODE>, dim3((unsigned)((waves + WPB - 1) / WPB)),
                        dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
@@ -1806,13 +1701,11 @@ int pico_csum_sorted_launch_mode3(const void* args, void* stream);
 // used when flags carry F_MACF (set by the host layer).
 int pico_csum_launch_sorted(void* base, uint64_t base_len, const void* desc, uint32_t n, int mode, int32_t crc_off,
                             uint32_t flags, uint16_t* out, uint32_t* bad, uint16_t* out_net, uint16_t* out_l4,
-                            uint8_t* verdict, uint32_t fpw, uint64_t mac48, uint32_t pgrid, uint32_t pwps,
-                            void* stream) {
+                            uint8_t* verdict, uint32_t fpw, uint64_t mac48, void* stream) {
     if (fpw < 1 || fpw > 64 || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
-               crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32),
-               pgrid, pwps, 0u};
+               crc_off, flags, out, bad, out_net, out_l4, verdict, (uint32_t)mac48, (uint32_t)(mac48 >> 32)};
     switch (mode) {
         case 0: return pico_csum_sorted_launch_mode0(&a, stream);
         case 1: return pico_csum_sorted_launch_mode1(&a, stream);
