@@ -105,6 +105,10 @@ CONFIGS = {
                                "1448 B fragments (45 per datagram, 40 B header + 8 B fragment header, 14 B Ethernet "
                                "gap each), each fragment's extension headers walked, gathered into reassembled "
                                "buffers with the TCP pseudo-header check of each datagram in the same pass"),
+    "c3_reasm_il": dict(kind="frag", frames=4096, frame_bytes=64512, interleave=True,
+                        workload="C3 reassembly, fragments of the 4K datagrams interleaved as a NIC receives "
+                                 "concurrent flows (fragment k of every datagram, then k + 1, ...), otherwise as "
+                                 "c3_reasm"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -204,7 +208,7 @@ FRAG = 1480                 # IPv4 fragment payload (MTU 1500 - 20 B header)
 FRAG6 = 1448                # IPv6 fragment payload (MTU 1500 - 40 B header - 8 B fragment header, 8-aligned)
 
 
-def make_frag(n, tl, device, seed, v6=False):
+def make_frag(n, tl, device, seed, v6=False, interleave=False):
     """n IPv4/TCP (IPv6/TCP) datagrams of tl transport bytes as in-order 1480 B (1448 B)
     fragments, each behind a 14 B gap, built on the device (vectorized); the TCP checksum made
     valid with one untimed reassembly pass.  Returns (buffer, fragment descriptors, groups, out,
@@ -220,6 +224,9 @@ def make_frag(n, tl, device, seed, v6=False):
     buf = torch.randint(0, 256, (n * per,), dtype=torch.uint8, device=device, generator=g)
     rel = np.concatenate([[0], np.cumsum(fsz)[:-1]]) + 14          # header offsets in one datagram
     net = (np.arange(n, dtype=np.int64)[:, None] * per + rel[None, :]).reshape(-1)
+    if interleave:     # arrival order fragment-major: fragment k of datagrams 0..n-1, then k + 1
+        kstart = np.concatenate([[0], np.cumsum(fsz * n)[:-1]])     # where fragment k's run starts
+        net = (kstart[None, :] + np.arange(n, dtype=np.int64)[:, None] * fsz[None, :] + 14).reshape(-1)
     hdr = np.zeros((n, nf, hl), np.uint8)
     tot = hl + pl
     if v6:
@@ -740,7 +747,7 @@ def main():
         n, ln = cfg["frames"], cfg["frame_bytes"]
         rot = a.rotate or max(2, rotation(2 * n * ln))
         v6 = bool(cfg.get("v6"))
-        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6) for i in range(rot)]
+        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6, bool(cfg.get("interleave"))) for i in range(rot)]
         res = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 

@@ -329,7 +329,10 @@ int pico_checksum_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
  * no shape override, and -- where a frame can start at an odd address -- no carry out of 32 bits in
  * the byte-swapped fold (len <= 65535, seed < 2^31).  Measured against uniform_shape's kernels:
  * DESIGN.md 4. */
-#define UNIFORM_STREAM_MIN_LEN 4096u    /* automatic: frames of at least this many bytes (C3) */
+/* automatic: rings of at least 1 GiB.  One long stream per SIMD beats the lane-group kernels there
+ * (C3 -5 %, C3 64 KiB -6 %, C4 -3.6 %) but not on C1's 375 MiB (+6 %: the XCDs' dispatch stagger
+ * is a larger share of a shorter stream), profiles/r05/ab_uniform_stream_*.txt */
+#define UNIFORM_STREAM_MIN_BYTES (1ull << 30)
 
 static int uniform_stream_ok(const void *d_base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed)
 {
@@ -359,8 +362,10 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return rc;
     if (g_ovr_group == 2)
         return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
-    if (uniform_stream_ok(d_base, stride, len, n, seed) && (g_ovr_smode == 1 || len >= UNIFORM_STREAM_MIN_LEN)) {
-        /* frames per wave: one wave per SIMD over the whole batch (C3: 256 frames of 9000 B) */
+    if (uniform_stream_ok(d_base, stride, len, n, seed) &&
+        (g_ovr_smode == 1 || (uint64_t)n * stride >= UNIFORM_STREAM_MIN_BYTES)) {
+        /* frames per wave: one wave per SIMD over the whole batch (C3: 256 frames of 9000 B, C4: 4096
+         * of 1500 B) */
         const uint32_t waves = 4u * cur_cus();
         const uint32_t fpw = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + waves - 1u) / waves);
         if ((uint64_t)(fpw - 1u) * stride + len + 32u < (1ull << 31))
@@ -551,24 +556,29 @@ int pico_ipv6_reassemble_batch_dev(const void *d_base, uint64_t base_len, const 
 /* descriptors per chunk of a host-resident descriptor batch (>= 64 bytes a frame on average) */
 #define CTX_MAX_DESC(staging) ((staging) / 64u + 64u)
 
+/* staging slots (a buffer, a stream, an event each): the uniform ring alternates slots 0 and 1 (its
+ * chunks need no per-chunk host work); descriptor batches rotate over all NSLOT, so the host loop
+ * waits on the chunk three back, not two (r05: C2 staged) */
+#define NSLOT 3
+
 struct pico_csum_ctx {
     int device;
     uint64_t staging;          /* bytes per staging buffer */
-    void *d_buf[2];
-    uint16_t *d_out[2];
-    hipStream_t st[2];
-    hipEvent_t done[2];
+    void *d_buf[NSLOT];
+    uint16_t *d_out[NSLOT];
+    hipStream_t st[NSLOT];
+    hipEvent_t done[NSLOT];
     /* descriptor batches (allocated on first use): rebased descriptors (pinned host ->
      * device) and the per-frame results of a chunk */
-    struct pico_csum_desc *h_desc[2], *d_desc[2];
+    struct pico_csum_desc *h_desc[NSLOT], *d_desc[NSLOT];
     /* a chunk's results, packed [net: 2 cnt B | transport: 2 cnt B | verdict: cnt B], so one D2H
      * brings them all back */
-    uint8_t *d_res[2];
+    uint8_t *d_res[NSLOT];
     /* pinned result staging: the D2H stays asynchronous (into pageable memory HIP would block
      * the host loop until it completes, serialising the chunks); copied out when the slot is
      * next reused or at the end */
-    uint8_t *h_res[2];
-    uint32_t pend_first[2], pend_cnt[2];
+    uint8_t *h_res[NSLOT];
+    uint32_t pend_first[NSLOT], pend_cnt[NSLOT];
     int desc_ready;
 };
 
@@ -587,7 +597,7 @@ struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes)
     c->device = device;
     c->staging = staging_bytes;
     if (hipSetDevice(device) != hipSuccess) { fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", device); free(c); return NULL; }
-    for (i = 0; i < 2; i++) {
+    for (i = 0; i < NSLOT; i++) {
         if (hipMalloc(&c->d_buf[i], staging_bytes) != hipSuccess ||
             hipMalloc((void **)&c->d_out[i], 2u * CTX_MAX_FRAMES(staging_bytes)) != hipSuccess ||
             hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking) != hipSuccess ||
@@ -606,7 +616,7 @@ void pico_csum_ctx_destroy(struct pico_csum_ctx *c)
     if (!c)
         return;
     hipSetDevice(c->device);
-    for (i = 0; i < 2; i++) {
+    for (i = 0; i < NSLOT; i++) {
         if (c->st[i]) hipStreamSynchronize(c->st[i]);
         if (c->d_buf[i]) hipFree(c->d_buf[i]);
         if (c->d_out[i]) hipFree(c->d_out[i]);
@@ -692,7 +702,7 @@ enum { HB_RAW = 0, HB_IPV4 = 1, HB_IPV6 = 2, HB_ETH = 3 };
 static void ctx_desc_free(struct pico_csum_ctx *c)
 {
     int i;
-    for (i = 0; i < 2; i++) {
+    for (i = 0; i < NSLOT; i++) {
         if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
         if (c->d_desc[i]) hipFree(c->d_desc[i]);
         if (c->d_res[i]) hipFree(c->d_res[i]);
@@ -710,7 +720,7 @@ static int ctx_desc_alloc(struct pico_csum_ctx *c)
     int i;
     if (c->desc_ready)
         return 0;
-    for (i = 0; i < 2; i++) {
+    for (i = 0; i < NSLOT; i++) {
         if (hipHostMalloc((void **)&c->h_desc[i], nd * sizeof(struct pico_csum_desc), hipHostMallocDefault) != hipSuccess ||
             hipMalloc((void **)&c->d_desc[i], nd * sizeof(struct pico_csum_desc)) != hipSuccess ||
             hipMalloc((void **)&c->d_res[i], nd * 5u) != hipSuccess ||
@@ -746,7 +756,9 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
 {
     const uint64_t maxd = CTX_MAX_DESC(c ? c->staging : 0);
     const int write = (flags & PICO_CSUM_F_WRITE) != 0;
-    uint64_t wlo[2] = {UINT64_MAX, UINT64_MAX}, whi[2] = {0, 0};   /* F_WRITE hulls issued per stream */
+    uint32_t k;
+    int o;
+    uint64_t wlo[NSLOT], whi[NSLOT];            /* F_WRITE hulls issued per stream */
     uint32_t i = 0;
     int b = 0, rc = 0;
     if (!c || !base || !desc)
@@ -761,7 +773,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
     if ((rc = ctx_desc_alloc(c)) != 0)
         return rc;
-    c->pend_cnt[0] = c->pend_cnt[1] = 0;
+    for (k = 0; k < NSLOT; k++) {
+        c->pend_cnt[k] = 0;
+        wlo[k] = UINT64_MAX;
+        whi[k] = 0;
+    }
     /* results of slot bb's last chunk, from pinned staging to the caller's arrays */
 #define FLUSH(bb)                                                                                  \
     do {                                                                                           \
@@ -782,7 +798,7 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
     }
     while (i < n) {
         uint64_t lo = UINT64_MAX, hi = 0, hlo = UINT64_MAX;
-        uint32_t j = i, k, cnt;
+        uint32_t j = i, cnt;
         hipError_t e;
         int vbase;
         uint8_t *kbase, *r_ver;
@@ -834,8 +850,12 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         r_net = (uint16_t *)c->d_res[b];
         r_l4 = (uint16_t *)(c->d_res[b] + 2u * (size_t)cnt);
         r_ver = c->d_res[b] + 4u * (size_t)cnt;
-        if (write && hi > hlo && hlo < whi[b ^ 1] && wlo[b ^ 1] < hi)
-            TRY(hipStreamWaitEvent(c->st[b], c->done[b ^ 1], 0), "stream wait")
+        for (o = 0; o < NSLOT && rc == 0; o++)      /* F_WRITE hulls of the other streams' chunks */
+            if (o != b && write && hi > hlo && hlo < whi[o] && wlo[o] < hi)
+                if ((e = hipStreamWaitEvent(c->st[b], c->done[o], 0)) != hipSuccess)
+                    rc = fail(PICO_CSUM_EIO, "%s: stream wait: %s", what, hipGetErrorString(e));
+        if (rc)
+            break;
         if (hi > lo)
             TRY(hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice, c->st[b]), "H2D")
         TRY(hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
@@ -873,16 +893,16 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         }
         TRY(hipEventRecord(c->done[b], c->st[b]), "event record")
         i = j;
-        b ^= 1;
+        b = b + 1 == NSLOT ? 0 : b + 1;
     }
 #undef TRY
-    /* drain both streams whatever happened: no copy may land after the return */
-    if (hipStreamSynchronize(c->st[0]) != hipSuccess || hipStreamSynchronize(c->st[1]) != hipSuccess)
-        if (!rc) rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
-    if (!rc) {
-        FLUSH(0);
-        FLUSH(1);
-    }
+    /* drain every stream whatever happened: no copy may land after the return */
+    for (o = 0; o < NSLOT; o++)
+        if (hipStreamSynchronize(c->st[o]) != hipSuccess && !rc)
+            rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
+    if (!rc)
+        for (o = 0; o < NSLOT; o++)
+            FLUSH(o);
 #undef FLUSH
     return rc;
 }
