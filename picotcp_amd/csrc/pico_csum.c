@@ -38,6 +38,8 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t fpw, void *stream);
+int pico_csum_launch_uniform_chunks(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
+                                    uint16_t *out, uint32_t cf, uint32_t waves, int dyn, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
                                   uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
@@ -148,8 +150,9 @@ static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 
 
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave)
 {
-    if (!(mode == 0 || mode == 1 || mode == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "uniform stream mode must be 0 (auto), 1 (on) or PICO_CSUM_STREAM_OFF");
+    if (!(mode <= 3 || mode == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "uniform stream mode must be 0 (auto), 1 (ranges), 2 (claimed chunks), "
+                                        "3 (chunks, static order) or PICO_CSUM_STREAM_OFF");
     if (frames_per_wave > 65536)
         return fail(PICO_CSUM_EINVAL, "frames per wave in [1, 65536] (0 = auto)");
     g_ovr_smode = mode;
@@ -362,8 +365,18 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return rc;
     if (g_ovr_group == 2)
         return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
+    if (uniform_stream_ok(d_base, stride, len, n, seed) && (g_ovr_smode == 2 || g_ovr_smode == 3)) {
+        /* one wave per SIMD over chunks of cf frames, about 4 chunks per wave at least */
+        const uint32_t waves = 4u * cur_cus();
+        uint32_t cf = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + 4u * waves - 1u) / (4u * waves));
+        cf = cf < 1u ? 1u : cf > 64u ? 64u : cf;
+        if ((uint64_t)(cf - 1u) * stride + len + 32u < (1ull << 31))
+            return launch_status(pico_csum_launch_uniform_chunks(d_base, stride, len, n, seed, d_out, cf, waves,
+                                                                 g_ovr_smode == 2, stream),
+                                 "pico_checksum_batch_uniform_dev");
+    }
     if (uniform_stream_ok(d_base, stride, len, n, seed) &&
-        (g_ovr_smode == 1 || (uint64_t)n * stride >= UNIFORM_STREAM_MIN_BYTES)) {
+        (g_ovr_smode == 1 || (g_ovr_smode == 0 && (uint64_t)n * stride >= UNIFORM_STREAM_MIN_BYTES))) {
         /* frames per wave: one wave per SIMD over the whole batch (C3: 256 frames of 9000 B, C4: 4096
          * of 1500 B) */
         const uint32_t waves = 4u * cur_cus();

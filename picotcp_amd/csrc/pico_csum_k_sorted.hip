@@ -3,6 +3,8 @@
 // Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
 #include "pico_csum_dev.h"
 
+#include <atomic>
+
 #ifndef SORTED_MODE
 #define SORTED_MODE 0
 #endif
@@ -1492,6 +1494,217 @@ __device__ __forceinline__ void uniform_stream_range(const UniArgs& p, StreamLds
     }
 }
 
+// ---- the same stream over claimed chunks (csum_uniform_chunk_kernel)
+//
+// One wave per SIMD reads fastest per byte (C3: 7.0 TB/s against 6.5 for a wave per 64 frames), but
+// a fixed range per wave leaves a tail: the XCDs start a few microseconds apart and the waves'
+// rates differ, about 13 us of a C1 launch (profiles/r05/ab_uniform_stream_*.txt).  Here the batch
+// is cut into chunks of cf frames (<= 64: lane j owns frame j of a chunk); wave w streams chunk w,
+// then chunks claimed from per-XCD ranges (an XCD's waves claim from its range, then from the
+// others once it is empty -- the balancing across XCDs), and the stream does not stop between
+// chunks: the next chunk's first step is loaded during this chunk's last one.  A claim is one
+// returning atomic, issued after a step's loads and read a step later (so the in-order vmcnt the
+// step's data waits on never includes it), once per chunk -- a few per wave, not a burst.
+struct StreamCtl {
+    uint32_t head[8];      // per-XCD claim counters
+    uint32_t done[8];      // per-XCD workgroups that left
+    uint32_t xcds;         // XCDs whose workgroups all left
+    uint32_t pad[15];
+};
+constexpr uint32_t NCTL = 4096;
+__device__ StreamCtl g_stream_ctl[NCTL];
+
+__device__ __forceinline__ uint32_t ctl_add(uint32_t* a) {
+    return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct UniChunkArgs {
+    uint8_t* base;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t n;
+    uint32_t seed;
+    uint32_t cf;           // frames per chunk (1 .. 64)
+    uint16_t* out;
+    uint32_t ctl_slot;     // NCTL: no claims (chunks w, w + P, ...)
+};
+
+struct ChunkSpan {
+    Window w;
+    uint32_t q1, nsteps, r0, cnt;
+};
+
+__device__ __forceinline__ ChunkSpan chunk_span(const UniChunkArgs& p, uint32_t c) {
+    ChunkSpan k;
+    const uint64_t f0 = (uint64_t)c * p.cf;
+    k.cnt = (uint32_t)min((uint64_t)p.cf, (uint64_t)p.n - f0);
+    const uint64_t first = reinterpret_cast<uintptr_t>(p.base) + f0 * p.stride;
+    const uint64_t lo = first & ~(uint64_t)15;
+    const uint64_t end = first + (uint64_t)(k.cnt - 1u) * p.stride + p.len;
+    const uint32_t extent = (uint32_t)(((end + 15u) & ~(uint64_t)15) - lo);
+    k.w = make_window(lo, extent);
+    k.q1 = extent >> 4;
+    k.nsteps = (k.q1 + SQ - 1u) / SQ;
+    k.r0 = (uint32_t)(first - lo);
+    return k;
+}
+
+template <int WPS>
+__global__ __launch_bounds__(64 * WPB, WPS) void csum_uniform_chunk_kernel(UniChunkArgs p) {
+    __shared__ StreamLds lds_all[WPB];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    StreamLds& S = lds_all[wv];
+    StreamCtl* const ctl = p.ctl_slot < NCTL ? g_stream_ctl + p.ctl_slot : nullptr;
+    const uint32_t P = gridDim.x * WPB;
+    const uint32_t nch = (uint32_t)(((uint64_t)p.n + p.cf - 1u) / p.cf);
+    const uint32_t dyn = ctl && nch > P ? nch - P : 0u;
+    const uint32_t R = (dyn + 7u) >> 3;
+    const uint32_t home = blockIdx.x & 7u;
+    constexpr uint32_t NO = 0xFFFFFFFFu;
+    uint32_t empty = dyn ? 0u : 0xFFu;       // claim ranges found exhausted
+    uint32_t c = blockIdx.x * WPB + wv;      // the chunk being streamed
+    uint32_t cn = NO;                        // the next one, once known
+    bool asked = false;                      // a claim has gone out for this chunk's successor
+    int xp = -1;                             // head of the claim in flight (its result read a step later)
+    uint32_t kp = 0;
+    auto range_size = [&](uint32_t x) { return x * R < dyn ? min(R, dyn - x * R) : 0u; };
+    auto next_head = [&]() -> int {          // the first non-empty range, home first
+        for (uint32_t t = 0; t < 8u; ++t) {
+            const uint32_t x = (home + t) & 7u;
+            if (!(empty & (1u << x))) return (int)x;
+        }
+        return -1;
+    };
+    auto issue_claim = [&]() {
+        const int x = next_head();
+        xp = x;
+        if (x >= 0 && lane == 0) kp = ctl_add(&ctl->head[x]);
+    };
+    auto read_claim = [&]() {                // the claim in flight: a chunk, or its range is empty
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kp);
+        const uint32_t x = (uint32_t)xp;
+        xp = -1;
+        if (k < range_size(x)) cn = P + x * R + k;
+        else empty |= 1u << x;
+    };
+    auto static_next = [&]() { cn = c + P < nch ? c + P : NO; };
+    if (c < nch) {
+        ChunkSpan k = chunk_span(p, c), kn;
+        kn.nsteps = 0;
+        // this lane's frame of the chunk: points (span positions), prefixes
+        uint32_t b1 = 0, b2 = 0, P1 = 0, P2 = 0, base = 0;
+        bool t1 = false;
+        auto frame_points = [&]() {
+            const uint32_t rel = k.r0 + (uint32_t)((uint64_t)lane * p.stride);
+            b1 = rel;
+            b2 = rel + p.len;
+            P1 = P2 = 0u;
+            t1 = rel == 0u;
+            base = 0u;
+        };
+        frame_points();
+        uint32_t st = 0;                     // step of chunk c being processed
+        uint4 v[SCPL], vn[SCPL];
+        auto load_to = [&](const Window& w, uint32_t qs, uint32_t q1, uint4 (&dst)[SCPL]) {
+            const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
+#pragma unroll
+            for (uint32_t cc = 0; cc < SCPL; ++cc)
+                dst[cc] = load_win<true>(w, o + 1024u * cc < oe ? o + 1024u * cc : WIN_OOB);
+        };
+        load_to(k.w, 0u, k.q1, v);
+        bool live = true;
+        auto step = [&](uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
+            // the successor must be known before the loads that follow this chunk's last step
+            if (st + 1u >= k.nsteps && cn == NO) {
+                if (!ctl) {
+                    static_next();
+                } else {
+                    if (xp >= 0) read_claim();
+                    while (cn == NO && next_head() >= 0) {
+                        issue_claim();
+                        read_claim();
+                    }
+                }
+                if (cn != NO) kn = chunk_span(p, cn);
+            }
+            if (st + 1u < k.nsteps) load_to(k.w, (st + 1u) * SQ, k.q1, nxt);
+            else if (cn != NO) load_to(kn.w, 0u, kn.q1, nxt);
+            asm volatile("" ::: "memory");
+            // claims ride behind the loads just issued: a result is read one step later
+            if (ctl) {
+                if (xp >= 0) {
+                    read_claim();
+                    if (cn != NO) kn = chunk_span(p, cn);
+                }
+                if (cn == NO && xp < 0 && next_head() >= 0 && (!asked || st + 1u < k.nsteps)) {
+                    issue_claim();
+                    asked = true;
+                }
+            }
+#pragma unroll
+            for (uint32_t cc = 0; cc < SCPL; ++cc) S.raw[sslot(64u * cc + lane)] = cur[cc];
+            __builtin_amdgcn_wave_barrier();
+            uint32_t loc[SCPL];
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < SCPL; ++q) {
+                loc[q] = t;
+                t = add_full<false>(S.raw[sslot(SCPL * lane + q)], SEL_EVEN, t);
+            }
+            const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
+            const uint32_t exs = base + incs - t;
+#pragma unroll
+            for (uint32_t q = 0; q < SCPL; q += 4)
+                *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + q]) =
+                    make_uint4(exs + loc[q], exs + loc[q + 1], exs + loc[q + 2], exs + loc[q + 3]);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t byte0 = 16u * st * SQ;
+            if (lane < k.cnt) {
+                if (!t1) t1 = stream_point(S, b1, byte0, P1);
+                if (t1) stream_point(S, b2, byte0, P2);
+            }
+            base += tot;
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (++st == k.nsteps) {          // the chunk's last step: results, then its successor
+                if (lane < k.cnt)
+                    p.out[(uint64_t)c * p.cf + lane] = (uint16_t)finalize(p.seed + pairing(P2 - P1, (b1 & 1u) != 0u));
+                c = cn;
+                cn = NO;
+                asked = false;
+                st = 0;
+                live = c != NO;
+                if (live) {
+                    k = kn;
+                    frame_points();
+                }
+            }
+        };
+        for (;;) {
+            step(v, vn);
+            if (!live) break;
+            step(vn, v);
+            if (!live) break;
+        }
+    }
+    if (!ctl) return;
+    // every wave is out of the loop: the last workgroup resets the slot (per-XCD arrivals)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t wgs = (gridDim.x - home + 7u) >> 3;
+        const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u;
+        if (ctl_add(&ctl->done[home]) == wgs - 1u && ctl_add(&ctl->xcds) == nx - 1u) {
+#pragma unroll
+            for (uint32_t x = 0; x < 8u; ++x) {
+                __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->done[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_store(&ctl->xcds, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int WPS>
 __global__ __launch_bounds__(64 * WPB, WPS) void csum_uniform_stream_kernel(UniArgs p) {
     __shared__ StreamLds lds_all[WPB];
@@ -1722,6 +1935,20 @@ int pico_csum_launch_uniform_stream(const void* base, uint64_t stride, uint32_t 
     UniArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), stride, len, n, seed, fpw, out};
     const uint64_t waves = ((uint64_t)n + fpw - 1u) / fpw;
     hipLaunchKernelGGL(csum_uniform_stream_kernel<4>, dim3((unsigned)((waves + WPB - 1u) / WPB)), dim3(64 * WPB), 0,
+                       static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
+}
+
+// Uniform rings on claimed chunks: waves workgroups' worth of one-per-SIMD waves, cf frames a chunk,
+// claims on (dyn) or static chunk order.
+int pico_csum_launch_uniform_chunks(const void* base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
+                                    uint16_t* out, uint32_t cf, uint32_t waves, int dyn, void* stream) {
+    static std::atomic<uint32_t> slot{0};
+    if (n == 0) return (int)hipSuccess;
+    if (cf < 1 || cf > 64 || waves < WPB) return (int)hipErrorInvalidValue;
+    UniChunkArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), stride, len, n, seed, cf, out,
+                   dyn ? slot.fetch_add(1u, std::memory_order_relaxed) % NCTL : NCTL};
+    hipLaunchKernelGGL(csum_uniform_chunk_kernel<1>, dim3(waves / WPB), dim3(64 * WPB), 0,
                        static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
