@@ -38,6 +38,9 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t fpw, void *stream);
+int pico_csum_launch_pstream(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
+                             uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t fpw, uint32_t wps,
+                             uint32_t cus, void *stream);
 int pico_csum_launch_uniform_chunks(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t cf, uint32_t waves, int dyn, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
@@ -147,6 +150,21 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
  * launch from another thread). */
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 = automatic */
+static __thread uint32_t g_ovr_pmode, g_ovr_pwps, g_ovr_pfpg;   /* persistent descriptor stream */
+
+int pico_csum_set_desc_stream(uint32_t mode, uint32_t waves_per_simd, uint32_t frames_per_group)
+{
+    if (!(mode <= 1 || mode == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "descriptor stream mode must be 0 (auto), 1 (on) or PICO_CSUM_STREAM_OFF");
+    if (waves_per_simd > 2)
+        return fail(PICO_CSUM_EINVAL, "waves per SIMD must be 1 or 2 (0 = auto)");
+    if (frames_per_group > 64)
+        return fail(PICO_CSUM_EINVAL, "frames per group in [1, 64] (0 = auto)");
+    g_ovr_pmode = mode;
+    g_ovr_pwps = waves_per_simd;
+    g_ovr_pfpg = frames_per_group;
+    return 0;
+}
 
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave)
 {
@@ -413,6 +431,14 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
+    if (g_ovr_pmode == 1 && g_ovr_group != 2 && n < 0x80000000u) {
+        /* the persistent stream waves (pico_csum_k_sorted.hip csum_pstream_kernel): a fixed grid
+         * streaming claimed groups back to back */
+        const uint32_t wps = g_ovr_pwps ? g_ovr_pwps : 1u, fpg = g_ovr_pfpg ? g_ovr_pfpg : 64u;
+        return launch_status(pico_csum_launch_pstream(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
+                                                      d_verdict, fpg, wps, cur_cus(), stream),
+                             "pico_ipv4_checksum_batch_dev");
+    }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv4_checksum_batch_dev");

@@ -906,217 +906,19 @@ __device__ __forceinline__ uint32_t lds_pair(const uint32_t* wl, uint32_t pos) {
     return __builtin_amdgcn_alignbyte(wl[q + 1], wl[q], pos & 3u) & 0xFFFFu;
 }
 
-template <bool NATM, bool V6 = false, bool ETH = false>
-__device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane, uint64_t f0) {
-    constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
-    if (!ETH && (p.flags & F_MACF)) return false;
-    const uint32_t cnt = f0 < p.n ? (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0) : 0u;
-    const bool tx = (p.flags & 2u) != 0;
+// The finish of a streamed group (stream_batch, the persistent waves): lane j's frame from its head
+// window and the prefixes taken at its points -- the verdict, the sums, the stores (finish_frame).
+// Returns false, with nothing written, for a group the stream does not finish (the sorted rounds
+// take it): options, a field or trailing bytes past the head window, an IPv6 walk, NAT with options.
+template <bool NATM, bool V6, bool ETH>
+__device__ __forceinline__ bool stream_finish(const FlatArgs& p, StreamLds& S, uint32_t lane, uint64_t f0,
+                                              uint32_t cnt, bool tx, uint2 rw, bool valid, bool oob, uint32_t len,
+                                              bool seeded, uint32_t rel, uint64_t lo, const uint4 (&hw)[HW],
+                                              uint32_t P0, uint32_t P1, uint32_t P2, uint32_t P3, uint32_t P4) {
+    constexpr uint32_t L2 = ETH ? 14u : 0u;
     constexpr bool natm = NATM;
-    uint4 dcur = make_uint4(0, 0, 0, 0);
-    if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
-    // NAT: the frame's record {addr, port | dir << 16} (sorted_batch's NAT stage)
-    uint2 rw = make_uint2(0u, 0u);
-    if (NATM && lane < cnt)
-        rw = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo) +
-                                             8ull * (f0 + lane));
-    uint64_t off0 = ((uint64_t)dcur.y << 32) | dcur.x;
-    uint32_t len = lane < cnt ? dcur.z : 0u;
-    const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
-    if (oob || lane >= cnt) { len = 0; off0 = 0; }
-    const bool valid = len >= (V6 ? 40u : ETH ? 14u : 20u);  // shorter: MALFORMED, nothing to sum
-    const bool seeded = ETH && dcur.w != 0u;     // MODE 3 IPv6 with a stack-walked net_len: sorted rounds
-    const uint32_t blen = valid ? len : 0u;
-    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
-    const uint64_t la = addr & ~(uint64_t)15;
-    // MODE 3: the first step's loads go out before the span is worked out: 8 KiB from lane 0's
-    // frame's line (where a burst's span starts) through a window clamped to the batch buffer. They
-    // are kept when the span does start there -- bytes past the span's end only ever enter prefixes
-    // past every frame (a span longer than one step fills its first step) -- else the step is
-    // loaded again. (Measured: c2eth 23.3-23.5 against 24.5-24.7 us; C2 / C2-IPv6 no better, C2
-    // 21.5-21.8 against 21.2, so MODE 1 / MODE 2 load after the setup: profiles/r04/ab_spec_first_step.txt)
-    // (whole lines, as the span's own window: a buffer load partly past its window's end returns
-    // zeros for all of it, and a frame's last line can run past the batch buffer's end)
-    const uint64_t lo0 = uniform64(la);
-    const uint64_t bend = (reinterpret_cast<uintptr_t>(p.base) + p.base_len + 15u) & ~(uint64_t)15;
-    const Window w0 = make_window(lo0, (uint32_t)min((uint64_t)(16u * SQ), bend > lo0 ? bend - lo0 : 0ull));
-    uint4 v[SCPL], vn[SCPL];
-    if constexpr (ETH) {
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) v[c] = load_win<true>(w0, 16u * (64u * c + lane));
-    }
-    // ---- the span: anchor, extent, layout
-    uint64_t anchor = ~0ull;
-    int mn = 0, mx = 0;
-    uint32_t q1 = 0u, nsteps = 0u;
-    {
-        const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
-        if (!vb) return false;
-        // a stack-walked IPv6 seed, or a frame over 1 MiB (the 32-bit byte sums): no stream
-        if (__builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20)))) return false;
-        const int fv = __builtin_ffsll((long long)vb) - 1;
-        anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
-        const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
-        if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
-        // frames in address order (a burst): the first valid frame's line (dl = 0) and the last
-        // one's end bound the span; a frame outside them makes the wave scan for both
-        mx = __builtin_amdgcn_readlane((int)dh, 63 - __builtin_clzll(vb));
-        if (__builtin_amdgcn_ballot_w64(valid && (dl < 0 || dh > (int64_t)mx))) {
-            mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
-            mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
-        }
-        const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
-        const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
-        if (!((uint64_t)ext <= 2ull * rs + 4096u)) return false;    // not back to back
-        q1 = ext >> 4;
-        nsteps = (q1 + SQ - 1u) / SQ;
-    }
-    const uint64_t lo = uniform64(anchor + (int64_t)mn);
-    const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
-    const Window w = make_window(lo, (uint32_t)extent);
-    const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;   // frame start in the span
-    const uint32_t r = rel & 15u, hq = rel >> 4;
-    // head-window chunks: the header and, without options, the crc field (r + 38 <= 64). (MODE 3
-    // with a fifth -- a padded 60-byte frame's end at any start -- spills into its loop: a padded
-    // frame starting past byte 4 of its line sends the wave to the sorted rounds instead)
     constexpr uint32_t HS = 4u;
-    const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
-    uint4 hw[HW];
-#pragma unroll
-    for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
-    // boundaries (span byte positions, 0 = none): options start, transport start / end, field
-    // MODE 3: b0 = an IPv6 datagram's addresses (frame + 22), which can lie in the step before the
-    // one that completes the header parse: set once the ethertype is in (chunk 1), which is never
-    // later than the step holding frame + 21
-    uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
-    bool pre6 = !ETH || !valid;
-    // No IPv4 parse in the loop: the options start (where the transport starts without options),
-    // the frame's end and, for TX, the TCP crc field's place without options (MODE 2: the transport
-    // start and the TCP crc at 56); the finish corrects them from the head window (options, bytes
-    // past the datagram, the field with options) or falls back. MODE 3 moves an IPv6 frame's points
-    // once its ethertype is in, and parses IPv6 headers in the loop (their field depends on them).
-    if (valid) {
-        b1 = rel + min(V6 ? 40u : L2 + 20u, len);
-        b2 = rel + len;
-        if (V6 && tx && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }
-        if (ETH && tx && 52u <= len) { x0 = rel + 50u; x1 = x0 + 2u; }
-    }
-    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
-    bool pre = !valid;
-    uint32_t base = 0;
-    // two steps in flight: step k + 1's loads go out before step k is staged and summed
-    // (loads issued on two paths -- a layout branch -- leave the compiler's wait counting at the
-    // join with a full vmcnt(0): the next step's loads waited on before this one is staged)
-    auto load_step = [&](uint32_t qs, uint4 (&dst)[SCPL]) {
-        const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, o + 1024u * c < oe ? o + 1024u * c : WIN_OOB);
-    };
-    // NAT: the record is in before the loop (an older load still in flight at the loop leaves the
-    // compiler's wait counting with a vmcnt(0) at every stage write)
-    if constexpr (NATM) asm volatile("" ::"v"(rw.x), "v"(rw.y));
-    if (!ETH || lo != lo0) load_step(0u, v);             // MODE 3: the span starts elsewhere
-    STAMP(1);
-    // one step: cur is staged and summed while nxt's loads (step st + 1) are in flight
-    auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
-        const uint32_t qb = st * SQ;
-        load_step(qb + SQ, nxt);
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
-        __builtin_amdgcn_wave_barrier();
-        // lane-major: lane L's SCPL chunks, chunk prefixes, one wave scan of the lane totals
-        uint32_t loc[SCPL];
-        uint32_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < SCPL; ++k) {
-            loc[k] = t;
-            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
-        }
-        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
-        const uint32_t exs = base + incs - t;
-#pragma unroll
-        for (uint32_t k = 0; k < SCPL; k += 4)
-            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
-                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
-        __builtin_amdgcn_wave_barrier();
-        // frame j's head window chunks that are in this step
-#pragma unroll
-        for (uint32_t i = 0; i < HS; ++i) {
-            const uint32_t qi = hq + i - qb;
-            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
-        }
-        // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
-        // fails the header checks below never reads them)
-        if (ETH && !pre6 && hq + 1u < qb + SQ) {
-            // the ethertype: an IPv6 frame's addresses, transport start (neither taken yet: both
-            // lie past chunk 1); anything else needs no parse in the loop
-            pre6 = true;
-            uint32_t T[1];
-            window_words<1, true>(hw, r + 12u, T);
-            if ((T[0] & 0xFFFFu) == 0xDD86u) {
-                b0 = rel + 22u;
-                b1 = rel + min(54u, len);
-                x0 = x1 = 0u;
-            } else {
-                pre = true;
-            }
-        }
-        if (ETH && !pre && hq + 2u < qb + SQ) {
-            // MODE 3: an IPv6 frame -- its transport end and field, by prefixes (past the head chunks)
-            {
-                pre = true;
-                uint32_t H[3];
-                window_words<3, true>(hw, r + 14u, H);
-                const uint32_t ilen = len - 14u;
-                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
-                const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
-                if (ilen >= 40u) {
-                    // (b0, b1 since the ethertype)
-                    b2 = rel + 14u + min(40u + plen, ilen);
-                    const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);
-                    if (xo != NONE && 40u + xo < ilen) {
-                        x0 = rel + 54u + xo;
-                        x1 = x0 + min(2u, ilen - 40u - xo);
-                    }
-                }
-            }
-        }
-        const uint32_t byte0 = 16u * qb;
-        stream_point(S, b1, byte0, P1);
-        stream_point(S, b2, byte0, P2);
-        // the optional points, each cleared once taken (the group is skipped once none is left)
-        if ((ETH || V6) && __builtin_amdgcn_ballot_w64((b0 | x0 | x1) != 0u)) {
-            b0 = stream_point(S, b0, byte0, P0) ? 0u : b0;
-            x0 = stream_point(S, x0, byte0, P3) ? 0u : x0;
-            x1 = stream_point(S, x1, byte0, P4) ? 0u : x1;
-        }
-        base += tot;
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();               // every stage read before the next is written
-    };
-    if constexpr (!ETH) {
-        // two steps a trip, the register sets swapping roles: each step's wait covers only its own
-        // loads (a copy of the next set into this one at the end of a trip would wait on them too,
-        // leaving one step in flight across the wait)
-        for (uint32_t st = 0; st < nsteps; st += 2) {
-            step(st, v, vn);
-            if (st + 1u >= nsteps) break;
-            step(st + 1u, vn, v);
-        }
-    } else {
-        // MODE 3 (both families' parse in the loop): one step a trip, the sets copied -- the
-        // two-step trip spills there
-        for (uint32_t st = 0; st < nsteps; ++st) {
-            step(st, v, vn);
-#pragma unroll
-            for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
-        }
-    }
-
-    STAMP(2);
+    const uint32_t r = rel & 15u;
     // the head window into the stage (free now), 144 bytes a lane: the finish takes its header
     // words and fields with aligned LDS reads and one alignbyte each, not select chains over hw
     static_assert(64u * 36u * sizeof(uint32_t) <= sizeof(StreamLds), "head windows must fit the stage");
@@ -1376,6 +1178,221 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     return true;
 }
 
+template <bool NATM, bool V6 = false, bool ETH = false>
+__device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, uint32_t lane, uint64_t f0) {
+    constexpr uint32_t L2 = ETH ? 14u : 0u;   // the IPv4 header's offset in the frame
+    if (!ETH && (p.flags & F_MACF)) return false;
+    const uint32_t cnt = f0 < p.n ? (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0) : 0u;
+    const bool tx = (p.flags & 2u) != 0;
+    constexpr bool natm = NATM;
+    uint4 dcur = make_uint4(0, 0, 0, 0);
+    if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
+    // NAT: the frame's record {addr, port | dir << 16} (sorted_batch's NAT stage)
+    uint2 rw = make_uint2(0u, 0u);
+    if (NATM && lane < cnt)
+        rw = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(((uint64_t)p.mac_hi << 32) | p.mac_lo) +
+                                             8ull * (f0 + lane));
+    uint64_t off0 = ((uint64_t)dcur.y << 32) | dcur.x;
+    uint32_t len = lane < cnt ? dcur.z : 0u;
+    const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
+    if (oob || lane >= cnt) { len = 0; off0 = 0; }
+    const bool valid = len >= (V6 ? 40u : ETH ? 14u : 20u);  // shorter: MALFORMED, nothing to sum
+    const bool seeded = ETH && dcur.w != 0u;     // MODE 3 IPv6 with a stack-walked net_len: sorted rounds
+    const uint32_t blen = valid ? len : 0u;
+    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
+    const uint64_t la = addr & ~(uint64_t)15;
+    // MODE 3: the first step's loads go out before the span is worked out: 8 KiB from lane 0's
+    // frame's line (where a burst's span starts) through a window clamped to the batch buffer. They
+    // are kept when the span does start there -- bytes past the span's end only ever enter prefixes
+    // past every frame (a span longer than one step fills its first step) -- else the step is
+    // loaded again. (Measured: c2eth 23.3-23.5 against 24.5-24.7 us; C2 / C2-IPv6 no better, C2
+    // 21.5-21.8 against 21.2, so MODE 1 / MODE 2 load after the setup: profiles/r04/ab_spec_first_step.txt)
+    // (whole lines, as the span's own window: a buffer load partly past its window's end returns
+    // zeros for all of it, and a frame's last line can run past the batch buffer's end)
+    const uint64_t lo0 = uniform64(la);
+    const uint64_t bend = (reinterpret_cast<uintptr_t>(p.base) + p.base_len + 15u) & ~(uint64_t)15;
+    const Window w0 = make_window(lo0, (uint32_t)min((uint64_t)(16u * SQ), bend > lo0 ? bend - lo0 : 0ull));
+    uint4 v[SCPL], vn[SCPL];
+    if constexpr (ETH) {
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) v[c] = load_win<true>(w0, 16u * (64u * c + lane));
+    }
+    // ---- the span: anchor, extent, layout
+    uint64_t anchor = ~0ull;
+    int mn = 0, mx = 0;
+    uint32_t q1 = 0u, nsteps = 0u;
+    {
+        const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
+        if (!vb) return false;
+        // a stack-walked IPv6 seed, or a frame over 1 MiB (the 32-bit byte sums): no stream
+        if (__builtin_amdgcn_ballot_w64(valid && ((V6 && dcur.w != 0u) || len > (1u << 20)))) return false;
+        const int fv = __builtin_ffsll((long long)vb) - 1;
+        anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+        const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
+        if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return false;
+        // frames in address order (a burst): the first valid frame's line (dl = 0) and the last
+        // one's end bound the span; a frame outside them makes the wave scan for both
+        mx = __builtin_amdgcn_readlane((int)dh, 63 - __builtin_clzll(vb));
+        if (__builtin_amdgcn_ballot_w64(valid && (dl < 0 || dh > (int64_t)mx))) {
+            mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
+            mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
+        }
+        const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)blen), 63);
+        const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
+        if (!((uint64_t)ext <= 2ull * rs + 4096u)) return false;    // not back to back
+        q1 = ext >> 4;
+        nsteps = (q1 + SQ - 1u) / SQ;
+    }
+    const uint64_t lo = uniform64(anchor + (int64_t)mn);
+    const uint64_t extent = (uint64_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
+    const Window w = make_window(lo, (uint32_t)extent);
+    const uint32_t rel = valid ? (uint32_t)(addr - lo) : 0u;   // frame start in the span
+    const uint32_t r = rel & 15u, hq = rel >> 4;
+    // head-window chunks: the header and, without options, the crc field (r + 38 <= 64). (MODE 3
+    // with a fifth -- a padded 60-byte frame's end at any start -- spills into its loop: a padded
+    // frame starting past byte 4 of its line sends the wave to the sorted rounds instead)
+    constexpr uint32_t HS = 4u;
+    const uint32_t nlh = valid ? min(HS, (r + len + 15u) >> 4) : 0u;
+    uint4 hw[HW];
+#pragma unroll
+    for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
+    // boundaries (span byte positions, 0 = none): options start, transport start / end, field
+    // MODE 3: b0 = an IPv6 datagram's addresses (frame + 22), which can lie in the step before the
+    // one that completes the header parse: set once the ethertype is in (chunk 1), which is never
+    // later than the step holding frame + 21
+    uint32_t b0 = 0, b1 = 0, b2 = 0, x0 = 0, x1 = 0;
+    bool pre6 = !ETH || !valid;
+    // No IPv4 parse in the loop: the options start (where the transport starts without options),
+    // the frame's end and, for TX, the TCP crc field's place without options (MODE 2: the transport
+    // start and the TCP crc at 56); the finish corrects them from the head window (options, bytes
+    // past the datagram, the field with options) or falls back. MODE 3 moves an IPv6 frame's points
+    // once its ethertype is in, and parses IPv6 headers in the loop (their field depends on them).
+    if (valid) {
+        b1 = rel + min(V6 ? 40u : L2 + 20u, len);
+        b2 = rel + len;
+        if (V6 && tx && 58u <= len) { x0 = rel + 56u; x1 = x0 + 2u; }
+        if (ETH && tx && 52u <= len) { x0 = rel + 50u; x1 = x0 + 2u; }
+    }
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
+    bool pre = !valid;
+    uint32_t base = 0;
+    // two steps in flight: step k + 1's loads go out before step k is staged and summed
+    // (loads issued on two paths -- a layout branch -- leave the compiler's wait counting at the
+    // join with a full vmcnt(0): the next step's loads waited on before this one is staged)
+    auto load_step = [&](uint32_t qs, uint4 (&dst)[SCPL]) {
+        const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(w, o + 1024u * c < oe ? o + 1024u * c : WIN_OOB);
+    };
+    // NAT: the record is in before the loop (an older load still in flight at the loop leaves the
+    // compiler's wait counting with a vmcnt(0) at every stage write)
+    if constexpr (NATM) asm volatile("" ::"v"(rw.x), "v"(rw.y));
+    if (!ETH || lo != lo0) load_step(0u, v);             // MODE 3: the span starts elsewhere
+    STAMP(1);
+    // one step: cur is staged and summed while nxt's loads (step st + 1) are in flight
+    auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
+        const uint32_t qb = st * SQ;
+        load_step(qb + SQ, nxt);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
+        __builtin_amdgcn_wave_barrier();
+        // lane-major: lane L's SCPL chunks, chunk prefixes, one wave scan of the lane totals
+        uint32_t loc[SCPL];
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; ++k) {
+            loc[k] = t;
+            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
+        }
+        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
+        const uint32_t exs = base + incs - t;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; k += 4)
+            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
+                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
+        __builtin_amdgcn_wave_barrier();
+        // frame j's head window chunks that are in this step
+#pragma unroll
+        for (uint32_t i = 0; i < HS; ++i) {
+            const uint32_t qi = hq + i - qb;
+            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
+        }
+        // once chunks 0 and 1 are in: the boundaries (clamped into the frame; a frame that
+        // fails the header checks below never reads them)
+        if (ETH && !pre6 && hq + 1u < qb + SQ) {
+            // the ethertype: an IPv6 frame's addresses, transport start (neither taken yet: both
+            // lie past chunk 1); anything else needs no parse in the loop
+            pre6 = true;
+            uint32_t T[1];
+            window_words<1, true>(hw, r + 12u, T);
+            if ((T[0] & 0xFFFFu) == 0xDD86u) {
+                b0 = rel + 22u;
+                b1 = rel + min(54u, len);
+                x0 = x1 = 0u;
+            } else {
+                pre = true;
+            }
+        }
+        if (ETH && !pre && hq + 2u < qb + SQ) {
+            // MODE 3: an IPv6 frame -- its transport end and field, by prefixes (past the head chunks)
+            {
+                pre = true;
+                uint32_t H[3];
+                window_words<3, true>(hw, r + 14u, H);
+                const uint32_t ilen = len - 14u;
+                const uint32_t plen = ((H[1] & 0xFFu) << 8) | ((H[1] >> 8) & 0xFFu);
+                const uint32_t nh = (H[1] >> 16) & 0xFFu, b9 = (H[2] >> 8) & 0xFFu;
+                if (ilen >= 40u) {
+                    // (b0, b1 since the ethertype)
+                    b2 = rel + 14u + min(40u + plen, ilen);
+                    const uint32_t xo = eth6_field(tx, nh, b9, (p.flags & F_NXD) != 0u);
+                    if (xo != NONE && 40u + xo < ilen) {
+                        x0 = rel + 54u + xo;
+                        x1 = x0 + min(2u, ilen - 40u - xo);
+                    }
+                }
+            }
+        }
+        const uint32_t byte0 = 16u * qb;
+        stream_point(S, b1, byte0, P1);
+        stream_point(S, b2, byte0, P2);
+        // the optional points, each cleared once taken (the group is skipped once none is left)
+        if ((ETH || V6) && __builtin_amdgcn_ballot_w64((b0 | x0 | x1) != 0u)) {
+            b0 = stream_point(S, b0, byte0, P0) ? 0u : b0;
+            x0 = stream_point(S, x0, byte0, P3) ? 0u : x0;
+            x1 = stream_point(S, x1, byte0, P4) ? 0u : x1;
+        }
+        base += tot;
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();               // every stage read before the next is written
+    };
+    if constexpr (!ETH) {
+        // two steps a trip, the register sets swapping roles: each step's wait covers only its own
+        // loads (a copy of the next set into this one at the end of a trip would wait on them too,
+        // leaving one step in flight across the wait)
+        for (uint32_t st = 0; st < nsteps; st += 2) {
+            step(st, v, vn);
+            if (st + 1u >= nsteps) break;
+            step(st + 1u, vn, v);
+        }
+    } else {
+        // MODE 3 (both families' parse in the loop): one step a trip, the sets copied -- the
+        // two-step trip spills there
+        for (uint32_t st = 0; st < nsteps; ++st) {
+            step(st, v, vn);
+#pragma unroll
+            for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
+        }
+    }
+
+    STAMP(2);
+    return stream_finish<NATM, V6, ETH>(p, S, lane, f0, cnt, tx, rw, valid, oob, len, seeded, rel, lo, hw, P0, P1,
+                                        P2, P3, P4);
+}
+
 // One wave per batch of up to 64 frames.  (A persistent grid looping over batches
 // measured slower: every wave repeats the same serial descriptor -> rounds chain.)
 // The product shape (measured): 8 chunks per lane per round, the 1-lane class for
@@ -1399,6 +1416,294 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
     }
     STAMP(3);
 }
+
+#if SORTED_MODE == 1
+// ---------------------------------------------------------------- persistent stream waves (MODE 1)
+//
+// csum_sorted_kernel runs one wave per group of fpw datagrams: at 256K datagrams that is one
+// residency round of 4096 waves, every wave in the same phase at once -- descriptor round trips
+// while HBM idles at the start, a tail of late or heavy waves at the end (per-wave
+// stamps: setup 3.1 us median, streaming 6.7-14.3 us p1-p99, the median wave done 4-5 us before
+// the launch).  Here a fixed grid of waves (WPS per SIMD) streams groups back to back without a
+// gap: group k's last step is processed with group k+1's first step already in flight, and k's
+// finish (verdicts, stores) runs while it lands.  Descriptors run two groups ahead and the group
+// indices come from a claim counter (the first group of wave w is w, then P + claims in claim
+// order), each claim read a group after it went out -- so no wait in the stream covers anything
+// but the step it needs.  Claims balance the waves: the launch ends within about one group of
+// its last byte.  Every step issues exactly SCPL loads (an absent step reads zeros through an empty
+// window), so the compiler's in-order waits stay vmcnt(SCPL) across group boundaries.  A group the
+// stream does not take (not back to back) or does not finish (options, a field or trailing bytes
+// past the head window) is summed by the sorted rounds in the same wave, at the step that finds it.
+// The claim counter lives in a slot of g_pstream_ctl, one slot per launch (a ring the launcher
+// walks); the last wave out resets it, so a captured graph replays with the slot clean.
+struct PStreamCtl {
+    uint32_t head;         // claims handed out
+    uint32_t done;         // waves that left
+    uint32_t pad[14];
+};
+constexpr uint32_t NPCTL = 4096;
+__device__ PStreamCtl g_pstream_ctl[NPCTL];
+
+struct PSpan {
+    Window w;
+    uint64_t lo;
+    uint32_t nsteps;       // 0: not streamed
+};
+
+// A group's span, as stream_batch's setup (MODE 1): the first valid datagram's line to the last
+// one's end, when every datagram lies inside and the span holds at most 2 x their bytes + 4 KiB.
+__device__ __forceinline__ PSpan pstream_span(const FlatArgs& p, uint32_t lane, uint32_t g, uint4 d) {
+    PSpan s;
+    s.w = make_window(0ull, 0u);
+    s.lo = 0;
+    s.nsteps = 0;
+    if (g == NONE) return s;
+    const uint64_t f0 = (uint64_t)g * p.fpw;
+    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+    uint64_t off0 = ((uint64_t)d.y << 32) | d.x;
+    uint32_t len = lane < cnt ? d.z : 0u;
+    const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
+    if (oob || lane >= cnt) { len = 0; off0 = 0; }
+    const bool valid = len >= 20u;
+    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
+    const uint64_t la = addr & ~(uint64_t)15;
+    const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
+    if (!vb || __builtin_amdgcn_ballot_w64(valid && len > (1u << 20))) return s;
+    const int fv = __builtin_ffsll((long long)vb) - 1;
+    const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
+    const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
+    if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return s;
+    int mn = 0, mx = __builtin_amdgcn_readlane((int)dh, 63 - __builtin_clzll(vb));
+    if (__builtin_amdgcn_ballot_w64(valid && (dl < 0 || dh > (int64_t)mx))) {
+        mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
+        mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
+    }
+    const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)(valid ? len : 0u)), 63);
+    const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
+    if (!((uint64_t)ext <= 2ull * rs + 4096u)) return s;
+    s.lo = uniform64(anchor + (int64_t)mn);
+    s.w = make_window(s.lo, ext);
+    s.nsteps = ((ext >> 4) + SQ - 1u) / SQ;
+    return s;
+}
+
+constexpr uint32_t PFBQ = 64;                // a wave's list of groups for the sorted rounds
+constexpr uint32_t PFB_STOP = PFBQ - 8;       // no new claims once the list holds this many
+
+// The sorted rounds for the groups on a wave's list, as a call where nothing of the stream is live
+// (inlined into the pass loop it left the compiler unable to prove the stream's windows uniform: a
+// waterfall loop around every load; the arguments as values: a reference to the kernel's FlatArgs
+// would put it in scratch and every use of a field in the stream would wait on a scratch load)
+__device__ __attribute__((noinline)) void pstream_drain(uint8_t* base, uint64_t base_len, const pico_csum_desc_dev* desc,
+                                                       uint32_t n, uint32_t fpw, uint32_t flags, uint16_t* out_net,
+                                                       uint16_t* out_l4, uint8_t* verdict, SortedWaveSmem<true>& SM,
+                                                       const uint32_t* fbq, uint32_t nfb, uint32_t lane) {
+    const FlatArgs q{base, base_len, desc, n, fpw, -1, flags, nullptr, nullptr, out_net, out_l4, verdict, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < nfb; ++i)
+        sorted_batch<1, true, 8, true>(q, SM.s, SM.stage, lane,
+                                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)fbq[i]) * fpw);
+}
+
+template <int WPS>
+__global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p) {
+    __shared__ SortedWaveSmem<true> lds_all[WPB];
+    __shared__ uint32_t fbq_all[WPB][PFBQ];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    SortedWaveSmem<true>& SM = lds_all[wv];
+    StreamLds& S = SM.st;
+    uint32_t* const fbq = fbq_all[wv];
+    PStreamCtl* const ctl = g_pstream_ctl + p.ctl_slot;
+    const bool tx = (p.flags & 2u) != 0;
+    const uint32_t P = gridDim.x * WPB;
+    const uint64_t ng = ((uint64_t)p.n + p.fpw - 1u) / p.fpw;
+    constexpr uint32_t HS = 4u;
+    constexpr uint32_t EMPTY = NONE - 1u;               // the empty group a pass starts on
+    // group gi's descriptors (lane j: datagram j; absent lanes and groups read zeros)
+    auto load_desc = [&](uint32_t gi) __attribute__((always_inline)) -> uint4 {
+        const uint64_t f = gi == NONE ? 0ull : (uint64_t)gi * p.fpw;
+        const uint32_t c = gi == NONE ? 0u : (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f);
+        const Window dw = make_window(reinterpret_cast<uintptr_t>(p.desc + f), 16u * c);
+        return load_win<false>(dw, 16u * lane);
+    };
+    // claims: group P + k for the k-th claim (the first P groups go one per wave); `more` turns
+    // false once a claim comes back past the batch, `claiming` = a claim is in flight
+    uint32_t kc = 0;                                    // lane 0: the claim in flight
+    bool claiming = false, more = true;
+    uint32_t nfb = 0;                                   // groups in fbq
+    auto issue_claim = [&]() __attribute__((always_inline)) {
+        if (lane == 0) kc = __hip_atomic_fetch_add(&ctl->head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // the claim in flight -> a group (or NONE), and the next claim unless the batch is done or the
+    // list is near full (the pass then runs dry and the sorted rounds empty the list)
+    auto next_group = [&]() __attribute__((always_inline)) -> uint32_t {
+        if (!claiming) return NONE;
+        const uint64_t gi = (uint64_t)P + (uint32_t)__builtin_amdgcn_readfirstlane((int)kc);
+        const uint32_t r = gi < ng ? (uint32_t)gi : NONE;
+        more = r != NONE;
+        claiming = more && nfb < PFB_STOP;
+        if (claiming) issue_claim();
+        return r;
+    };
+    auto push_fb = [&](uint32_t gi) __attribute__((always_inline)) {
+        if (lane == 0) fbq[nfb] = gi;
+        ++nfb;
+    };
+    // (readfirstlane: the compiler cannot tell that threadIdx.x >> 6 is uniform in a wave -- a divergent
+    // group index makes every window a waterfall loop)
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WPB + wv));
+    // the pipeline: g (streaming), g1 (next: descriptors d1 in), g2 (after it: d2 in flight), and the
+    // claim for the one after g2.  A pass starts on an empty group (one step of zeros) whose
+    // boundary sets up the first real group.
+    uint32_t g = EMPTY, g1 = NONE, g2 = NONE;
+    uint4 d = make_uint4(0, 0, 0, 0), d1 = d, d2 = d;
+    PSpan sp, spn;
+    uint32_t cnt = 0, len = 0, rel = 0, hq = 0, nlh = 0, b1 = 0, b2 = 0, P1 = 0, P2 = 0, base = 0, st = 0;
+    bool valid = false, oob = false, live = true;
+    uint4 hw[HW];
+#pragma unroll
+    for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
+    auto setup_lanes = [&]() __attribute__((always_inline)) {
+        const uint64_t f0 = (uint64_t)g * p.fpw;
+        cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
+        uint64_t off0 = ((uint64_t)d.y << 32) | d.x;
+        len = lane < cnt ? d.z : 0u;
+        oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
+        if (oob || lane >= cnt) { len = 0; off0 = 0; }
+        valid = len >= 20u;
+        const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
+        rel = valid ? (uint32_t)(addr - sp.lo) : 0u;
+        hq = rel >> 4;
+        nlh = valid ? min(HS, ((rel & 15u) + len + 15u) >> 4) : 0u;
+        b1 = valid ? rel + min(20u, len) : 0u;
+        b2 = valid ? rel + len : 0u;
+        P1 = P2 = base = 0u;
+        st = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
+    };
+    auto load_step = [&](const Window& win, uint32_t qs, uint4 (&dst)[SCPL]) __attribute__((always_inline)) {
+        // the step starting at chunk qs (offsets past the window's end read zeros)
+        const uint32_t o = 16u * (qs + lane);
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(win, o + 1024u * c);
+    };
+    uint4 v[SCPL], vn[SCPL];
+    auto step = [&](uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) __attribute__((always_inline)) {
+        const bool last = st + 1u == sp.nsteps;
+        if (last) {
+            // the boundary: the claim read (g2) and the next claim, g2's descriptors, g1's span and
+            // its first step -- all but the last issued before this step's loads, so free to wait on
+            g2 = next_group();
+            d2 = load_desc(g2);
+            spn = pstream_span(p, lane, g1, d1);
+            load_step(spn.w, 0u, nxt);
+        } else {
+            load_step(sp.w, (st + 1u) * SQ, nxt);
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t loc[SCPL];
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; ++k) {
+            loc[k] = t;
+            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
+        }
+        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
+        const uint32_t exs = base + incs - t;
+#pragma unroll
+        for (uint32_t k = 0; k < SCPL; k += 4)
+            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
+                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t qb = st * SQ;
+#pragma unroll
+        for (uint32_t i = 0; i < HS; ++i) {
+            const uint32_t qi = hq + i - qb;
+            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
+        }
+        const uint32_t byte0 = 16u * qb;
+        stream_point(S, b1, byte0, P1);
+        stream_point(S, b2, byte0, P2);
+        base += tot;
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (!last) {
+            ++st;
+            return;
+        }
+        // group g's finish (the empty group has none) while g1's first step is in flight; a group it
+        // does not finish goes on the list for the sorted rounds
+        if (g != EMPTY &&
+            !stream_finish<false, false, false>(p, S, lane, (uint64_t)g * p.fpw, cnt, tx, make_uint2(0u, 0u),
+                                                valid, oob, len, false, rel, sp.lo, hw, 0u, P1, P2, 0u, 0u))
+            push_fb(g);
+        __builtin_amdgcn_wave_barrier();
+        g = g1;
+        d = d1;
+        sp = spn;
+        g1 = g2;
+        d1 = d2;
+        // a group that is not streamed goes on the list, and the one after it is set up here (its
+        // first step loaded again)
+        while (g != NONE && sp.nsteps == 0u) {
+            push_fb(g);
+            g = g1;
+            d = d1;
+            g1 = next_group();
+            d1 = load_desc(g1);
+            sp = pstream_span(p, lane, g, d);
+            load_step(sp.w, 0u, nxt);
+        }
+        live = g != NONE;
+        if (live) setup_lanes();
+    };
+    // passes: stream until the batch is done or the list is near full, then the sorted rounds for
+    // the list (nothing of the stream live across them), then the next pass from a fresh claim
+    for (bool first = true;; first = false) {
+        if (first) {
+            g1 = w < ng ? w : NONE;
+            more = g1 != NONE && (uint64_t)P < ng;
+            claiming = more;
+            if (claiming) issue_claim();
+        } else {
+            if (!more) break;
+            claiming = true;
+            issue_claim();
+            g1 = next_group();
+        }
+        d1 = load_desc(g1);
+        g = EMPTY;
+        sp.w = make_window(0ull, 0u);
+        sp.lo = 0;
+        sp.nsteps = 1;
+        st = 0;
+        live = true;
+        load_step(sp.w, 0u, v);                         // the empty group's step: zeros
+        for (;;) {
+            step(v, vn);
+            if (!live) break;
+            step(vn, v);
+            if (!live) break;
+        }
+        if (nfb) pstream_drain(p.base, p.base_len, p.desc, p.n, p.fpw, p.flags, p.out_net, p.out_l4, p.verdict, SM, fbq,
+                               nfb, lane);
+        nfb = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (!more) break;
+    }
+    // every claim this wave issued has been read: the last wave out resets the slot
+    if (lane == 0 &&
+        __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1u) {
+        __hip_atomic_store(&ctl->head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+#endif  // SORTED_MODE == 1
 
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- uniform rings: stream waves
@@ -1904,7 +2209,34 @@ int SORTED_LAUNCH(const void* args, void* stream) {
     return (int)hipGetLastError();
 }
 
+#if SORTED_MODE == 1
+// Persistent stream waves (IPv4 RX / TX, no NAT): wps waves per SIMD on cus compute units.
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream);
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream) {
+    static std::atomic<uint32_t> slot{0};
+    FlatArgs a = *static_cast<const FlatArgs*>(args);
+    if ((a.flags & F_NAT) || (wps != 1 && wps != 2) || cus == 0) return (int)hipErrorInvalidValue;
+    a.ctl_slot = slot.fetch_add(1u, std::memory_order_relaxed) % NPCTL;
+    auto kern = wps == 1 ? csum_pstream_kernel<1> : csum_pstream_kernel<2>;
+    hipLaunchKernelGGL(kern, dim3(cus * wps), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
+    return (int)hipGetLastError();
+}
+#endif
+
 #if SORTED_MODE == 0
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream);
+
+// Persistent stream waves over an IPv4 descriptor batch (mode 1 only for now): fpw datagrams a group.
+int pico_csum_launch_pstream(void* base, uint64_t base_len, const void* desc, uint32_t n, uint32_t flags,
+                             uint16_t* out_net, uint16_t* out_l4, uint8_t* verdict, uint32_t fpw, uint32_t wps,
+                             uint32_t cus, void* stream) {
+    if (fpw < 1 || fpw > 64 || n >= 0x80000000u) return (int)hipErrorInvalidValue;
+    if (n == 0) return (int)hipSuccess;
+    FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
+               -1, flags, nullptr, nullptr, out_net, out_l4, verdict, 0u, 0u, 0u};
+    return pico_csum_pstream_launch_mode1(&a, wps, cus, stream);
+}
+
 int pico_csum_sorted_launch_mode1(const void* args, void* stream);
 int pico_csum_sorted_launch_mode2(const void* args, void* stream);
 int pico_csum_sorted_launch_mode3(const void* args, void* stream);
