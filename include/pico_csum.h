@@ -424,8 +424,8 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
 
 /* Tuning knob (tests / bench sweeps), per calling thread: the persistent stream waves for IPv4
- * descriptor batches (pico_ipv4_checksum_batch_dev / _host without NAT) -- mode 0 = automatic, 1 = on,
- * PICO_CSUM_STREAM_OFF = one wave per group of datagrams; waves_per_simd 1 or 2 (0 = automatic),
+ * descriptor batches (pico_ipv4_checksum_batch_dev / _host without NAT) -- mode 0 = automatic, 1 = on
+ * with claimed groups, 2 = on in static group order, PICO_CSUM_STREAM_OFF = one wave per group of datagrams; waves_per_simd 1 or 2 (0 = automatic),
  * frames_per_group 1..64 (0 = automatic).  Results never depend on it. */
 int pico_csum_set_desc_stream(uint32_t mode, uint32_t waves_per_simd, uint32_t frames_per_group);
 

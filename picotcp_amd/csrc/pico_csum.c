@@ -40,7 +40,7 @@ int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t 
                                     uint16_t *out, uint32_t fpw, void *stream);
 int pico_csum_launch_pstream(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
                              uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t fpw, uint32_t wps,
-                             uint32_t cus, void *stream);
+                             uint32_t cus, int dyn, void *stream);
 int pico_csum_launch_uniform_chunks(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t cf, uint32_t waves, int dyn, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
@@ -154,8 +154,9 @@ static __thread uint32_t g_ovr_pmode, g_ovr_pwps, g_ovr_pfpg;   /* persistent de
 
 int pico_csum_set_desc_stream(uint32_t mode, uint32_t waves_per_simd, uint32_t frames_per_group)
 {
-    if (!(mode <= 1 || mode == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "descriptor stream mode must be 0 (auto), 1 (on) or PICO_CSUM_STREAM_OFF");
+    if (!(mode <= 2 || mode == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "descriptor stream mode must be 0 (auto), 1 (claimed groups), 2 (static "
+                                        "order) or PICO_CSUM_STREAM_OFF");
     if (waves_per_simd > 2)
         return fail(PICO_CSUM_EINVAL, "waves per SIMD must be 1 or 2 (0 = auto)");
     if (frames_per_group > 64)
@@ -431,12 +432,12 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    if (g_ovr_pmode == 1 && g_ovr_group != 2 && n < 0x80000000u) {
+    if ((g_ovr_pmode == 1 || g_ovr_pmode == 2) && g_ovr_group != 2 && n < 0x80000000u) {
         /* the persistent stream waves (pico_csum_k_sorted.hip csum_pstream_kernel): a fixed grid
          * streaming claimed groups back to back */
         const uint32_t wps = g_ovr_pwps ? g_ovr_pwps : 1u, fpg = g_ovr_pfpg ? g_ovr_pfpg : 64u;
         return launch_status(pico_csum_launch_pstream(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
-                                                      d_verdict, fpg, wps, cur_cus(), stream),
+                                                      d_verdict, fpg, wps, cur_cus(), g_ovr_pmode == 1, stream),
                              "pico_ipv4_checksum_batch_dev");
     }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,

@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p)
     SortedWaveSmem<true>& SM = lds_all[wv];
     StreamLds& S = SM.st;
     uint32_t* const fbq = fbq_all[wv];
-    PStreamCtl* const ctl = g_pstream_ctl + p.ctl_slot;
+    PStreamCtl* const ctl = g_pstream_ctl + (p.ctl_slot < NPCTL ? p.ctl_slot : 0u);
     const bool tx = (p.flags & 2u) != 0;
     const uint32_t P = gridDim.x * WPB;
     const uint64_t ng = ((uint64_t)p.n + p.fpw - 1u) / p.fpw;
@@ -1526,13 +1526,20 @@ __global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p)
         const Window dw = make_window(reinterpret_cast<uintptr_t>(p.desc + f), 16u * c);
         return load_win<false>(dw, 16u * lane);
     };
+    // (readfirstlane: the compiler cannot tell that threadIdx.x >> 6 is uniform in a wave -- a divergent
+    // group index makes every window a waterfall loop)
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WPB + wv));
     // claims: group P + k for the k-th claim (the first P groups go one per wave); `more` turns
     // false once a claim comes back past the batch, `claiming` = a claim is in flight
+    // (static order, ctl_slot == NPCTL: the k-th "claim" of wave w is group w + (k + 1) P, no atomics)
     uint32_t kc = 0;                                    // lane 0: the claim in flight
     bool claiming = false, more = true;
     uint32_t nfb = 0;                                   // groups in fbq
+    const bool dyn = p.ctl_slot < NPCTL;
+    uint32_t nclaims = 0;
     auto issue_claim = [&]() __attribute__((always_inline)) {
-        if (lane == 0) kc = __hip_atomic_fetch_add(&ctl->head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!dyn) kc = w + P * nclaims++;
+        else if (lane == 0) kc = __hip_atomic_fetch_add(&ctl->head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // the claim in flight -> a group (or NONE), and the next claim unless the batch is done or the
     // list is near full (the pass then runs dry and the sorted rounds empty the list)
@@ -1549,9 +1556,6 @@ __global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p)
         if (lane == 0) fbq[nfb] = gi;
         ++nfb;
     };
-    // (readfirstlane: the compiler cannot tell that threadIdx.x >> 6 is uniform in a wave -- a divergent
-    // group index makes every window a waterfall loop)
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WPB + wv));
     // the pipeline: g (streaming), g1 (next: descriptors d1 in), g2 (after it: d2 in flight), and the
     // claim for the one after g2.  A pass starts on an empty group (one step of zeros) whose
     // boundary sets up the first real group.
@@ -1697,7 +1701,7 @@ __global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p)
         if (!more) break;
     }
     // every claim this wave issued has been read: the last wave out resets the slot
-    if (lane == 0 &&
+    if (dyn && lane == 0 &&
         __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1u) {
         __hip_atomic_store(&ctl->head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2210,13 +2214,14 @@ int SORTED_LAUNCH(const void* args, void* stream) {
 }
 
 #if SORTED_MODE == 1
-// Persistent stream waves (IPv4 RX / TX, no NAT): wps waves per SIMD on cus compute units.
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream);
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream) {
+// Persistent stream waves (IPv4 RX / TX, no NAT): wps waves per SIMD on cus compute units; dyn: claimed
+// groups, else static order.
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream);
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream) {
     static std::atomic<uint32_t> slot{0};
     FlatArgs a = *static_cast<const FlatArgs*>(args);
     if ((a.flags & F_NAT) || (wps != 1 && wps != 2) || cus == 0) return (int)hipErrorInvalidValue;
-    a.ctl_slot = slot.fetch_add(1u, std::memory_order_relaxed) % NPCTL;
+    a.ctl_slot = dyn ? slot.fetch_add(1u, std::memory_order_relaxed) % NPCTL : NPCTL;
     auto kern = wps == 1 ? csum_pstream_kernel<1> : csum_pstream_kernel<2>;
     hipLaunchKernelGGL(kern, dim3(cus * wps), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
@@ -2224,17 +2229,17 @@ int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus,
 #endif
 
 #if SORTED_MODE == 0
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, void* stream);
+int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream);
 
 // Persistent stream waves over an IPv4 descriptor batch (mode 1 only for now): fpw datagrams a group.
 int pico_csum_launch_pstream(void* base, uint64_t base_len, const void* desc, uint32_t n, uint32_t flags,
                              uint16_t* out_net, uint16_t* out_l4, uint8_t* verdict, uint32_t fpw, uint32_t wps,
-                             uint32_t cus, void* stream) {
+                             uint32_t cus, int dyn, void* stream) {
     if (fpw < 1 || fpw > 64 || n >= 0x80000000u) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
                -1, flags, nullptr, nullptr, out_net, out_l4, verdict, 0u, 0u, 0u};
-    return pico_csum_pstream_launch_mode1(&a, wps, cus, stream);
+    return pico_csum_pstream_launch_mode1(&a, wps, cus, dyn, stream);
 }
 
 int pico_csum_sorted_launch_mode1(const void* args, void* stream);

@@ -41,11 +41,12 @@ def check_ipv4(buf, desc_h, flags=0, d_buf=None):
     return d_buf
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("wps,fpg", SHAPES)
-def test_golden_fixture(wps, fpg):
+def test_golden_fixture(wps, fpg, mode):
     """The IPv4 fixture (valid, corrupted, fragments, evil bit, IHL < 5, bad sources, options,
-    truncations), RX and TX, against its expectations."""
-    batch.set_desc_stream(1, wps, fpg)
+    truncations), RX and TX, against its expectations; claimed groups and static order."""
+    batch.set_desc_stream(mode, wps, fpg)
     cs = G.ipv4_cases()
     desc = batch.desc_to_device(G.ipv4_desc(cs["net"], cs["avail"]), DEV)
     n = cs["net"].size
@@ -56,10 +57,11 @@ def test_golden_fixture(wps, fpg):
         np.testing.assert_array_equal(u16(l4), cs[f"{key}_l4"], err_msg=key)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("wps,fpg", SHAPES)
-def test_c2_imix_rx_with_corruption(wps, fpg):
+def test_c2_imix_rx_with_corruption(wps, fpg, mode):
     """C2's layout (IMIX behind 14-byte gaps), 64K datagrams, 1/37 corrupted."""
-    batch.set_desc_stream(1, wps, fpg)
+    batch.set_desc_stream(mode, wps, fpg)
     lens = synth.imix_lengths(65536, 31 + fpg)
     buf, net_off, avail = synth.ipv4_batch(lens, seed=12 + wps, proto=6, eth=True)
     desc_h = G.ipv4_desc(net_off, avail)
@@ -92,13 +94,13 @@ def test_dense_tails_and_options(wps, fpg):
     check_ipv4(buf, desc_h)
 
 
-@pytest.mark.parametrize("wps,fpg", [(1, 2), (2, 2), (1, 64)])
-def test_every_group_falls_back(wps, fpg):
+@pytest.mark.parametrize("wps,fpg,mode", [(1, 2, 1), (2, 2, 1), (1, 64, 1), (1, 2, 2)])
+def test_every_group_falls_back(wps, fpg, mode):
     """No group is back to back: descriptors alternate between two copies of a datagram pool 4 MiB
     apart.  Every group goes on its wave's list; with 2-datagram groups a wave holds ~150 of them,
     so its list fills, the pass runs dry, the sorted rounds empty the list and the next pass starts
     from a fresh claim -- several passes a wave."""
-    batch.set_desc_stream(1, wps, fpg)
+    batch.set_desc_stream(mode, wps, fpg)
     lens = synth.imix_lengths(512, 3)
     pool, net_off, avail = synth.ipv4_batch(lens, seed=4, proto=6, eth=True)
     far = 4 << 20
@@ -144,7 +146,16 @@ def test_out_of_bounds_and_short():
     desc_h["len"][5::97] = 11
     desc_h["len"][9::211] = 0
     desc_h["off"][3::301] = np.uint64(1 << 40)
-    check_ipv4(buf, desc_h)
+    n = desc_h.size
+    net, l4, v = batch.ipv4_checksum_batch(to_dev(buf), batch.desc_to_device(desc_h, DEV), n)
+    # the oracle has no bound: past base_len is MALFORMED with zero outputs, as a zero-length one
+    ref = desc_h.copy()
+    ref["len"][3::301] = 0
+    wn, wl, wv = O.batch_ipv4(buf, ref)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    np.testing.assert_array_equal(u16(net), wn)
+    np.testing.assert_array_equal(u16(l4), wl)
+    assert (wv[3::301] == 8).all()
 
 
 def test_repeated_launches_and_graph():
