@@ -132,9 +132,6 @@ def parse():
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
     p.add_argument("--stream", default="", help="MODE,FPW the uniform rings' stream waves "
                                                   "(pico_csum_set_uniform_stream: 1 on, 255 off; frames per wave)")
-    p.add_argument("--pstream", default="", help="MODE,WPS,FPG the persistent stream waves for IPv4 batches "
-                                                   "(pico_csum_set_desc_stream: 1 on, 255 off; waves per SIMD; "
-                                                   "datagrams per group)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch the K timed steps one by one from Python instead of replaying them as one "
                         "captured HIP graph")
@@ -685,8 +682,6 @@ def main():
         batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
     if a.stream:
         batch.set_uniform_stream(*[int(x) for x in a.stream.split(",")])
-    if a.pstream:
-        batch.set_desc_stream(*[int(x) for x in a.pstream.split(",")])
     cfg = CONFIGS[a.config]
 
     # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)

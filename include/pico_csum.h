@@ -416,18 +416,11 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
                                   uint32_t pipeline);
 
 /* Tuning knob (tests / bench sweeps), per calling thread: the uniform rings' stream waves
- * (pico_checksum_batch_uniform_dev / _host on densely packed frames) -- mode 0 = automatic, 1 = one
- * range per wave wherever the ring allows it, 2 = one wave per SIMD over claimed chunks of
- * frames_per_wave frames, 3 = the same chunks in static order, PICO_CSUM_STREAM_OFF = the lane-group
- * kernels; frames_per_wave 0 = automatic.  Results never depend on it. */
+ * (pico_checksum_batch_uniform_dev / _host on densely packed frames) -- mode 0 = automatic, 1 = on
+ * wherever the ring allows them, PICO_CSUM_STREAM_OFF = the lane-group kernels; frames_per_wave
+ * 0 = automatic.  Results never depend on it. */
 #define PICO_CSUM_STREAM_OFF 0xFFu
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
-
-/* Tuning knob (tests / bench sweeps), per calling thread: the persistent stream waves for IPv4
- * descriptor batches (pico_ipv4_checksum_batch_dev / _host without NAT) -- mode 0 = automatic, 1 = on
- * with claimed groups, 2 = on in static group order, PICO_CSUM_STREAM_OFF = one wave per group of datagrams; waves_per_simd 1 or 2 (0 = automatic),
- * frames_per_group 1..64 (0 = automatic).  Results never depend on it. */
-int pico_csum_set_desc_stream(uint32_t mode, uint32_t waves_per_simd, uint32_t frames_per_group);
 
 #ifdef __cplusplus
 }

@@ -331,14 +331,6 @@ def set_uniform_stream(mode: int = 0, frames_per_wave: int = 0) -> None:
     _lib.check("pico_csum_set_uniform_stream", _lib.load().pico_csum_set_uniform_stream(mode, frames_per_wave))
 
 
-def set_desc_stream(mode: int = 0, waves_per_simd: int = 0, frames_per_group: int = 0) -> None:
-    """Persistent stream waves for IPv4 descriptor batches (tests / bench sweeps, this thread): mode 0
-    automatic, 1 on, STREAM_OFF one wave per group; waves per SIMD (1, 2; 0 = automatic), datagrams per
-    group (0 = automatic).  Results never depend on it (include/pico_csum.h)."""
-    _lib.check("pico_csum_set_desc_stream", _lib.load().pico_csum_set_desc_stream(mode, waves_per_simd,
-                                                                                  frames_per_group))
-
-
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps): group 0 = automatic; 2 = descriptor

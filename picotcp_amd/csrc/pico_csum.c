@@ -38,11 +38,6 @@ int pico_csum_launch_sorted(void *base, uint64_t base_len, const void *desc, uin
                             uint8_t *verdict, uint32_t fpw, uint64_t mac48, void *stream);
 int pico_csum_launch_uniform_stream(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
                                     uint16_t *out, uint32_t fpw, void *stream);
-int pico_csum_launch_pstream(void *base, uint64_t base_len, const void *desc, uint32_t n, uint32_t flags,
-                             uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict, uint32_t fpw, uint32_t wps,
-                             uint32_t cus, int dyn, void *stream);
-int pico_csum_launch_uniform_chunks(const void *base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
-                                    uint16_t *out, uint32_t cf, uint32_t waves, int dyn, void *stream);
 int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *desc, uint32_t n, const uint32_t *local,
                                   uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
@@ -150,28 +145,11 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
  * launch from another thread). */
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 = automatic */
-static __thread uint32_t g_ovr_pmode, g_ovr_pwps, g_ovr_pfpg;   /* persistent descriptor stream */
-
-int pico_csum_set_desc_stream(uint32_t mode, uint32_t waves_per_simd, uint32_t frames_per_group)
-{
-    if (!(mode <= 2 || mode == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "descriptor stream mode must be 0 (auto), 1 (claimed groups), 2 (static "
-                                        "order) or PICO_CSUM_STREAM_OFF");
-    if (waves_per_simd > 2)
-        return fail(PICO_CSUM_EINVAL, "waves per SIMD must be 1 or 2 (0 = auto)");
-    if (frames_per_group > 64)
-        return fail(PICO_CSUM_EINVAL, "frames per group in [1, 64] (0 = auto)");
-    g_ovr_pmode = mode;
-    g_ovr_pwps = waves_per_simd;
-    g_ovr_pfpg = frames_per_group;
-    return 0;
-}
 
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave)
 {
-    if (!(mode <= 3 || mode == PICO_CSUM_STREAM_OFF))
-        return fail(PICO_CSUM_EINVAL, "uniform stream mode must be 0 (auto), 1 (ranges), 2 (claimed chunks), "
-                                        "3 (chunks, static order) or PICO_CSUM_STREAM_OFF");
+    if (!(mode <= 1 || mode == PICO_CSUM_STREAM_OFF))
+        return fail(PICO_CSUM_EINVAL, "uniform stream mode must be 0 (auto), 1 (on) or PICO_CSUM_STREAM_OFF");
     if (frames_per_wave > 65536)
         return fail(PICO_CSUM_EINVAL, "frames per wave in [1, 65536] (0 = auto)");
     g_ovr_smode = mode;
@@ -384,16 +362,6 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return rc;
     if (g_ovr_group == 2)
         return fail(PICO_CSUM_EINVAL, "launch override group 2 is for descriptor batches");
-    if (uniform_stream_ok(d_base, stride, len, n, seed) && (g_ovr_smode == 2 || g_ovr_smode == 3)) {
-        /* one wave per SIMD over chunks of cf frames, about 4 chunks per wave at least */
-        const uint32_t waves = 4u * cur_cus();
-        uint32_t cf = g_ovr_sfpw ? g_ovr_sfpw : (uint32_t)(((uint64_t)n + 4u * waves - 1u) / (4u * waves));
-        cf = cf < 1u ? 1u : cf > 64u ? 64u : cf;
-        if ((uint64_t)(cf - 1u) * stride + len + 32u < (1ull << 31))
-            return launch_status(pico_csum_launch_uniform_chunks(d_base, stride, len, n, seed, d_out, cf, waves,
-                                                                 g_ovr_smode == 2, stream),
-                                 "pico_checksum_batch_uniform_dev");
-    }
     if (uniform_stream_ok(d_base, stride, len, n, seed) &&
         (g_ovr_smode == 1 || (g_ovr_smode == 0 && (uint64_t)n * stride >= UNIFORM_STREAM_MIN_BYTES))) {
         /* frames per wave: one wave per SIMD over the whole batch (C3: 256 frames of 9000 B, C4: 4096
@@ -432,14 +400,6 @@ int pico_ipv4_checksum_batch_dev(void *d_base, uint64_t base_len, const struct p
         return fail(PICO_CSUM_EINVAL, "F_WRITE is a TX (F_TX) operation");
     if ((rc = need_device()) != 0 || (rc = desc_fpw(n, &fpw)) != 0)
         return rc;
-    if ((g_ovr_pmode == 1 || g_ovr_pmode == 2) && g_ovr_group != 2 && n < 0x80000000u) {
-        /* the persistent stream waves (pico_csum_k_sorted.hip csum_pstream_kernel): a fixed grid
-         * streaming claimed groups back to back */
-        const uint32_t wps = g_ovr_pwps ? g_ovr_pwps : 1u, fpg = g_ovr_pfpg ? g_ovr_pfpg : 64u;
-        return launch_status(pico_csum_launch_pstream(d_base, base_len, d_desc, n, flags, d_out_net, d_out_transport,
-                                                      d_verdict, fpg, wps, cur_cus(), g_ovr_pmode == 1, stream),
-                             "pico_ipv4_checksum_batch_dev");
-    }
     return launch_status(pico_csum_launch_sorted(d_base, base_len, d_desc, n, 1, -1, flags, NULL,
                                                  NULL, d_out_net, d_out_transport, d_verdict, fpw, 0, stream),
                          "pico_ipv4_checksum_batch_dev");

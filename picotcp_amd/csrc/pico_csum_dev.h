@@ -460,7 +460,6 @@ struct FlatArgs {
     uint8_t* verdict;
     uint32_t mac_lo;      // ETH: the device's MAC as stored (bytes 0-3, 4-5), with F_MACF
     uint32_t mac_hi;
-    uint32_t ctl_slot;    // persistent stream waves: this launch's claim-counter slot
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;

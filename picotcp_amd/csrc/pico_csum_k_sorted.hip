@@ -3,8 +3,6 @@
 // Helpers, argument structs and the arithmetic contract: pico_csum_dev.h.
 #include "pico_csum_dev.h"
 
-#include <atomic>
-
 #ifndef SORTED_MODE
 #define SORTED_MODE 0
 #endif
@@ -1184,7 +1182,6 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     if (!ETH && (p.flags & F_MACF)) return false;
     const uint32_t cnt = f0 < p.n ? (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0) : 0u;
     const bool tx = (p.flags & 2u) != 0;
-    constexpr bool natm = NATM;
     uint4 dcur = make_uint4(0, 0, 0, 0);
     if (lane < cnt) dcur = *reinterpret_cast<const uint4*>(p.desc + f0 + lane);
     // NAT: the frame's record {addr, port | dir << 16} (sorted_batch's NAT stage)
@@ -1417,297 +1414,6 @@ __global__ __launch_bounds__(64 * WPB, 16 / WPB) void csum_sorted_kernel(FlatArg
     STAMP(3);
 }
 
-#if SORTED_MODE == 1
-// ---------------------------------------------------------------- persistent stream waves (MODE 1)
-//
-// csum_sorted_kernel runs one wave per group of fpw datagrams: at 256K datagrams that is one
-// residency round of 4096 waves, every wave in the same phase at once -- descriptor round trips
-// while HBM idles at the start, a tail of late or heavy waves at the end (per-wave
-// stamps: setup 3.1 us median, streaming 6.7-14.3 us p1-p99, the median wave done 4-5 us before
-// the launch).  Here a fixed grid of waves (WPS per SIMD) streams groups back to back without a
-// gap: group k's last step is processed with group k+1's first step already in flight, and k's
-// finish (verdicts, stores) runs while it lands.  Descriptors run two groups ahead and the group
-// indices come from a claim counter (the first group of wave w is w, then P + claims in claim
-// order), each claim read a group after it went out -- so no wait in the stream covers anything
-// but the step it needs.  Claims balance the waves: the launch ends within about one group of
-// its last byte.  Every step issues exactly SCPL loads (an absent step reads zeros through an empty
-// window), so the compiler's in-order waits stay vmcnt(SCPL) across group boundaries.  A group the
-// stream does not take (not back to back) or does not finish (options, a field or trailing bytes
-// past the head window) is summed by the sorted rounds in the same wave, at the step that finds it.
-// The claim counter lives in a slot of g_pstream_ctl, one slot per launch (a ring the launcher
-// walks); the last wave out resets it, so a captured graph replays with the slot clean.
-struct PStreamCtl {
-    uint32_t head;         // claims handed out
-    uint32_t done;         // waves that left
-    uint32_t pad[14];
-};
-constexpr uint32_t NPCTL = 4096;
-__device__ PStreamCtl g_pstream_ctl[NPCTL];
-
-struct PSpan {
-    Window w;
-    uint64_t lo;
-    uint32_t nsteps;       // 0: not streamed
-};
-
-// A group's span, as stream_batch's setup (MODE 1): the first valid datagram's line to the last
-// one's end, when every datagram lies inside and the span holds at most 2 x their bytes + 4 KiB.
-__device__ __forceinline__ PSpan pstream_span(const FlatArgs& p, uint32_t lane, uint32_t g, uint4 d) {
-    PSpan s;
-    s.w = make_window(0ull, 0u);
-    s.lo = 0;
-    s.nsteps = 0;
-    if (g == NONE) return s;
-    const uint64_t f0 = (uint64_t)g * p.fpw;
-    const uint32_t cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
-    uint64_t off0 = ((uint64_t)d.y << 32) | d.x;
-    uint32_t len = lane < cnt ? d.z : 0u;
-    const bool oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
-    if (oob || lane >= cnt) { len = 0; off0 = 0; }
-    const bool valid = len >= 20u;
-    const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
-    const uint64_t la = addr & ~(uint64_t)15;
-    const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
-    if (!vb || __builtin_amdgcn_ballot_w64(valid && len > (1u << 20))) return s;
-    const int fv = __builtin_ffsll((long long)vb) - 1;
-    const uint64_t anchor = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(la >> 32), fv) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)la, fv);
-    const int64_t dl = (int64_t)(la - anchor), dh = (int64_t)(addr + len - anchor);
-    if (__builtin_amdgcn_ballot_w64(valid && (dl < -(1ll << 29) || dh > (1ll << 29)))) return s;
-    int mn = 0, mx = __builtin_amdgcn_readlane((int)dh, 63 - __builtin_clzll(vb));
-    if (__builtin_amdgcn_ballot_w64(valid && (dl < 0 || dh > (int64_t)mx))) {
-        mn = __builtin_amdgcn_readlane(wave_incl<1>(valid ? (int)dl : 0x7FFFFFFF), 63);
-        mx = __builtin_amdgcn_readlane(wave_incl<2>(valid ? (int)dh : -0x7FFFFFFF), 63);
-    }
-    const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(wave_incl<0>((int)(valid ? len : 0u)), 63);
-    const uint32_t ext = (uint32_t)(((int64_t)mx + 15 - (int64_t)mn) & ~(int64_t)15);
-    if (!((uint64_t)ext <= 2ull * rs + 4096u)) return s;
-    s.lo = uniform64(anchor + (int64_t)mn);
-    s.w = make_window(s.lo, ext);
-    s.nsteps = ((ext >> 4) + SQ - 1u) / SQ;
-    return s;
-}
-
-constexpr uint32_t PFBQ = 64;                // a wave's list of groups for the sorted rounds
-constexpr uint32_t PFB_STOP = PFBQ - 8;       // no new claims once the list holds this many
-
-// The sorted rounds for the groups on a wave's list, as a call where nothing of the stream is live
-// (inlined into the pass loop it left the compiler unable to prove the stream's windows uniform: a
-// waterfall loop around every load; the arguments as values: a reference to the kernel's FlatArgs
-// would put it in scratch and every use of a field in the stream would wait on a scratch load)
-__device__ __attribute__((noinline)) void pstream_drain(uint8_t* base, uint64_t base_len, const pico_csum_desc_dev* desc,
-                                                       uint32_t n, uint32_t fpw, uint32_t flags, uint16_t* out_net,
-                                                       uint16_t* out_l4, uint8_t* verdict, SortedWaveSmem<true>& SM,
-                                                       const uint32_t* fbq, uint32_t nfb, uint32_t lane) {
-    const FlatArgs q{base, base_len, desc, n, fpw, -1, flags, nullptr, nullptr, out_net, out_l4, verdict, 0u, 0u, 0u};
-    for (uint32_t i = 0; i < nfb; ++i)
-        sorted_batch<1, true, 8, true>(q, SM.s, SM.stage, lane,
-                                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)fbq[i]) * fpw);
-}
-
-template <int WPS>
-__global__ __launch_bounds__(64 * WPB, WPS) void csum_pstream_kernel(FlatArgs p) {
-    __shared__ SortedWaveSmem<true> lds_all[WPB];
-    __shared__ uint32_t fbq_all[WPB][PFBQ];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    SortedWaveSmem<true>& SM = lds_all[wv];
-    StreamLds& S = SM.st;
-    uint32_t* const fbq = fbq_all[wv];
-    PStreamCtl* const ctl = g_pstream_ctl + (p.ctl_slot < NPCTL ? p.ctl_slot : 0u);
-    const bool tx = (p.flags & 2u) != 0;
-    const uint32_t P = gridDim.x * WPB;
-    const uint64_t ng = ((uint64_t)p.n + p.fpw - 1u) / p.fpw;
-    constexpr uint32_t HS = 4u;
-    constexpr uint32_t EMPTY = NONE - 1u;               // the empty group a pass starts on
-    // group gi's descriptors (lane j: datagram j; absent lanes and groups read zeros)
-    auto load_desc = [&](uint32_t gi) __attribute__((always_inline)) -> uint4 {
-        const uint64_t f = gi == NONE ? 0ull : (uint64_t)gi * p.fpw;
-        const uint32_t c = gi == NONE ? 0u : (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f);
-        const Window dw = make_window(reinterpret_cast<uintptr_t>(p.desc + f), 16u * c);
-        return load_win<false>(dw, 16u * lane);
-    };
-    // (readfirstlane: the compiler cannot tell that threadIdx.x >> 6 is uniform in a wave -- a divergent
-    // group index makes every window a waterfall loop)
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * WPB + wv));
-    // claims: group P + k for the k-th claim (the first P groups go one per wave); `more` turns
-    // false once a claim comes back past the batch, `claiming` = a claim is in flight
-    // (static order, ctl_slot == NPCTL: the k-th "claim" of wave w is group w + (k + 1) P, no atomics)
-    uint32_t kc = 0;                                    // lane 0: the claim in flight
-    bool claiming = false, more = true;
-    uint32_t nfb = 0;                                   // groups in fbq
-    const bool dyn = p.ctl_slot < NPCTL;
-    uint32_t nclaims = 0;
-    auto issue_claim = [&]() __attribute__((always_inline)) {
-        if (!dyn) kc = w + P * nclaims++;
-        else if (lane == 0) kc = __hip_atomic_fetch_add(&ctl->head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // the claim in flight -> a group (or NONE), and the next claim unless the batch is done or the
-    // list is near full (the pass then runs dry and the sorted rounds empty the list)
-    auto next_group = [&]() __attribute__((always_inline)) -> uint32_t {
-        if (!claiming) return NONE;
-        const uint64_t gi = (uint64_t)P + (uint32_t)__builtin_amdgcn_readfirstlane((int)kc);
-        const uint32_t r = gi < ng ? (uint32_t)gi : NONE;
-        more = r != NONE;
-        claiming = more && nfb < PFB_STOP;
-        if (claiming) issue_claim();
-        return r;
-    };
-    auto push_fb = [&](uint32_t gi) __attribute__((always_inline)) {
-        if (lane == 0) fbq[nfb] = gi;
-        ++nfb;
-    };
-    // the pipeline: g (streaming), g1 (next: descriptors d1 in), g2 (after it: d2 in flight), and the
-    // claim for the one after g2.  A pass starts on an empty group (one step of zeros) whose
-    // boundary sets up the first real group.
-    uint32_t g = EMPTY, g1 = NONE, g2 = NONE;
-    uint4 d = make_uint4(0, 0, 0, 0), d1 = d, d2 = d;
-    PSpan sp, spn;
-    uint32_t cnt = 0, len = 0, rel = 0, hq = 0, nlh = 0, b1 = 0, b2 = 0, P1 = 0, P2 = 0, base = 0, st = 0;
-    bool valid = false, oob = false, live = true;
-    uint4 hw[HW];
-#pragma unroll
-    for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
-    auto setup_lanes = [&]() __attribute__((always_inline)) {
-        const uint64_t f0 = (uint64_t)g * p.fpw;
-        cnt = (uint32_t)min((uint64_t)p.fpw, (uint64_t)p.n - f0);
-        uint64_t off0 = ((uint64_t)d.y << 32) | d.x;
-        len = lane < cnt ? d.z : 0u;
-        oob = lane < cnt && (off0 > p.base_len || len > p.base_len - off0);
-        if (oob || lane >= cnt) { len = 0; off0 = 0; }
-        valid = len >= 20u;
-        const uint64_t addr = reinterpret_cast<uintptr_t>(p.base) + off0;
-        rel = valid ? (uint32_t)(addr - sp.lo) : 0u;
-        hq = rel >> 4;
-        nlh = valid ? min(HS, ((rel & 15u) + len + 15u) >> 4) : 0u;
-        b1 = valid ? rel + min(20u, len) : 0u;
-        b2 = valid ? rel + len : 0u;
-        P1 = P2 = base = 0u;
-        st = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < HW; ++i) hw[i] = make_uint4(0, 0, 0, 0);
-    };
-    auto load_step = [&](const Window& win, uint32_t qs, uint4 (&dst)[SCPL]) __attribute__((always_inline)) {
-        // the step starting at chunk qs (offsets past the window's end read zeros)
-        const uint32_t o = 16u * (qs + lane);
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) dst[c] = load_win<true>(win, o + 1024u * c);
-    };
-    uint4 v[SCPL], vn[SCPL];
-    auto step = [&](uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) __attribute__((always_inline)) {
-        const bool last = st + 1u == sp.nsteps;
-        if (last) {
-            // the boundary: the claim read (g2) and the next claim, g2's descriptors, g1's span and
-            // its first step -- all but the last issued before this step's loads, so free to wait on
-            g2 = next_group();
-            d2 = load_desc(g2);
-            spn = pstream_span(p, lane, g1, d1);
-            load_step(spn.w, 0u, nxt);
-        } else {
-            load_step(sp.w, (st + 1u) * SQ, nxt);
-        }
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
-        __builtin_amdgcn_wave_barrier();
-        uint32_t loc[SCPL];
-        uint32_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < SCPL; ++k) {
-            loc[k] = t;
-            t = add_full<false>(S.raw[sslot(SCPL * lane + k)], SEL_EVEN, t);
-        }
-        const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
-        const uint32_t exs = base + incs - t;
-#pragma unroll
-        for (uint32_t k = 0; k < SCPL; k += 4)
-            *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + k]) =
-                make_uint4(exs + loc[k], exs + loc[k + 1], exs + loc[k + 2], exs + loc[k + 3]);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t qb = st * SQ;
-#pragma unroll
-        for (uint32_t i = 0; i < HS; ++i) {
-            const uint32_t qi = hq + i - qb;
-            if (i < nlh && qi < SQ) hw[i] = S.raw[sslot(qi)];
-        }
-        const uint32_t byte0 = 16u * qb;
-        stream_point(S, b1, byte0, P1);
-        stream_point(S, b2, byte0, P2);
-        base += tot;
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (!last) {
-            ++st;
-            return;
-        }
-        // group g's finish (the empty group has none) while g1's first step is in flight; a group it
-        // does not finish goes on the list for the sorted rounds
-        if (g != EMPTY &&
-            !stream_finish<false, false, false>(p, S, lane, (uint64_t)g * p.fpw, cnt, tx, make_uint2(0u, 0u),
-                                                valid, oob, len, false, rel, sp.lo, hw, 0u, P1, P2, 0u, 0u))
-            push_fb(g);
-        __builtin_amdgcn_wave_barrier();
-        g = g1;
-        d = d1;
-        sp = spn;
-        g1 = g2;
-        d1 = d2;
-        // a group that is not streamed goes on the list, and the one after it is set up here (its
-        // first step loaded again)
-        while (g != NONE && sp.nsteps == 0u) {
-            push_fb(g);
-            g = g1;
-            d = d1;
-            g1 = next_group();
-            d1 = load_desc(g1);
-            sp = pstream_span(p, lane, g, d);
-            load_step(sp.w, 0u, nxt);
-        }
-        live = g != NONE;
-        if (live) setup_lanes();
-    };
-    // passes: stream until the batch is done or the list is near full, then the sorted rounds for
-    // the list (nothing of the stream live across them), then the next pass from a fresh claim
-    for (bool first = true;; first = false) {
-        if (first) {
-            g1 = w < ng ? w : NONE;
-            more = g1 != NONE && (uint64_t)P < ng;
-            claiming = more;
-            if (claiming) issue_claim();
-        } else {
-            if (!more) break;
-            claiming = true;
-            issue_claim();
-            g1 = next_group();
-        }
-        d1 = load_desc(g1);
-        g = EMPTY;
-        sp.w = make_window(0ull, 0u);
-        sp.lo = 0;
-        sp.nsteps = 1;
-        st = 0;
-        live = true;
-        load_step(sp.w, 0u, v);                         // the empty group's step: zeros
-        for (;;) {
-            step(v, vn);
-            if (!live) break;
-            step(vn, v);
-            if (!live) break;
-        }
-        if (nfb) pstream_drain(p.base, p.base_len, p.desc, p.n, p.fpw, p.flags, p.out_net, p.out_l4, p.verdict, SM, fbq,
-                               nfb, lane);
-        nfb = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (!more) break;
-    }
-    // every claim this wave issued has been read: the last wave out resets the slot
-    if (dyn && lane == 0 &&
-        __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1u) {
-        __hip_atomic_store(&ctl->head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-#endif  // SORTED_MODE == 1
 
 #if SORTED_MODE == 0
 // ---------------------------------------------------------------- uniform rings: stream waves
@@ -1800,217 +1506,6 @@ __device__ __forceinline__ void uniform_stream_range(const UniArgs& p, StreamLds
         step(st, v, vn);
         if (st + 1u >= nsteps) break;
         step(st + 1u, vn, v);
-    }
-}
-
-// ---- the same stream over claimed chunks (csum_uniform_chunk_kernel)
-//
-// One wave per SIMD reads fastest per byte (C3: 7.0 TB/s against 6.5 for a wave per 64 frames), but
-// a fixed range per wave leaves a tail: the XCDs start a few microseconds apart and the waves'
-// rates differ, about 13 us of a C1 launch (profiles/r05/ab_uniform_stream_*.txt).  Here the batch
-// is cut into chunks of cf frames (<= 64: lane j owns frame j of a chunk); wave w streams chunk w,
-// then chunks claimed from per-XCD ranges (an XCD's waves claim from its range, then from the
-// others once it is empty -- the balancing across XCDs), and the stream does not stop between
-// chunks: the next chunk's first step is loaded during this chunk's last one.  A claim is one
-// returning atomic, issued after a step's loads and read a step later (so the in-order vmcnt the
-// step's data waits on never includes it), once per chunk -- a few per wave, not a burst.
-struct StreamCtl {
-    uint32_t head[8];      // per-XCD claim counters
-    uint32_t done[8];      // per-XCD workgroups that left
-    uint32_t xcds;         // XCDs whose workgroups all left
-    uint32_t pad[15];
-};
-constexpr uint32_t NCTL = 4096;
-__device__ StreamCtl g_stream_ctl[NCTL];
-
-__device__ __forceinline__ uint32_t ctl_add(uint32_t* a) {
-    return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct UniChunkArgs {
-    uint8_t* base;
-    uint64_t stride;
-    uint32_t len;
-    uint32_t n;
-    uint32_t seed;
-    uint32_t cf;           // frames per chunk (1 .. 64)
-    uint16_t* out;
-    uint32_t ctl_slot;     // NCTL: no claims (chunks w, w + P, ...)
-};
-
-struct ChunkSpan {
-    Window w;
-    uint32_t q1, nsteps, r0, cnt;
-};
-
-__device__ __forceinline__ ChunkSpan chunk_span(const UniChunkArgs& p, uint32_t c) {
-    ChunkSpan k;
-    const uint64_t f0 = (uint64_t)c * p.cf;
-    k.cnt = (uint32_t)min((uint64_t)p.cf, (uint64_t)p.n - f0);
-    const uint64_t first = reinterpret_cast<uintptr_t>(p.base) + f0 * p.stride;
-    const uint64_t lo = first & ~(uint64_t)15;
-    const uint64_t end = first + (uint64_t)(k.cnt - 1u) * p.stride + p.len;
-    const uint32_t extent = (uint32_t)(((end + 15u) & ~(uint64_t)15) - lo);
-    k.w = make_window(lo, extent);
-    k.q1 = extent >> 4;
-    k.nsteps = (k.q1 + SQ - 1u) / SQ;
-    k.r0 = (uint32_t)(first - lo);
-    return k;
-}
-
-template <int WPS>
-__global__ __launch_bounds__(64 * WPB, WPS) void csum_uniform_chunk_kernel(UniChunkArgs p) {
-    __shared__ StreamLds lds_all[WPB];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    StreamLds& S = lds_all[wv];
-    StreamCtl* const ctl = p.ctl_slot < NCTL ? g_stream_ctl + p.ctl_slot : nullptr;
-    const uint32_t P = gridDim.x * WPB;
-    const uint32_t nch = (uint32_t)(((uint64_t)p.n + p.cf - 1u) / p.cf);
-    const uint32_t dyn = ctl && nch > P ? nch - P : 0u;
-    const uint32_t R = (dyn + 7u) >> 3;
-    const uint32_t home = blockIdx.x & 7u;
-    constexpr uint32_t NO = 0xFFFFFFFFu;
-    uint32_t empty = dyn ? 0u : 0xFFu;       // claim ranges found exhausted
-    uint32_t c = blockIdx.x * WPB + wv;      // the chunk being streamed
-    uint32_t cn = NO;                        // the next one, once known
-    bool asked = false;                      // a claim has gone out for this chunk's successor
-    int xp = -1;                             // head of the claim in flight (its result read a step later)
-    uint32_t kp = 0;
-    auto range_size = [&](uint32_t x) { return x * R < dyn ? min(R, dyn - x * R) : 0u; };
-    auto next_head = [&]() -> int {          // the first non-empty range, home first
-        for (uint32_t t = 0; t < 8u; ++t) {
-            const uint32_t x = (home + t) & 7u;
-            if (!(empty & (1u << x))) return (int)x;
-        }
-        return -1;
-    };
-    auto issue_claim = [&]() {
-        const int x = next_head();
-        xp = x;
-        if (x >= 0 && lane == 0) kp = ctl_add(&ctl->head[x]);
-    };
-    auto read_claim = [&]() {                // the claim in flight: a chunk, or its range is empty
-        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)kp);
-        const uint32_t x = (uint32_t)xp;
-        xp = -1;
-        if (k < range_size(x)) cn = P + x * R + k;
-        else empty |= 1u << x;
-    };
-    auto static_next = [&]() { cn = c + P < nch ? c + P : NO; };
-    if (c < nch) {
-        ChunkSpan k = chunk_span(p, c), kn;
-        kn.nsteps = 0;
-        // this lane's frame of the chunk: points (span positions), prefixes
-        uint32_t b1 = 0, b2 = 0, P1 = 0, P2 = 0, base = 0;
-        bool t1 = false;
-        auto frame_points = [&]() {
-            const uint32_t rel = k.r0 + (uint32_t)((uint64_t)lane * p.stride);
-            b1 = rel;
-            b2 = rel + p.len;
-            P1 = P2 = 0u;
-            t1 = rel == 0u;
-            base = 0u;
-        };
-        frame_points();
-        uint32_t st = 0;                     // step of chunk c being processed
-        uint4 v[SCPL], vn[SCPL];
-        auto load_to = [&](const Window& w, uint32_t qs, uint32_t q1, uint4 (&dst)[SCPL]) {
-            const uint32_t o = 16u * (qs + lane), oe = 16u * q1;
-#pragma unroll
-            for (uint32_t cc = 0; cc < SCPL; ++cc)
-                dst[cc] = load_win<true>(w, o + 1024u * cc < oe ? o + 1024u * cc : WIN_OOB);
-        };
-        load_to(k.w, 0u, k.q1, v);
-        bool live = true;
-        auto step = [&](uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
-            // the successor must be known before the loads that follow this chunk's last step
-            if (st + 1u >= k.nsteps && cn == NO) {
-                if (!ctl) {
-                    static_next();
-                } else {
-                    if (xp >= 0) read_claim();
-                    while (cn == NO && next_head() >= 0) {
-                        issue_claim();
-                        read_claim();
-                    }
-                }
-                if (cn != NO) kn = chunk_span(p, cn);
-            }
-            if (st + 1u < k.nsteps) load_to(k.w, (st + 1u) * SQ, k.q1, nxt);
-            else if (cn != NO) load_to(kn.w, 0u, kn.q1, nxt);
-            asm volatile("" ::: "memory");
-            // claims ride behind the loads just issued: a result is read one step later
-            if (ctl) {
-                if (xp >= 0) {
-                    read_claim();
-                    if (cn != NO) kn = chunk_span(p, cn);
-                }
-                if (cn == NO && xp < 0 && next_head() >= 0 && (!asked || st + 1u < k.nsteps)) {
-                    issue_claim();
-                    asked = true;
-                }
-            }
-#pragma unroll
-            for (uint32_t cc = 0; cc < SCPL; ++cc) S.raw[sslot(64u * cc + lane)] = cur[cc];
-            __builtin_amdgcn_wave_barrier();
-            uint32_t loc[SCPL];
-            uint32_t t = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < SCPL; ++q) {
-                loc[q] = t;
-                t = add_full<false>(S.raw[sslot(SCPL * lane + q)], SEL_EVEN, t);
-            }
-            const uint32_t incs = (uint32_t)wave_incl<0>((int)t);
-            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incs, 63);
-            const uint32_t exs = base + incs - t;
-#pragma unroll
-            for (uint32_t q = 0; q < SCPL; q += 4)
-                *reinterpret_cast<uint4*>(&S.pxc[SCPL * lane + q]) =
-                    make_uint4(exs + loc[q], exs + loc[q + 1], exs + loc[q + 2], exs + loc[q + 3]);
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t byte0 = 16u * st * SQ;
-            if (lane < k.cnt) {
-                if (!t1) t1 = stream_point(S, b1, byte0, P1);
-                if (t1) stream_point(S, b2, byte0, P2);
-            }
-            base += tot;
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            if (++st == k.nsteps) {          // the chunk's last step: results, then its successor
-                if (lane < k.cnt)
-                    p.out[(uint64_t)c * p.cf + lane] = (uint16_t)finalize(p.seed + pairing(P2 - P1, (b1 & 1u) != 0u));
-                c = cn;
-                cn = NO;
-                asked = false;
-                st = 0;
-                live = c != NO;
-                if (live) {
-                    k = kn;
-                    frame_points();
-                }
-            }
-        };
-        for (;;) {
-            step(v, vn);
-            if (!live) break;
-            step(vn, v);
-            if (!live) break;
-        }
-    }
-    if (!ctl) return;
-    // every wave is out of the loop: the last workgroup resets the slot (per-XCD arrivals)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t wgs = (gridDim.x - home + 7u) >> 3;
-        const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u;
-        if (ctl_add(&ctl->done[home]) == wgs - 1u && ctl_add(&ctl->xcds) == nx - 1u) {
-#pragma unroll
-            for (uint32_t x = 0; x < 8u; ++x) {
-                __hip_atomic_store(&ctl->head[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl->done[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __hip_atomic_store(&ctl->xcds, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
@@ -2213,35 +1708,7 @@ int SORTED_LAUNCH(const void* args, void* stream) {
     return (int)hipGetLastError();
 }
 
-#if SORTED_MODE == 1
-// Persistent stream waves (IPv4 RX / TX, no NAT): wps waves per SIMD on cus compute units; dyn: claimed
-// groups, else static order.
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream);
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream) {
-    static std::atomic<uint32_t> slot{0};
-    FlatArgs a = *static_cast<const FlatArgs*>(args);
-    if ((a.flags & F_NAT) || (wps != 1 && wps != 2) || cus == 0) return (int)hipErrorInvalidValue;
-    a.ctl_slot = dyn ? slot.fetch_add(1u, std::memory_order_relaxed) % NPCTL : NPCTL;
-    auto kern = wps == 1 ? csum_pstream_kernel<1> : csum_pstream_kernel<2>;
-    hipLaunchKernelGGL(kern, dim3(cus * wps), dim3(64 * WPB), 0, static_cast<hipStream_t>(stream), a);
-    return (int)hipGetLastError();
-}
-#endif
-
 #if SORTED_MODE == 0
-int pico_csum_pstream_launch_mode1(const void* args, uint32_t wps, uint32_t cus, int dyn, void* stream);
-
-// Persistent stream waves over an IPv4 descriptor batch (mode 1 only for now): fpw datagrams a group.
-int pico_csum_launch_pstream(void* base, uint64_t base_len, const void* desc, uint32_t n, uint32_t flags,
-                             uint16_t* out_net, uint16_t* out_l4, uint8_t* verdict, uint32_t fpw, uint32_t wps,
-                             uint32_t cus, int dyn, void* stream) {
-    if (fpw < 1 || fpw > 64 || n >= 0x80000000u) return (int)hipErrorInvalidValue;
-    if (n == 0) return (int)hipSuccess;
-    FlatArgs a{static_cast<uint8_t*>(base), base_len, static_cast<const pico_csum_desc_dev*>(desc), n, fpw,
-               -1, flags, nullptr, nullptr, out_net, out_l4, verdict, 0u, 0u, 0u};
-    return pico_csum_pstream_launch_mode1(&a, wps, cus, dyn, stream);
-}
-
 int pico_csum_sorted_launch_mode1(const void* args, void* stream);
 int pico_csum_sorted_launch_mode2(const void* args, void* stream);
 int pico_csum_sorted_launch_mode3(const void* args, void* stream);
@@ -2272,20 +1739,6 @@ int pico_csum_launch_uniform_stream(const void* base, uint64_t stride, uint32_t 
     UniArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), stride, len, n, seed, fpw, out};
     const uint64_t waves = ((uint64_t)n + fpw - 1u) / fpw;
     hipLaunchKernelGGL(csum_uniform_stream_kernel<4>, dim3((unsigned)((waves + WPB - 1u) / WPB)), dim3(64 * WPB), 0,
-                       static_cast<hipStream_t>(stream), a);
-    return (int)hipGetLastError();
-}
-
-// Uniform rings on claimed chunks: waves workgroups' worth of one-per-SIMD waves, cf frames a chunk,
-// claims on (dyn) or static chunk order.
-int pico_csum_launch_uniform_chunks(const void* base, uint64_t stride, uint32_t len, uint32_t n, uint32_t seed,
-                                    uint16_t* out, uint32_t cf, uint32_t waves, int dyn, void* stream) {
-    static std::atomic<uint32_t> slot{0};
-    if (n == 0) return (int)hipSuccess;
-    if (cf < 1 || cf > 64 || waves < WPB) return (int)hipErrorInvalidValue;
-    UniChunkArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), stride, len, n, seed, cf, out,
-                   dyn ? slot.fetch_add(1u, std::memory_order_relaxed) % NCTL : NCTL};
-    hipLaunchKernelGGL(csum_uniform_chunk_kernel<1>, dim3(waves / WPB), dim3(64 * WPB), 0,
                        static_cast<hipStream_t>(stream), a);
     return (int)hipGetLastError();
 }
