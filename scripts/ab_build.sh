@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B variant of the library: rebuild one kernel TU with extra -D flags and link it with the
-# product's other objects into picotcp_amd/ab/libpicocsum_<name>.so (scripts/gpu_ab.sh A=<name>).
+# product's other objects into ablib/libpicocsum_<name>.so (scripts/gpu_ab.sh A=<name>).
 #   [SRC=<other source of the TU>] scripts/ab_build.sh <name> <tu: frag|raw|sorted_m0..3|sorted_fused> -DFLAG=V ...
 # sorted_fused: the sorted TU's fused modes 1-3 (the stream paths) from SRC, mode 0 from the product.
 set -e
@@ -8,7 +8,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; TU=$2; shift 2
 make -s -j8 -C $R/picotcp_amd/csrc
 B=$R/build/csrc; H=$R/picotcp_amd/csrc
-mkdir -p $R/picotcp_amd/ab $B/ab
+mkdir -p $R/ablib $B/ab
 HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include"
 case $TU in
   sorted_fused)
@@ -22,6 +22,6 @@ if [ $TU != sorted_fused ]; then
   $HIPCC $EXTRA "$@" -c $SRC -o $B/ab/$NAME.o
   OBJS="$(ls $B/pico_csum_k_raw.o $B/k_sorted_m?.o $B/pico_csum_k_frag.o $B/pico_csum.o | grep -v "^$OBJ\$") $B/ab/$NAME.o"
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/picotcp_amd/ab/libpicocsum_$NAME.so $OBJS \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/ablib/libpicocsum_$NAME.so $OBJS \
     -Wl,--no-undefined -Wl,-soname,libpicocsum.so
-echo "picotcp_amd/ab/libpicocsum_$NAME.so"
+echo "ablib/libpicocsum_$NAME.so"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Interleaved A/B of two builds of the library on one box: picotcp_amd/ab/libpicocsum_<A>.so vs
+# Interleaved A/B of two builds of the library on one box: ablib/libpicocsum_<A>.so vs
 # the in-tree picotcp_amd/libpicocsum.so ("new"), ROUNDS x configs, bench lines without the CPU
 # legs.  Output: gpurun_out/ab_$TAG.txt (variant config kernel_avg_us value).
 set -e
@@ -13,7 +13,7 @@ cd $R
 for r in $(seq ${ROUNDS:-3}); do
   for v in $A new; do
     lib=$R/picotcp_amd/libpicocsum.so
-    [ $v != new ] && lib=$R/picotcp_amd/ab/libpicocsum_$v.so
+    [ $v != new ] && lib=$R/ablib/libpicocsum_$v.so
     for c in ${CFGS:-c2 c2v6 c2eth c2tx}; do
       PICO_CSUM_LIB=$lib timeout -k 10 120 python bench.py --config $c --steps ${STEPS:-100} --warmup 10 \
           --no-e2e --no-cpu ${VERIFY:---no-verify} ${EXTRA:-} > $O/ab_line.json 2> $O/ab_err.txt

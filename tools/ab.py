@@ -3,7 +3,7 @@
 and host legs; every run under its own `timeout`; the first failure ends the script).
 
   python tools/ab.py --tag T --configs c2,c2v6 --rounds 2 \\
-      --variant r04=picotcp_amd/ab/libpicocsum_r04.so --variant new= --variant "classic=:--stream 255,0"
+      --variant r04=ablib/libpicocsum_r04.so --variant new= --variant "classic=:--stream 255,0"
 
 A variant is name=[library][:extra bench args]; an empty library is the in-tree one.  Output: gpurun_out/ab_<tag>.txt, one line per run: variant config kernel_avg_us value
 mismatches (or '-' with --no-verify)."""
