@@ -3,7 +3,8 @@
 c3_reasm_il layout) -- tools/gather_ceiling.hip copies every fragment's payload to its place in the
 output, nothing parsed or summed -- timed with HIP events beside the reassembly kernel itself on the
 same batch, interleaved, and the device's sequential copy of the same bytes.  The practical ceiling
-the reassembly kernel is priced against.
+the reassembly kernel is priced against; bare_gather has the reassembly kernel's
+shape (one wave per datagram, two fragments a step), the other bare gathers other grid shapes.
 
   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/gather_ceiling.hip -o tools/bin/libgather_ceiling.so
   python tools/gather_ceiling.py [--v6] [--interleave] [--reps 50]
@@ -36,8 +37,8 @@ def main():
     dev = torch.device("cuda:0")
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "bin", "libgather_ceiling.so"))
     lib.gather_ceiling_launch.restype = ctypes.c_int
-    lib.gather_ceiling_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4 + \
-        [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    lib.gather_ceiling_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4 + \
+        [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     tl = 64512
     hl = 48 if a.v6 else 20
     H = 40 if a.v6 else 20
@@ -60,11 +61,14 @@ def main():
         sets.append((st, t, d_grp))
     s = torch.cuda.current_stream(dev)
 
-    def gather(i):
-        (buf, d_desc, d_grp, out, d_od, nfr, payload), (fs, fd, fl), gr = sets[i % a.rotate]
-        rc = lib.gather_ceiling_launch(buf.data_ptr(), buf.numel(), fs.data_ptr(), fd.data_ptr(), fl.data_ptr(),
-                                       gr.data_ptr(), a.n, out.data_ptr(), out.numel(), ctypes.c_void_p(s.cuda_stream))
-        assert rc == 0
+    def gather(mode):
+        def f(i):
+            (buf, d_desc, d_grp, out, d_od, nfr, payload), (fs, fd, fl), gr = sets[i % a.rotate]
+            rc = lib.gather_ceiling_launch(mode, buf.data_ptr(), buf.numel(), fs.data_ptr(), fd.data_ptr(), fl.data_ptr(),
+                                           gr.data_ptr(), a.n, nfr, out.data_ptr(), out.numel(),
+                                           ctypes.c_void_p(s.cuda_stream))
+            assert rc == 0
+        return f
 
     def reasm(i):
         (buf, d_desc, d_grp, out, d_od, nfr, payload), _, _ = sets[i % a.rotate]
@@ -90,7 +94,9 @@ def main():
     payload = sets[0][0][6]
     res = {}
     for rnd in range(3):
-        for name, f in (("reassemble", reasm), ("bare_gather", gather), ("sequential_copy", copy)):
+        for name, f in (("reassemble", reasm), ("bare_gather", gather(0)), ("bare_gather_4frag_steps", gather(1)),
+                        ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)),
+                        ("sequential_copy", copy)):
             res.setdefault(name, []).append(timed(f))
     out = {"layout": ("ipv6" if a.v6 else "ipv4") + (" interleaved" if a.interleave else " datagram-major"),
            "datagrams": a.n, "payload_bytes": payload}
