@@ -415,6 +415,13 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
 int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll, uint32_t fpw, uint32_t nt,
                                   uint32_t pipeline);
 
+/* Host-resident descriptor batches (pico_*_batch_host), per calling thread: 1 (the default) = a
+ * burst whose whole [base, base + base_len) the device addresses directly -- page-locked by
+ * hipHostMalloc or pico_csum_host_register -- is read (and with F_WRITE written) in place by the
+ * kernel, only descriptors and results staged; 0 = always through the staging buffers.  Results
+ * never depend on it. */
+int pico_csum_set_host_in_place(uint32_t on);
+
 /* Tuning knob (tests / bench sweeps), per calling thread: the uniform rings' stream waves
  * (pico_checksum_batch_uniform_dev / _host on densely packed frames) -- mode 0 = automatic, 1 = on
  * wherever the ring allows them, PICO_CSUM_STREAM_OFF = the lane-group kernels; frames_per_wave

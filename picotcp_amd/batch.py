@@ -331,6 +331,12 @@ def set_uniform_stream(mode: int = 0, frames_per_wave: int = 0) -> None:
     _lib.check("pico_csum_set_uniform_stream", _lib.load().pico_csum_set_uniform_stream(mode, frames_per_wave))
 
 
+def set_host_in_place(on: bool = True) -> None:
+    """Host-resident descriptor batches (this thread): read a device-addressable (page-locked) burst
+    in place (True, the default) or always stage it (False).  Results never depend on it."""
+    _lib.check("pico_csum_set_host_in_place", _lib.load().pico_csum_set_host_in_place(1 if on else 0))
+
+
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps): group 0 = automatic; 2 = descriptor

@@ -145,6 +145,15 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
  * launch from another thread). */
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 = automatic */
+static __thread uint32_t g_host_staged;                 /* host descriptor batches: 1 = never in place */
+
+int pico_csum_set_host_in_place(uint32_t on)
+{
+    if (on > 1)
+        return fail(PICO_CSUM_EINVAL, "in-place mode must be 0 (always staged) or 1 (automatic)");
+    g_host_staged = !on;
+    return 0;
+}
 
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave)
 {
@@ -738,6 +747,107 @@ static int in_bounds(const struct pico_csum_desc *d, uint64_t base_len)
     return d->off <= base_len && d->len <= base_len - d->off;
 }
 
+/* results of slot bb's last chunk, from pinned staging to the caller's arrays */
+static void flush_results(struct pico_csum_ctx *c, int bb, uint16_t *out, uint16_t *out_net, uint16_t *out_l4,
+                          uint8_t *verdict)
+{
+    const uint32_t f0 = c->pend_first[bb], fc = c->pend_cnt[bb];
+    const uint8_t *r = c->h_res[bb];
+    if (!fc)
+        return;
+    if (out) memcpy(out + f0, r + 2u * (size_t)fc, (size_t)fc * 2u);
+    if (out_net) memcpy(out_net + f0, r, (size_t)fc * 2u);
+    if (out_l4) memcpy(out_l4 + f0, r + 2u * (size_t)fc, (size_t)fc * 2u);
+    if (verdict) memcpy(verdict + f0, r + 4u * (size_t)fc, fc);
+    c->pend_cnt[bb] = 0;
+}
+
+static int run_desc_batch(int mode, void *kbase, uint64_t klen, const struct pico_csum_desc *d_desc, uint32_t cnt,
+                          int32_t crc_off, uint32_t flags, const uint8_t *mac, uint8_t *d_res, void *stream)
+{
+    uint16_t *r_net = (uint16_t *)d_res, *r_l4 = (uint16_t *)(d_res + 2u * (size_t)cnt);
+    uint8_t *r_ver = d_res + 4u * (size_t)cnt;
+    switch (mode) {
+    case HB_RAW:
+        return pico_checksum_batch_dev(kbase, klen, d_desc, cnt, crc_off, flags, r_l4, NULL, stream);
+    case HB_IPV4:
+        return pico_ipv4_checksum_batch_dev(kbase, klen, d_desc, cnt, flags, r_net, r_l4, r_ver, stream);
+    case HB_IPV6:
+        return pico_ipv6_checksum_batch_dev(kbase, klen, d_desc, cnt, flags, r_l4, r_ver, stream);
+    default:
+        return pico_eth_checksum_batch_dev(kbase, klen, d_desc, cnt, flags, mac, r_net, r_l4, r_ver, stream);
+    }
+}
+
+/* the requested results of a chunk as one D2H range of its packed slot [net | transport | verdict] */
+static void result_range(uint32_t cnt, const void *out, const void *out_net, const void *out_l4, const void *verdict,
+                         size_t *r0, size_t *r1)
+{
+    *r0 = out_net ? 0u : (out || out_l4) ? 2u * (size_t)cnt : 4u * (size_t)cnt;
+    *r1 = verdict ? 5u * (size_t)cnt : (out || out_l4) ? 4u * (size_t)cnt : 2u * (size_t)cnt;
+}
+
+#define ZC_DESC 32768u
+
+/* The in-place form of desc_batch_host: d_base is the burst's device alias. */
+static int desc_batch_in_place(struct pico_csum_ctx *c, int mode, void *d_base, uint64_t base_len,
+                               const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
+                               const uint8_t *mac, uint16_t *out, uint16_t *out_net, uint16_t *out_l4,
+                               uint8_t *verdict, const char *what)
+{
+    const uint64_t maxd = CTX_MAX_DESC(c->staging);
+    const uint32_t per = (uint32_t)(maxd < ZC_DESC ? maxd : ZC_DESC);
+    const int write = (flags & PICO_CSUM_F_WRITE) != 0;
+    uint32_t i = 0;
+    int b = 0, prev = -1, o, rc = 0;
+    hipError_t e;
+    while (i < n) {
+        const uint32_t cnt = n - i < per ? n - i : per;
+        size_t r0, r1;
+        if ((e = hipEventSynchronize(c->done[b])) != hipSuccess) {
+            rc = fail(PICO_CSUM_EIO, "%s: event synchronize: %s", what, hipGetErrorString(e));
+            break;
+        }
+        flush_results(c, b, out, out_net, out_l4, verdict);
+        memcpy(c->h_desc[b], desc + i, (size_t)cnt * sizeof(struct pico_csum_desc));
+        if (write && prev >= 0 && (e = hipStreamWaitEvent(c->st[b], c->done[prev], 0)) != hipSuccess) {
+            rc = fail(PICO_CSUM_EIO, "%s: stream wait: %s", what, hipGetErrorString(e));
+            break;
+        }
+        if ((e = hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
+                                hipMemcpyHostToDevice, c->st[b])) != hipSuccess) {
+            rc = fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
+            break;
+        }
+        if ((rc = run_desc_batch(mode, d_base, base_len, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b],
+                                 c->st[b])) != 0)
+            break;
+        result_range(cnt, out, out_net, out_l4, verdict, &r0, &r1);
+        if ((out || out_net || out_l4 || verdict) && r1 > r0 &&
+            (e = hipMemcpyAsync(c->h_res[b] + r0, c->d_res[b] + r0, r1 - r0, hipMemcpyDeviceToHost, c->st[b])) !=
+                hipSuccess) {
+            rc = fail(PICO_CSUM_EIO, "%s: D2H: %s", what, hipGetErrorString(e));
+            break;
+        }
+        c->pend_first[b] = i;
+        c->pend_cnt[b] = cnt;
+        if ((e = hipEventRecord(c->done[b], c->st[b])) != hipSuccess) {
+            rc = fail(PICO_CSUM_EIO, "%s: event record: %s", what, hipGetErrorString(e));
+            break;
+        }
+        prev = b;
+        i += cnt;
+        b = b + 1 == NSLOT ? 0 : b + 1;
+    }
+    for (o = 0; o < NSLOT; o++)                  /* drain: nothing lands after the return */
+        if (hipStreamSynchronize(c->st[o]) != hipSuccess && !rc)
+            rc = fail(PICO_CSUM_EIO, "%s: stream synchronize failed", what);
+    if (!rc)
+        for (o = 0; o < NSLOT; o++)
+            flush_results(c, o, out, out_net, out_l4, verdict);
+    return rc;
+}
+
 /* One burst: descriptors [i, j) whose bytes span at most the staging buffer go H2D (the span
  * and the descriptors, rebased to it) on stream b, through the device batch, and their results
  * D2H; the next chunk's H2D overlaps this one on the other stream.  A region outside base_len is
@@ -778,19 +888,22 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         wlo[k] = UINT64_MAX;
         whi[k] = 0;
     }
-    /* results of slot bb's last chunk, from pinned staging to the caller's arrays */
-#define FLUSH(bb)                                                                                  \
-    do {                                                                                           \
-        uint32_t f0 = c->pend_first[bb], fc = c->pend_cnt[bb];                                     \
-        if (fc) {                                                                                  \
-            const uint8_t *r_ = c->h_res[bb];                                                      \
-            if (out) memcpy(out + f0, r_ + 2u * (size_t)fc, (size_t)fc * 2u);                      \
-            if (out_net) memcpy(out_net + f0, r_, (size_t)fc * 2u);                                \
-            if (out_l4) memcpy(out_l4 + f0, r_ + 2u * (size_t)fc, (size_t)fc * 2u);                \
-            if (verdict) memcpy(verdict + f0, r_ + 4u * (size_t)fc, fc);                           \
-            c->pend_cnt[bb] = 0;                                                                   \
-        }                                                                                          \
-    } while (0)
+    /* A burst in page-locked memory the device addresses directly (hipHostMalloc'd, or registered
+     * with pico_csum_host_register) is read in place -- and with F_WRITE written in place -- by the
+     * kernel through its device alias: only descriptors and results go through the staging slots
+     * (C2: 46 GiB/s against 40 staged, DESIGN.md 4 "PCIe-inclusive rate").  Chunks of
+     * ZC_DESC descriptors let one chunk's descriptor copy overlap the previous chunk's kernel; with
+     * F_WRITE the kernels run in order (a chunk may read bytes an earlier one writes). */
+    if (!g_host_staged && base_len > 0) {
+        void *d0 = NULL, *d1 = NULL;
+        if (hipHostGetDevicePointer(&d0, (void *)base, 0) == hipSuccess && d0 &&
+            hipHostGetDevicePointer(&d1, (void *)((const uint8_t *)base + base_len - 1u), 0) == hipSuccess &&
+            (uintptr_t)d1 - (uintptr_t)d0 == base_len - 1u)
+            return desc_batch_in_place(c, mode, d0, base_len, desc, n, crc_off, flags, mac, out, out_net, out_l4,
+                                       verdict, what);
+        (void)hipGetLastError();                 /* (a pageable burst: the staged path below) */
+    }
+#define FLUSH(bb) flush_results(c, bb, out, out_net, out_l4, verdict)
 #define TRY(call, msg)                                                                             \
     if ((e = (call)) != hipSuccess) {                                                              \
         rc = fail(PICO_CSUM_EIO, "%s: %s: %s", what, msg, hipGetErrorString(e));                   \
@@ -801,9 +914,8 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         uint32_t j = i, cnt;
         hipError_t e;
         int vbase;
-        uint8_t *kbase, *r_ver;
+        uint8_t *kbase;
         uint64_t klen;
-        uint16_t *r_net, *r_l4;
         /* grow the chunk while the span fits the staging buffer */
         while (j < n && (uint64_t)(j - i) < maxd) {
             uint64_t o = desc[j].off, oa, end;
@@ -847,9 +959,6 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         }
         kbase = vbase ? (uint8_t *)c->d_buf[b] - lo : (uint8_t *)c->d_buf[b];
         klen = vbase ? hi : hi - lo;
-        r_net = (uint16_t *)c->d_res[b];
-        r_l4 = (uint16_t *)(c->d_res[b] + 2u * (size_t)cnt);
-        r_ver = c->d_res[b] + 4u * (size_t)cnt;
         for (o = 0; o < NSLOT && rc == 0; o++)      /* F_WRITE hulls of the other streams' chunks */
             if (o != b && write && hi > hlo && hlo < whi[o] && wlo[o] < hi)
                 if ((e = hipStreamWaitEvent(c->st[b], c->done[o], 0)) != hipSuccess)
@@ -860,26 +969,12 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
             TRY(hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice, c->st[b]), "H2D")
         TRY(hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
                            hipMemcpyHostToDevice, c->st[b]), "H2D")
-        switch (mode) {
-        case HB_RAW:
-            rc = pico_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, crc_off, flags, r_l4, NULL, c->st[b]);
-            break;
-        case HB_IPV4:
-            rc = pico_ipv4_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, r_net, r_l4, r_ver, c->st[b]);
-            break;
-        case HB_IPV6:
-            rc = pico_ipv6_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, r_l4, r_ver, c->st[b]);
-            break;
-        default:
-            rc = pico_eth_checksum_batch_dev(kbase, klen, c->d_desc[b], cnt, flags, mac, r_net, r_l4, r_ver, c->st[b]);
-            break;
-        }
-        if (rc)
+        if ((rc = run_desc_batch(mode, kbase, klen, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b], c->st[b])) != 0)
             break;
         /* every requested result in one D2H (from the first requested array to the last) */
         {
-            const size_t r0 = out_net ? 0u : (out || out_l4) ? 2u * (size_t)cnt : 4u * (size_t)cnt;
-            const size_t r1 = verdict ? 5u * (size_t)cnt : (out || out_l4) ? 4u * (size_t)cnt : 2u * (size_t)cnt;
+            size_t r0, r1;
+            result_range(cnt, out, out_net, out_l4, verdict, &r0, &r1);
             if ((out || out_net || out_l4 || verdict) && r1 > r0)
                 TRY(hipMemcpyAsync(c->h_res[b] + r0, c->d_res[b] + r0, r1 - r0, hipMemcpyDeviceToHost, c->st[b]), "D2H")
         }
