@@ -787,7 +787,9 @@ static void result_range(uint32_t cnt, const void *out, const void *out_net, con
     *r1 = verdict ? 5u * (size_t)cnt : (out || out_l4) ? 4u * (size_t)cnt : 2u * (size_t)cnt;
 }
 
+#ifndef ZC_DESC
 #define ZC_DESC 32768u
+#endif
 
 /* The in-place form of desc_batch_host: d_base is the burst's device alias. */
 static int desc_batch_in_place(struct pico_csum_ctx *c, int mode, void *d_base, uint64_t base_len,
