@@ -416,9 +416,18 @@ class HostBatch:
                                                       ctypes.c_void_p(out.ctypes.data)))
         return out
 
-    def ipv4_checksum_batch(self, base: np.ndarray, desc: np.ndarray, flags: int = 0):
+    def ipv4_checksum_batch(self, base: np.ndarray, desc: np.ndarray, flags: int = 0, out=None):
+        """`out` may pass the (out_net uint16, out_transport uint16, verdict uint8) host arrays -- e.g.
+        page-locked ones, which with a page-locked burst and descriptors make the call zero-copy."""
         d, b, bl, dp, n = self._desc_args(base, desc)
-        on, ol, v = self._outs(n, np.uint16, np.uint16, np.uint8)
+        if out is None:
+            on, ol, v = self._outs(n, np.uint16, np.uint16, np.uint8)
+        else:
+            on, ol, v = out
+            for a, nm, dt in ((on, "out_net", np.uint16), (ol, "out_transport", np.uint16), (v, "verdict", np.uint8)):
+                self._host(a, nm, dt)
+                if a.size < n:
+                    raise ValueError(f"{nm} shorter than n")
         _lib.check("pico_ipv4_checksum_batch_host",
                    self._lib.pico_ipv4_checksum_batch_host(self._ctx, b, bl, dp, n, flags, on.ctypes.data,
                                                            ol.ctypes.data, v.ctypes.data))

@@ -762,11 +762,11 @@ static void flush_results(struct pico_csum_ctx *c, int bb, uint16_t *out, uint16
     c->pend_cnt[bb] = 0;
 }
 
+/* the device batch of a host batch's mode (raw: its results in r_l4) */
 static int run_desc_batch(int mode, void *kbase, uint64_t klen, const struct pico_csum_desc *d_desc, uint32_t cnt,
-                          int32_t crc_off, uint32_t flags, const uint8_t *mac, uint8_t *d_res, void *stream)
+                          int32_t crc_off, uint32_t flags, const uint8_t *mac, uint16_t *r_net, uint16_t *r_l4,
+                          uint8_t *r_ver, void *stream)
 {
-    uint16_t *r_net = (uint16_t *)d_res, *r_l4 = (uint16_t *)(d_res + 2u * (size_t)cnt);
-    uint8_t *r_ver = d_res + 4u * (size_t)cnt;
     switch (mode) {
     case HB_RAW:
         return pico_checksum_batch_dev(kbase, klen, d_desc, cnt, crc_off, flags, r_l4, NULL, stream);
@@ -779,6 +779,31 @@ static int run_desc_batch(int mode, void *kbase, uint64_t klen, const struct pic
     }
 }
 
+/* a chunk's packed result slot [net: 2 cnt B | transport: 2 cnt B | verdict: cnt B] */
+static int run_desc_batch_packed(int mode, void *kbase, uint64_t klen, const struct pico_csum_desc *d_desc,
+                                 uint32_t cnt, int32_t crc_off, uint32_t flags, const uint8_t *mac, uint8_t *d_res,
+                                 void *stream)
+{
+    return run_desc_batch(mode, kbase, klen, d_desc, cnt, crc_off, flags, mac, (uint16_t *)d_res,
+                          (uint16_t *)(d_res + 2u * (size_t)cnt), d_res + 4u * (size_t)cnt, stream);
+}
+
+/* the device alias of host memory [p, p + bytes) when the device addresses all of it (page-locked
+ * by hipHostMalloc or registered), else NULL */
+static void *host_alias(const void *p, uint64_t bytes)
+{
+    void *d0 = NULL, *d1 = NULL;
+    if (!p || bytes == 0)
+        return NULL;
+    if (hipHostGetDevicePointer(&d0, (void *)p, 0) != hipSuccess || !d0 ||
+        hipHostGetDevicePointer(&d1, (void *)((const uint8_t *)p + bytes - 1u), 0) != hipSuccess ||
+        (uintptr_t)d1 - (uintptr_t)d0 != bytes - 1u) {
+        (void)hipGetLastError();
+        return NULL;
+    }
+    return d0;
+}
+
 /* the requested results of a chunk as one D2H range of its packed slot [net | transport | verdict] */
 static void result_range(uint32_t cnt, const void *out, const void *out_net, const void *out_l4, const void *verdict,
                          size_t *r0, size_t *r1)
@@ -787,8 +812,10 @@ static void result_range(uint32_t cnt, const void *out, const void *out_net, con
     *r1 = verdict ? 5u * (size_t)cnt : (out || out_l4) ? 4u * (size_t)cnt : 2u * (size_t)cnt;
 }
 
+/* descriptors a chunk of the in-place path (r05: 32K chunks 31.6 GiB/s, 128K 41.2, one chunk 40.4
+ * on the C2 burst; profiles/r05/host_inplace_*.txt) */
 #ifndef ZC_DESC
-#define ZC_DESC 32768u
+#define ZC_DESC 131072u
 #endif
 
 /* The in-place form of desc_batch_host: d_base is the burst's device alias. */
@@ -803,6 +830,21 @@ static int desc_batch_in_place(struct pico_csum_ctx *c, int mode, void *d_base, 
     uint32_t i = 0;
     int b = 0, prev = -1, o, rc = 0;
     hipError_t e;
+    /* descriptors and every requested result array device-addressable too (a driver's pinned
+     * rings): one launch over their aliases, nothing staged at all */
+    {
+        void *dd = ((uintptr_t)desc & 15u) == 0 ? host_alias(desc, (uint64_t)n * sizeof(struct pico_csum_desc)) : NULL;
+        void *a_out = out ? host_alias(out, 2ull * n) : NULL, *a_net = out_net ? host_alias(out_net, 2ull * n) : NULL;
+        void *a_l4 = out_l4 ? host_alias(out_l4, 2ull * n) : NULL, *a_ver = verdict ? host_alias(verdict, n) : NULL;
+        if (dd && (!out || a_out) && (!out_net || a_net) && (!out_l4 || a_l4) && (!verdict || a_ver)) {
+            rc = run_desc_batch(mode, d_base, base_len, (const struct pico_csum_desc *)dd, n, crc_off, flags, mac,
+                                (uint16_t *)a_net, (uint16_t *)(mode == HB_RAW ? a_out : a_l4), (uint8_t *)a_ver,
+                                c->st[0]);
+            if ((e = hipStreamSynchronize(c->st[0])) != hipSuccess && !rc)
+                rc = fail(PICO_CSUM_EIO, "%s: stream synchronize: %s", what, hipGetErrorString(e));
+            return rc;
+        }
+    }
     while (i < n) {
         const uint32_t cnt = n - i < per ? n - i : per;
         size_t r0, r1;
@@ -821,8 +863,8 @@ static int desc_batch_in_place(struct pico_csum_ctx *c, int mode, void *d_base, 
             rc = fail(PICO_CSUM_EIO, "%s: H2D: %s", what, hipGetErrorString(e));
             break;
         }
-        if ((rc = run_desc_batch(mode, d_base, base_len, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b],
-                                 c->st[b])) != 0)
+        if ((rc = run_desc_batch_packed(mode, d_base, base_len, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b],
+                                        c->st[b])) != 0)
             break;
         result_range(cnt, out, out_net, out_l4, verdict, &r0, &r1);
         if ((out || out_net || out_l4 || verdict) && r1 > r0 &&
@@ -896,14 +938,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
      * (C2: 46 GiB/s against 40 staged, DESIGN.md 4 "PCIe-inclusive rate").  Chunks of
      * ZC_DESC descriptors let one chunk's descriptor copy overlap the previous chunk's kernel; with
      * F_WRITE the kernels run in order (a chunk may read bytes an earlier one writes). */
-    if (!g_host_staged && base_len > 0) {
-        void *d0 = NULL, *d1 = NULL;
-        if (hipHostGetDevicePointer(&d0, (void *)base, 0) == hipSuccess && d0 &&
-            hipHostGetDevicePointer(&d1, (void *)((const uint8_t *)base + base_len - 1u), 0) == hipSuccess &&
-            (uintptr_t)d1 - (uintptr_t)d0 == base_len - 1u)
+    if (!g_host_staged) {
+        void *d0 = host_alias(base, base_len);   /* (a pageable burst: the staged path below) */
+        if (d0)
             return desc_batch_in_place(c, mode, d0, base_len, desc, n, crc_off, flags, mac, out, out_net, out_l4,
                                        verdict, what);
-        (void)hipGetLastError();                 /* (a pageable burst: the staged path below) */
     }
 #define FLUSH(bb) flush_results(c, bb, out, out_net, out_l4, verdict)
 #define TRY(call, msg)                                                                             \
@@ -971,7 +1010,8 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
             TRY(hipMemcpyAsync(c->d_buf[b], (const uint8_t *)base + lo, hi - lo, hipMemcpyHostToDevice, c->st[b]), "H2D")
         TRY(hipMemcpyAsync(c->d_desc[b], c->h_desc[b], (size_t)cnt * sizeof(struct pico_csum_desc),
                            hipMemcpyHostToDevice, c->st[b]), "H2D")
-        if ((rc = run_desc_batch(mode, kbase, klen, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b], c->st[b])) != 0)
+        if ((rc = run_desc_batch_packed(mode, kbase, klen, c->d_desc[b], cnt, crc_off, flags, mac, c->d_res[b],
+                                        c->st[b])) != 0)
             break;
         /* every requested result in one D2H (from the first requested array to the last) */
         {

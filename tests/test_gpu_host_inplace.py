@@ -139,6 +139,35 @@ def test_registered_numpy_burst(hb):
         np.testing.assert_array_equal(y, w)
 
 
+def test_all_pinned_is_one_zero_copy_launch(hb):
+    """Burst, descriptors and result arrays all page-locked (a driver's pinned rings): one launch on
+    their device aliases, nothing staged -- TX written in place too."""
+    lens = synth.imix_lengths(50_000, 53)
+    buf, net, avail = synth.ipv4_batch(lens, seed=53, proto=6)
+    d = batch.make_desc(net, avail)
+    kb, pb = pinned(buf)
+    kd = torch.from_numpy(np.ascontiguousarray(d).view(np.uint8).copy()).pin_memory()
+    pd = kd.numpy().view(batch.DESC_DTYPE)
+    assert pd.ctypes.data % 16 == 0
+    outs = [torch.zeros(d.size, dtype=dt).pin_memory() for dt in (torch.int16, torch.int16, torch.uint8)]
+    po = (outs[0].numpy().view(np.uint16), outs[1].numpy().view(np.uint16), outs[2].numpy())
+    for tx in (False, True):
+        on, ol, v = hb.ipv4_checksum_batch(pb, pd, flags=_lib.F_TX if tx else 0, out=po)
+        assert on is po[0]
+        wn, wl, wv = O.batch_ipv4(buf, d, tx=tx)
+        np.testing.assert_array_equal(v, wv)
+        np.testing.assert_array_equal(on, wn)
+        np.testing.assert_array_equal(ol, wl)
+    hb.ipv4_checksum_batch(pb, pd, flags=_lib.F_TX | _lib.F_WRITE, out=po)
+    kr, ref = pinned(buf)
+    batch.set_host_in_place(False)
+    hb.ipv4_checksum_batch(ref, d, flags=_lib.F_TX | _lib.F_WRITE)
+    batch.set_host_in_place(True)
+    np.testing.assert_array_equal(pb, ref)
+    on, ol, v = hb.ipv4_checksum_batch(pb, pd, out=po)
+    assert (v == 1).all() and (on == 0).all() and (ol == 0).all()
+
+
 def test_knob_rejects_bad_mode():
     with pytest.raises(_lib.PicoCsumError):
         _lib.check("pico_csum_set_host_in_place", _lib.load().pico_csum_set_host_in_place(2))
