@@ -373,9 +373,10 @@ int pico_checksum_batch_uniform_host(struct pico_csum_ctx *ctx, const void *base
  * rebased descriptors go H2D, the device batch of the same name runs, and only the per-frame
  * results come back (with PICO_CSUM_F_WRITE also the span, crc fields stored); chunk c+1's
  * H2D overlaps chunk c's kernel and D2H on the other stream.  Results, verdicts and error
- * rules are those of the _dev functions; a frame larger than the staging buffer is -EINVAL.
- * With F_WRITE, frames of different chunks must not share bytes (true for a frame ring).
- * Returns when every result is in host memory. */
+ * rules are those of the _dev functions; on the staged path a frame larger than the staging
+ * buffer is -EINVAL.  With F_WRITE, frames of different chunks must not share bytes (true for a
+ * frame ring).  A burst the device addresses directly (page-locked) is read in place instead:
+ * pico_csum_set_host_in_place.  Returns when every result is in host memory. */
 int pico_checksum_batch_host(struct pico_csum_ctx *ctx, const void *base, uint64_t base_len,
                              const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
                              uint16_t *out);
@@ -418,8 +419,9 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
 /* Host-resident descriptor batches (pico_*_batch_host), per calling thread: 1 (the default) = a
  * burst whose whole [base, base + base_len) the device addresses directly -- page-locked by
  * hipHostMalloc or pico_csum_host_register -- is read (and with F_WRITE written) in place by the
- * kernel, only descriptors and results staged; 0 = always through the staging buffers.  Results
- * never depend on it. */
+ * kernel, only descriptors and results staged, and nothing staged when the descriptor and result
+ * arrays are device-addressable too (then frames larger than the staging buffer are fine);
+ * 0 = always through the staging buffers.  Results never depend on it. */
 int pico_csum_set_host_in_place(uint32_t on);
 
 /* Tuning knob (tests / bench sweeps), per calling thread: the uniform rings' stream waves

@@ -747,6 +747,12 @@ static int in_bounds(const struct pico_csum_desc *d, uint64_t base_len)
     return d->off <= base_len && d->len <= base_len - d->off;
 }
 
+/* a frame the staged path cannot stage (its 16-byte-aligned span exceeds the staging buffer) */
+static int too_big(const struct pico_csum_ctx *c, const struct pico_csum_desc *d, uint64_t base_len)
+{
+    return in_bounds(d, base_len) && (d->len > c->staging || (d->off & 15u) + d->len > c->staging);
+}
+
 /* results of slot bb's last chunk, from pinned staging to the caller's arrays */
 static void flush_results(struct pico_csum_ctx *c, int bb, uint16_t *out, uint16_t *out_net, uint16_t *out_l4,
                           uint8_t *verdict)
@@ -901,8 +907,10 @@ static int desc_batch_in_place(struct pico_csum_ctx *c, int mode, void *d_base, 
  * end) -- never the 16-byte rounding below it, which may hold the previous chunk's last frame --
  * and a chunk whose hull overlaps the hull of any chunk issued on the other stream (descriptors
  * not in ascending order) first waits for that stream, so no stale copy can land over a
- * result.  Every argument is checked before the first copy: an error returns with nothing
- * queued and no byte of `base` changed; a HIP error mid-burst drains both streams first. */
+ * result.  With F_WRITE every argument is checked before the first copy: an error returns with
+ * nothing queued and no byte of `base` changed; without it a frame too large to stage is found
+ * where its chunk would start (the results before it are unspecified, nothing is written to
+ * `base`); a HIP error mid-burst drains the streams first. */
 static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, uint64_t base_len,
                            const struct pico_csum_desc *desc, uint32_t n, int32_t crc_off, uint32_t flags,
                            const uint8_t *mac, uint16_t *out, uint16_t *out_net, uint16_t *out_l4, uint8_t *verdict,
@@ -919,10 +927,6 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
         return fail(PICO_CSUM_EINVAL, "%s: NULL argument", what);
     if (n == 0)
         return 0;
-    for (i = 0; i < n; i++)                     /* before anything is queued */
-        if (in_bounds(&desc[i], base_len) && (desc[i].len > c->staging || (desc[i].off & 15u) + desc[i].len > c->staging))
-            return fail(PICO_CSUM_EINVAL, "%s: frame %u of %u bytes exceeds the staging buffer", what, i, desc[i].len);
-    i = 0;
     if (hipSetDevice(c->device) != hipSuccess)
         return fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", c->device);
     if ((rc = ctx_desc_alloc(c)) != 0)
@@ -934,16 +938,26 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
     }
     /* A burst in page-locked memory the device addresses directly (hipHostMalloc'd, or registered
      * with pico_csum_host_register) is read in place -- and with F_WRITE written in place -- by the
-     * kernel through its device alias: only descriptors and results go through the staging slots
-     * (C2: 46 GiB/s against 40 staged, DESIGN.md 4 "PCIe-inclusive rate").  Chunks of
-     * ZC_DESC descriptors let one chunk's descriptor copy overlap the previous chunk's kernel; with
-     * F_WRITE the kernels run in order (a chunk may read bytes an earlier one writes). */
+     * kernel through its device alias: only descriptors and results go through the staging slots,
+     * or nothing at all when they are device-addressable too (DESIGN.md 4 "PCIe-inclusive rate").
+     * Chunks of ZC_DESC descriptors let one chunk's descriptor copy overlap the previous chunk's
+     * kernel; with F_WRITE the kernels run in order (a chunk may read bytes an earlier one writes).
+     * No frame is staged there, so no frame is too large for the staging buffer. */
     if (!g_host_staged) {
         void *d0 = host_alias(base, base_len);   /* (a pageable burst: the staged path below) */
         if (d0)
             return desc_batch_in_place(c, mode, d0, base_len, desc, n, crc_off, flags, mac, out, out_net, out_l4,
                                        verdict, what);
     }
+    /* a frame larger than the staging buffer: with F_WRITE found before anything is queued (no byte
+     * of base changes); else where the chunk loop meets it (the streams drained first) -- a pass
+     * over every descriptor up front costs an RX burst ~0.2 ms of host time (C2, r05) */
+    if (write)
+        for (i = 0; i < n; i++)
+            if (too_big(c, &desc[i], base_len))
+                return fail(PICO_CSUM_EINVAL, "%s: frame %u of %u bytes exceeds the staging buffer", what, i,
+                            desc[i].len);
+    i = 0;
 #define FLUSH(bb) flush_results(c, bb, out, out_net, out_l4, verdict)
 #define TRY(call, msg)                                                                             \
     if ((e = (call)) != hipSuccess) {                                                              \
@@ -964,6 +978,11 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
                 j++;
                 continue;
             }
+            if (too_big(c, &desc[j], base_len)) {
+                rc = fail(PICO_CSUM_EINVAL, "%s: frame %u of %u bytes exceeds the staging buffer", what, j,
+                          desc[j].len);
+                break;
+            }
             oa = o & ~(uint64_t)15;   /* the span starts on a 16-byte line: frames keep their alignment */
             end = o + desc[j].len;
             if ((end > hi ? end : hi) - (oa < lo ? oa : lo) > c->staging)
@@ -973,6 +992,8 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
             if (end > hi) hi = end;
             j++;
         }
+        if (rc)
+            break;
         cnt = j - i;
         if (lo == UINT64_MAX) lo = hi = hlo = 0;
         /* the pinned descriptor and result slots are reused: the previous chunk on them must be

@@ -127,6 +127,20 @@ def test_write_packed_unaligned_and_shuffled(hb, shuffle):
     np.testing.assert_array_equal(buf, exp)
 
 
+def test_oversized_frame_mid_burst_rx_then_next_call_works(hb):
+    """Without F_WRITE a frame too large to stage is found where its chunk would start: -EINVAL
+    after the earlier chunks drained, and the context serves the next call."""
+    buf, offs, lens, _ = _packed_small_frames(20_000, 6)
+    full = np.concatenate([buf, np.zeros(3 << 20, np.uint8)])
+    offs2 = np.concatenate([offs[:10_000], [buf.size], offs[10_000:]]).astype(np.uint64)
+    lens2 = np.concatenate([lens[:10_000], [2 << 20], lens[10_000:]]).astype(np.uint32)
+    with pytest.raises(_lib.PicoCsumError) as e:
+        hb.checksum_batch(full, batch.make_desc(offs2, lens2))
+    assert e.value.rc == -_lib.EINVAL
+    d = batch.make_desc(offs, lens)
+    np.testing.assert_array_equal(hb.checksum_batch(full, d), O.batch_raw(full, d))
+
+
 def test_oversized_frame_mid_burst_with_write_changes_nothing(hb):
     """A frame larger than the staging buffer in the middle of an F_WRITE burst: -EINVAL before
     anything is queued -- no byte of the caller's buffer changes, before or after the return."""

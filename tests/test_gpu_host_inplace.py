@@ -168,6 +168,20 @@ def test_all_pinned_is_one_zero_copy_launch(hb):
     assert (v == 1).all() and (on == 0).all() and (ol == 0).all()
 
 
+def test_frame_larger_than_staging_in_place(hb):
+    """No frame is staged on the in-place path: a 2 MiB frame with 1 MiB of staging is summed (the
+    staged path refuses it, tests/test_gpu_host_desc.py)."""
+    raw = synth.random_bytes(91, 3 << 20)
+    d = batch.make_desc([5, 1 << 20], [2 << 20, 777], [0, 0])
+    kr, br = pinned(raw)
+    out = hb.checksum_batch(br, d)
+    np.testing.assert_array_equal(out, O.batch_raw(raw, d))
+    batch.set_host_in_place(False)
+    with pytest.raises(_lib.PicoCsumError) as e:
+        hb.checksum_batch(br, d)
+    assert e.value.rc == -_lib.EINVAL
+
+
 def test_knob_rejects_bad_mode():
     with pytest.raises(_lib.PicoCsumError):
         _lib.check("pico_csum_set_host_in_place", _lib.load().pico_csum_set_host_in_place(2))
