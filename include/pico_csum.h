@@ -326,8 +326,13 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
  *                      wraps), a fragment header or payload past desc.len or base_len, an empty
  *                      group or one of more than 512 fragments, an output region too small.
  * The bytes of an output region are unspecified when its datagram is not reassembled (the
- * gather starts before completeness is known); no byte outside the region is written.
- * Any of the three output pointers may be NULL. */
+ * gather starts before completeness is known) and past the reassembled datagram's end (a
+ * repeated offset's later arrival may have been gathered there); no byte outside the region is
+ * written.  Any of the three output pointers may be NULL.  Batches of 1024 datagrams or more run
+ * on a flat grid whose per-datagram plans and partial sums live in library scratch (about
+ * 32 + 4 x fragments / 4 bytes a datagram): per calling thread and stream, kept across calls; in
+ * a call captured into a graph, owned by that graph -- two executable instances of one captured
+ * graph must not run concurrently (pico_csum_set_reasm_flat selects the grid). */
 int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
                                    uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
                                    uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
@@ -430,6 +435,12 @@ int pico_csum_set_host_in_place(uint32_t on);
  * 0 = automatic.  Results never depend on it. */
 #define PICO_CSUM_STREAM_OFF 0xFFu
 int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
+
+/* Tuning knob (tests / bench sweeps), per calling thread: the reassembly batches' flat grid
+ * (pico_ipv4_reassemble_batch_dev / pico_ipv6_reassemble_batch_dev) -- 0 = automatic (IPv4
+ * batches of 1024 datagrams or more), 1 = always (IPv6 too), 2 = never (one workgroup per
+ * datagram).  Results never depend on it. */
+int pico_csum_set_reasm_flat(uint32_t mode);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,7 @@ EXPORTED = (
     "pico_csum_set_launch_override",
     "pico_csum_set_uniform_stream",
     "pico_csum_set_host_in_place",
+    "pico_csum_set_reasm_flat",
 )
 
 F_WRITE = 0x1
@@ -120,6 +121,8 @@ def load() -> ctypes.CDLL:
         sig("pico_csum_set_uniform_stream", ctypes.c_int, u32, u32)
     if hasattr(lib, "pico_csum_set_host_in_place"):
         sig("pico_csum_set_host_in_place", ctypes.c_int, u32)
+    if hasattr(lib, "pico_csum_set_reasm_flat"):
+        sig("pico_csum_set_reasm_flat", ctypes.c_int, u32)
     del u8p
     if lib.pico_csum_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {lib.pico_csum_abi_version()}, this binding {ABI_VERSION}: rebuild it")

@@ -337,6 +337,12 @@ def set_host_in_place(on: bool = True) -> None:
     _lib.check("pico_csum_set_host_in_place", _lib.load().pico_csum_set_host_in_place(1 if on else 0))
 
 
+def set_reasm_flat(mode: int = 0) -> None:
+    """Reassembly batches' flat grid (tests / bench sweeps, this thread): 0 automatic (IPv4 batches
+    from 1024 datagrams), 1 always (IPv6 too), 2 never.  Results never depend on it."""
+    _lib.check("pico_csum_set_reasm_flat", _lib.load().pico_csum_set_reasm_flat(mode))
+
+
 def set_launch_override(group: int = 0, cpl: int = 0, fpw: int = 0, unroll: int | None = None, nt: int = 0,
                         pipeline: int = 0) -> None:
     """Force a kernel launch shape (tests / bench sweeps): group 0 = automatic; 2 = descriptor

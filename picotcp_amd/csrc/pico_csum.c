@@ -42,7 +42,8 @@ int pico_csum_launch_ipv4_forward(void *base, uint64_t base_len, const void *des
                                   uint32_t n_local, uint32_t *state, uint8_t *verdict, void *stream);
 int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, const void *frag, uint32_t n_frag,
                                 const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len, const void *out_desc,
-                                uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict, uint32_t flags, void *stream);
+                                uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict, uint32_t flags, uint32_t flat_min,
+                                void *stream);
 
 /* ------------------------------------------------------------------ errors */
 
@@ -146,6 +147,15 @@ uint32_t pico_ipv6_pseudo_partial(const void *src16, const void *dst16, uint8_t 
 static __thread uint32_t g_ovr_group, g_ovr_cpl, g_ovr_unroll, g_ovr_fpw, g_ovr_nt, g_ovr_pipe;
 static __thread uint32_t g_ovr_smode, g_ovr_sfpw;     /* uniform-ring stream: 0 = automatic */
 static __thread uint32_t g_host_staged;                 /* host descriptor batches: 1 = never in place */
+static __thread uint32_t g_reasm_flat;                  /* reassembly flat grid: 0 auto, 1 always, 2 never */
+
+int pico_csum_set_reasm_flat(uint32_t mode)
+{
+    if (mode > 2)
+        return fail(PICO_CSUM_EINVAL, "reassembly flat-grid mode must be 0 (auto), 1 (always) or 2 (never)");
+    g_reasm_flat = mode;
+    return 0;
+}
 
 int pico_csum_set_host_in_place(uint32_t on)
 {
@@ -535,7 +545,8 @@ static int reassemble_dev(int v6, const void *d_base, uint64_t base_len, const s
         return rc;
     return launch_status(pico_csum_launch_reassemble(v6, d_base, base_len, d_frag, n_frag, d_groups, n_dgram, d_out,
                                                      out_len, d_out_desc, d_out_len, d_out_transport, d_verdict,
-                                                     flags, stream),
+                                                     flags, g_reasm_flat == 1 ? 1u : g_reasm_flat == 2 ? UINT32_MAX : 0u,
+                                                     stream),
                          what);
 }
 

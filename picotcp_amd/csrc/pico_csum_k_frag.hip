@@ -12,8 +12,11 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// One workgroup (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are
-// a contiguous descriptor range, in arrival order):
+// IPv4 batches of >= 1024 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
+// the gather spread over ~one wave per four fragments, the plan and the sums brought together
+// after it).  Otherwise -- and for a flat-grid datagram the plan could not settle -- one workgroup
+// (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are a contiguous
+// descriptor range, in arrival order):
 //   1. all threads parse the fragment headers (IPv4: IHL, total length, MF, offset; IPv6: the
 //      extension-header walk, payload length, M, offset, protocol) into LDS and
 //      mark repeated offsets (pico_tree_insert rejects a repeated key: the earliest arrival
@@ -48,8 +51,12 @@
 //      larger-occupancy LDS tables, three register sets, the completeness check or the header
 //      copy after the gather, a lean whole-unit slot path with the edge units in 4 lanes, the
 //      gather in tree order.
-// The bytes of an output region are unspecified when its datagram is not reassembled.
+// The bytes of an output region are unspecified when its datagram is not reassembled, and past
+// the reassembled datagram's end.
 #include "pico_csum_dev.h"
+
+#include <mutex>
+#include <vector>
 
 namespace {
 
@@ -88,7 +95,22 @@ struct FragArgs {
     uint32_t* o_len;
     uint16_t* o_l4;
     uint8_t* verdict;
+    // flat grid (reasm_flat_kernel, then reassemble_kernel<V6, 1, true>): S waves per datagram,
+    // one plan per datagram, one partial sum per wave
+    struct ReasmPlan* plan;
+    uint32_t* slot;
+    uint32_t S;
 };
+
+// A datagram's plan, written by wave 0 of its flat-grid slice: GOOD (complete: the finish adds the
+// waves' partial sums), BAD (not reassembled) or SLOW (repeated offsets or more than FLAT_MAXF
+// fragments: the finish runs the one-wave path over the datagram again).
+struct ReasmPlan {
+    uint32_t state, len, proto, pseudo, w0, w1, pad0, pad1;
+};
+constexpr uint32_t PLAN_GOOD = 0u, PLAN_BAD = 1u, PLAN_SLOW = 2u;
+constexpr uint32_t FLAT_MAXF = 64u;          // fragments a plan holds (one per lane)
+constexpr uint32_t FLAT_NP = 2u;             // fragment pairs a flat-grid wave gathers at once
 
 struct FragLds {
     uint32_t key[FRAG_MAX];   // offset | MF << 16 | dup << 24
@@ -102,8 +124,72 @@ struct FragLds {
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*p; }
 
+// One fragment's header.  IPv4 as pico_ipv4_process_in hands a fragment on (net_len,
+// transport_len = tot - net_len, frag); IPv6 as pico_ipv6_extension_headers does (the walk must
+// reach the transport behind a fragment header; transport_len = payload_len - (net_len - 40)).
+// key = offset | MF << 16; pr: IPv6, the walk's transport protocol.  False: the fragment is
+// malformed (its datagram is not reassembled).
+template <bool V6>
+__device__ __forceinline__ bool frag_parse(const FragArgs& p, const pico_csum_desc_dev& d, uint32_t& key, uint32_t& tl,
+                                           uint32_t& hl, uint32_t& pr) {
+    constexpr uint32_t HDR = V6 ? 40u : 20u;
+    key = tl = hl = pr = 0;
+    if (d.len < HDR || d.off > p.base_len || d.len > p.base_len - d.off) return false;
+    const uint8_t* h = p.base + d.off;
+    if constexpr (!V6) {
+        const uint32_t ihl = ld_u8(h) & 0x0Fu;
+        hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
+        tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
+        const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
+        key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u);
+        return hl + tl <= d.len;
+    } else {
+        const uint64_t w = ipv6_walk_packed(h, d.len);
+        const uint32_t om = (uint32_t)(w >> 32);
+        hl = ((uint32_t)w >> 8) & 0xFFFFu;
+        tl = ((((ld_u8(h + 4) << 8) | ld_u8(h + 5))) - (hl - 40u)) & 0xFFFFu;
+        key = (om & 0xFFF8u) | ((om & 1u) << 16);
+        pr = ((uint32_t)w >> 24) & 0xFFu;
+        return (int)(w & 0xFFu) - 1 == WALK_FRAG && hl + tl <= d.len;
+    }
+}
+
+// pico_transport_crc_check on the reassembled frame (ICMPv6: pico_icmp6_process_in): s = the
+// transport's word sum, word0 / word1 = its bytes 0..3 / 4..7 (little-endian)
+template <bool V6>
+__device__ __forceinline__ uint32_t reasm_verdict(uint32_t flags, uint32_t len, uint32_t proto, uint32_t pseudo,
+                                                  uint32_t s, uint32_t word0, uint32_t word1, uint32_t& l4) {
+    uint32_t v = V_ACCEPT;
+    l4 = 0;
+    if constexpr (!V6) {
+        if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
+            l4 = finalize(pseudo + s);
+            if (l4) v = V_L4_BAD;
+        }
+    } else {
+        const uint32_t module = proto & 0xFFu, b9 = proto >> 8;
+        uint32_t cp = module;
+        bool check = false;
+        if (module == 6u || module == 17u) {
+            if (!(flags & F_NXD)) cp = b9;                // pico_socket.c:1923 through the IPv4 cast
+            check = cp == 6u || (cp == 17u && len >= 8u && (word1 >> 16) != 0u);
+        } else if (module == 58u && len >= 1u) {
+            check = true;
+        }
+        if (check) {
+            l4 = finalize(pseudo + (cp << 8) + s);
+            const uint32_t type = word0 & 0xFFu;
+            const bool checked = module != 58u || (type >= 130u && type <= 137u) || type == 143u;
+            if (l4 && checked) v = V_L4_BAD;
+        }
+    }
+    return v;
+}
+
 // WPD waves per datagram (1 or 4; the launcher picks it from the batch size)
-template <bool V6, int WPD>
+// FIN: the flat grid's finish -- a datagram whose plan is GOOD or BAD gets its results from the
+// plan and the waves' partial sums; a SLOW one runs the whole path below.
+template <bool V6, int WPD, bool FIN = false>
 __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;          // PICO_SIZE_IP6HDR / PICO_SIZE_IP4HDR
     constexpr uint32_t NT = 64u * WPD;
@@ -111,6 +197,24 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t g = blockIdx.x;
     if (g >= p.n_dgram) return;                       // workgroup-uniform
+    if constexpr (FIN) {
+        const uint32_t state = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.plan[g].state);
+        if (state != PLAN_SLOW) {
+            if (wv == 0) {
+                const uint32_t sv = lane < p.S ? p.slot[(uint64_t)g * p.S + lane] : 0u;
+                const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(sv), 63);
+                if (lane == 0) {
+                    const ReasmPlan r = p.plan[g];
+                    uint32_t l4 = 0, v = V_MALFORMED;
+                    if (state == PLAN_GOOD) v = reasm_verdict<V6>(p.flags, r.len, r.proto, r.pseudo, sum, r.w0, r.w1, l4);
+                    if (p.o_len) p.o_len[g] = state == PLAN_GOOD ? r.len : 0u;
+                    if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
+                    if (p.verdict) p.verdict[g] = (uint8_t)v;
+                }
+            }
+            return;
+        }
+    }
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
     const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
@@ -121,33 +225,13 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     }
     __syncthreads();
 
-    // ---- 1. parse.  IPv4 as pico_ipv4_process_in hands a fragment on (net_len, transport_len =
-    //         tot - net_len, frag); IPv6 as pico_ipv6_extension_headers does (the walk must reach
-    //         the transport behind a fragment header; transport_len = payload_len - (net_len - 40))
+    // ---- 1. parse (frag_parse)
     if (!bad0) {
         for (uint32_t j = tid; j < cnt; j += NT) {
             const pico_csum_desc_dev d = p.frag[first + j];
-            uint32_t key = 0, tl = 0, hl = 0;
-            if (d.len < HDR || d.off > p.base_len || d.len > p.base_len - d.off) {
-                L.bad = 1u;
-            } else if constexpr (!V6) {
-                const uint8_t* h = p.base + d.off;
-                const uint32_t ihl = ld_u8(h) & 0x0Fu;
-                hl = 20u + (ihl > 5u ? 4u * (ihl - 5u) : 0u);
-                tl = (((ld_u8(h + 2) << 8) | ld_u8(h + 3)) - hl) & 0xFFFFu;
-                const uint32_t frag = (ld_u8(h + 6) << 8) | ld_u8(h + 7);
-                key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u);
-                if (hl + tl > d.len) L.bad = 1u;
-            } else {
-                const uint8_t* h = p.base + d.off;
-                const uint64_t w = ipv6_walk_packed(h, d.len);
-                const uint32_t om = (uint32_t)(w >> 32);
-                hl = ((uint32_t)w >> 8) & 0xFFFFu;
-                tl = ((((ld_u8(h + 4) << 8) | ld_u8(h + 5))) - (hl - 40u)) & 0xFFFFu;
-                key = (om & 0xFFF8u) | ((om & 1u) << 16);
-                L.pr[j] = (uint8_t)((uint32_t)w >> 24);
-                if ((int)(w & 0xFFu) - 1 != WALK_FRAG || hl + tl > d.len) L.bad = 1u;
-            }
+            uint32_t key, tl, hl, pr;
+            if (!frag_parse<V6>(p, d, key, tl, hl, pr)) L.bad = 1u;
+            if constexpr (V6) L.pr[j] = (uint8_t)pr;
             L.key[j] = key;
             L.tl[j] = tl;
             L.src[j] = reinterpret_cast<uint64_t>(p.base + d.off) + hl;
@@ -447,29 +531,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
                 word0 |= L.w0[k];
                 word1 |= L.w1[k];
             }
-            v = V_ACCEPT;
-            if constexpr (!V6) {
-                if (proto == 6u || (proto == 17u && len >= 8u && (word1 >> 16) != 0u)) {
-                    l4 = finalize(L.pseudo + s);
-                    if (l4) v = V_L4_BAD;
-                }
-            } else {
-                const uint32_t module = proto & 0xFFu, b9 = proto >> 8;
-                uint32_t cp = module;
-                bool check = false;
-                if (module == 6u || module == 17u) {
-                    if (!(p.flags & F_NXD)) cp = b9;          // pico_socket.c:1923 through the IPv4 cast
-                    check = cp == 6u || (cp == 17u && len >= 8u && (word1 >> 16) != 0u);
-                } else if (module == 58u && len >= 1u) {
-                    check = true;
-                }
-                if (check) {
-                    l4 = finalize(L.pseudo + (cp << 8) + s);
-                    const uint32_t type = word0 & 0xFFu;
-                    const bool checked = module != 58u || (type >= 130u && type <= 137u) || type == 143u;
-                    if (l4 && checked) v = V_L4_BAD;
-                }
-            }
+            v = reasm_verdict<V6>(p.flags, len, proto, L.pseudo, s, word0, word1, l4);
         }
         if (p.o_len) p.o_len[g] = bad ? 0u : len;
         if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
@@ -477,24 +539,433 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     }
 }
 
+// ---------------------------------------------------------------- flat grid
+//
+// Large batches: S one-wave workgroups per datagram (S ~ its fragment pairs), each gathering
+// fragment pairs s, s + S, ... of its datagram at their own offsets straight from their own
+// headers, so the dispatcher balances the gather over the whole batch instead of one wave walking
+// a whole datagram; wave s = 0 also plans the datagram (its fragments one per lane: dedup,
+// completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
+// (reassemble_kernel<V6, 1, true>) adds them.  A datagram with repeated offsets or more than
+// FLAT_MAXF fragments is gathered again there by the one-wave path (its flat-grid bytes may hold
+// a later arrival's copy; the region past the reassembled datagram is unspecified).
+
+// wave 0 of the datagram's slice: pico_fragments_check_complete on registers (lane j: fragment j)
+template <bool V6>
+__device__ __forceinline__ void plan_datagram(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, bool bad0,
+                                              uint8_t* t, uint32_t cap, uint32_t lane) {
+    constexpr uint32_t HDR = V6 ? 40u : 20u;
+    auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+    uint32_t state = PLAN_BAD, len = 0, proto = 0, pseudo = 0, w0 = 0, w1 = 0;
+    if (!bad0 && cnt > FLAT_MAXF) {
+        state = PLAN_SLOW;
+    } else if (!bad0) {
+        const bool in = lane < cnt;
+        uint32_t key = 0, tl = 0, hl = 0, pr = 0;
+        uint64_t off = 0;
+        bool ok = true;
+        if (in) {
+            const pico_csum_desc_dev d = p.frag[first + lane];
+            off = d.off;
+            ok = frag_parse<V6>(p, d, key, tl, hl, pr);
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+            const uint32_t o = key & 0xFFFFu;
+            uint32_t P = 0, rank = 0;                 // transport bytes / fragments below this offset
+            bool dup = false;                         // an earlier arrival has this offset
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t kk = rl(key, k) & 0xFFFFu, tk = rl(tl, k);
+                dup |= k < lane && kk == o;
+                P += kk < o ? tk : 0u;
+                rank += kk < o ? 1u : 0u;
+            }
+            if (__builtin_amdgcn_ballot_w64(in && dup) != 0) {
+                state = PLAN_SLOW;
+            } else {
+                // offsets distinct: rank = tree position.  Complete: offset == the transport bytes
+                // below it up to the first MF-clear fragment in tree order, which is the last
+                const bool mfc = in && !(key & (1u << 16));
+                const uint32_t re = 64u - rl(wave_scan_max(mfc ? 64u - rank : 0u), 63);
+                bool b = re >= cnt || re + 1u != cnt ||
+                         __builtin_amdgcn_ballot_w64(in && rank <= re && o != P) != 0;
+                if (!b) {
+                    const uint32_t le = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(mfc && rank == re));
+                    len = rl(P + tl, le);
+                    b = HDR + len > 0xFFFFu || len > cap;
+                }
+                if (!b) {
+                    // the first fragment's header (pico_fragments.c:332-338), its transport bytes
+                    // 0..7 and the pseudo header's address part (as in reassemble_kernel)
+                    const uint32_t f0 = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(in && o == 0u));
+                    const uint8_t* h0 =
+                        p.base + (((uint64_t)rl((uint32_t)(off >> 32), f0) << 32) | rl((uint32_t)off, f0));
+                    const uint32_t hl0 = rl(hl, f0), tl0 = rl(tl, f0);
+                    const uint32_t hb = lane < HDR ? ld_u8(h0 + lane) : 0u;
+                    if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hb;
+                    const uint32_t tb8 = lane < 8u && lane < tl0 ? ld_u8(h0 + hl0 + lane) : 0u;
+                    w0 = rl(tb8, 0) | (rl(tb8, 1) << 8) | (rl(tb8, 2) << 16) | (rl(tb8, 3) << 24);
+                    w1 = rl(tb8, 4) | (rl(tb8, 5) << 8) | (rl(tb8, 6) << 16) | (rl(tb8, 7) << 24);
+                    if constexpr (!V6) {
+                        proto = (uint32_t)__shfl((int)hb, 9);
+                        const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                        pseudo = rl(group_sum<64>(pw), 63) + (proto << 8) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                    } else {
+                        // the module: the walk's protocol of the latest arrival (every fragment is kept)
+                        proto = rl(pr, cnt - 1u) | ((uint32_t)__shfl((int)hb, 9) << 8);
+                        const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                        pseudo = rl(group_sum<64>(pw), 63) + (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) +
+                                 (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                    }
+                    state = PLAN_GOOD;
+                }
+            }
+        }
+    }
+    if (lane == 0) p.plan[g] = ReasmPlan{state, len, proto, pseudo, w0, w1, 0u, 0u};
+}
+
+// One or two fragments' payloads gathered into the transport at tb (fragment A: transport bytes
+// [ata, ata + ta) from address srcA; B likewise when nb_on), in 16-byte units on the output's lines
+// as reassemble_kernel phase 3 (its unit arithmetic and store sequence), split into prep / issue /
+// process so that two pairs' loads are in flight together.  Both payloads within 1 GiB of each
+// other (the window; the caller splits a pair otherwise).
+struct PairStep {
+    uint64_t wlo;
+    uint32_t wsz, va, vb, na, nt, oa, ob, ata, atb, ta, tbb;
+    bool nb_on;
+};
+
+__device__ __forceinline__ PairStep pair_prep(uint64_t tb, uint64_t srcA, uint32_t ata, uint32_t ta, bool nb_on,
+                                              uint64_t srcB, uint32_t atb, uint32_t tbl) {
+    PairStep q;
+    q.nb_on = nb_on;
+    q.oa = (uint32_t)((tb + ata) & 15u);
+    q.ob = nb_on ? (uint32_t)((tb + atb) & 15u) : 0u;
+    const uint64_t sa = srcA - q.oa, sb = nb_on ? srcB - q.ob : sa;
+    q.na = (q.oa + ta + 15u) >> 4;
+    q.nt = q.na + (nb_on ? (q.ob + tbl + 15u) >> 4 : 0u);
+    q.wlo = (nb_on ? min64s(sa, sb) : sa) & ~15ull;
+    const uint64_t whi = nb_on ? max64s(sa + q.oa + ta, sb + q.ob + tbl) : sa + q.oa + ta;
+    q.wsz = (uint32_t)(((whi + 15u) & ~15ull) - q.wlo + 16u);
+    q.va = (uint32_t)(sa - q.wlo);
+    q.vb = (uint32_t)(sb - q.wlo);
+    q.ata = ata;
+    q.atb = atb;
+    q.ta = ta;
+    q.tbb = nb_on ? tbl : 0u;
+    return q;
+}
+
+template <int U>
+__device__ __forceinline__ void pair_issue(const PairStep& q, uint32_t lane, uint32_t u0, uint4 (&c0)[U]) {
+    const Window win = make_window(q.wlo, q.wsz);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint32_t x = u0 + 64u * k + lane;
+        const bool inb = x >= q.na;
+        const uint32_t u = inb ? x - q.na : x, v = inb ? q.vb : q.va;
+        c0[k] = load_win<true>(win, x < q.nt ? v + 16u * u : WIN_OOB);
+    }
+}
+
+template <int U>
+__device__ __forceinline__ uint32_t pair_process(const PairStep& q, const Window& ow, uint32_t lane, uint32_t u0,
+                                                 const uint4 (&c0)[U], uint32_t acc) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint32_t x = u0 + 64u * k + lane;
+        const bool ok = x < q.nt;
+        const bool inb = x >= q.na;
+        const uint32_t u = inb ? x - q.na : x;
+        const uint32_t tl = inb ? q.tbb : q.ta, at = inb ? q.atb : q.ata, o = inb ? q.ob : q.oa;
+        uint32_t xw[4] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w};
+        const uint32_t lo = ok && u == 0u ? o : 0u, hi = ok ? min(16u, o + tl - 16u * u) : 0u;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t kb = 4u * w < lo ? 0u : min((uint32_t)max((int)hi - 4 * w, 0), 4u);
+            xw[w] &= (uint32_t)(0xFFFFFFFFull >> (32u - 8u * kb));
+        }
+        const uint32_t so = at + 16u * u - o;
+        const bool whole = lo == 0u && hi == 16u;
+        const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
+        const uint32_t nr = hi > lo ? hi & 3u : 0u;
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
+                                               (int)(whole ? so : WIN_OOB), 0, 0);
+        const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
+            (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc,
+                                              (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, 0);
+        const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc,
+                                              (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
+                                             (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, 0);
+        acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));
+    }
+    return acc;
+}
+
+__device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window& ow, uint32_t lane, uint32_t acc) {
+    for (uint32_t u0 = 0; u0 < q.nt; u0 += 192u) {
+        uint4 c0[3];
+        pair_issue<3>(q, lane, u0, c0);
+        acc = pair_process<3>(q, ow, lane, u0, c0, acc);
+    }
+    return acc;
+}
+
+// The flat grid: S one-wave workgroups per datagram; wave s takes fragments FPI s, ... in groups
+// of FPI = 2 FLAT_NP (two pairs' loads in flight).  c3_reasm (profiles/r05/ab_reasm_flat.txt):
+// 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
+// descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
+// or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
+// 115.7 at 4 (105 VGPRs).  IPv6 measured 175.7 us against 133.3 us (the walk): not flat by default.
+template <bool V6>
+__global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
+    constexpr uint32_t HDR = V6 ? 40u : 20u;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t S = p.S;
+    const uint32_t g = blockIdx.x / S, s = blockIdx.x - g * S;
+    if (g >= p.n_dgram) return;
+    const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
+    const pico_csum_desc_dev od = p.odesc[g];
+    const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
+                      (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < HDR;
+    uint8_t* t = p.out + od.off + HDR;
+    const uint32_t cap = od.len - HDR;
+    if (s == 0) plan_datagram<V6>(p, g, first, cnt, bad0, t, cap, lane);
+    uint32_t acc = 0;
+    if (!bad0 && cnt <= FLAT_MAXF) {
+        const uint64_t tb = reinterpret_cast<uintptr_t>(t);
+        const Window ow = make_window(tb, cap);
+        auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+        constexpr uint32_t NP = FLAT_NP, FPI = 2u * NP;          // pairs / fragments per iteration
+        for (uint32_t j0 = FPI * s; j0 < cnt; j0 += FPI * S) {
+            // lanes 0..FPI-1 read fragments j0, ..., j0 + FPI - 1; a fragment is gathered when it
+            // parses and the output region holds it (repeated offsets too: SLOW plans are gathered
+            // again); the NP pairs' loads are in flight at once
+            const uint32_t j = j0 + lane;
+            uint32_t key = 0, tl = 0, hl = 0, pr = 0;
+            uint64_t src = 0;
+            bool ok = false;
+            if (lane < FPI && j < cnt) {
+                const pico_csum_desc_dev d = p.frag[first + j];
+                ok = frag_parse<V6>(p, d, key, tl, hl, pr) && (key & 0xFFFFu) + tl <= cap;
+                src = reinterpret_cast<uint64_t>(p.base + d.off) + hl;
+            }
+            const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+            PairStep ps[NP];
+            bool one = true;                  // every pair in one step of 3 x 64 units
+#pragma unroll
+            for (uint32_t q = 0; q < NP; ++q) {
+                const uint32_t la = 2u * q, lb = la + 1u;
+                const uint64_t sA = ((uint64_t)rl((uint32_t)(src >> 32), la) << 32) | rl((uint32_t)src, la);
+                const uint64_t sB = ((uint64_t)rl((uint32_t)(src >> 32), lb) << 32) | rl((uint32_t)src, lb);
+                const uint32_t aA = rl(key, la) & 0xFFFFu, aB = rl(key, lb) & 0xFFFFu, tA = rl(tl, la), tB = rl(tl, lb);
+                const bool vA = (m >> la) & 1u, vB = (m >> lb) & 1u;
+                if (vA && vB && max64s(sA + tA, sB + tB) - min64s(sA, sB) < (1ull << 30)) {
+                    ps[q] = pair_prep(tb, sA, aA, tA, true, sB, aB, tB);
+                } else if (vA) {
+                    ps[q] = pair_prep(tb, sA, aA, tA, false, 0, 0, 0);
+                    if (vB) acc = pair_gather(pair_prep(tb, sB, aB, tB, false, 0, 0, 0), ow, lane, acc);   // (far apart)
+                } else if (vB) {
+                    ps[q] = pair_prep(tb, sB, aB, tB, false, 0, 0, 0);
+                } else {
+                    ps[q] = pair_prep(tb, 0, 0, 0, false, 0, 0, 0);
+                    ps[q].nt = 0;
+                }
+                one = one && ps[q].nt <= 192u;
+            }
+            if (one) {
+                uint4 c[NP][3];
+#pragma unroll
+                for (uint32_t q = 0; q < NP; ++q) pair_issue<3>(ps[q], lane, 0u, c[q]);
+#pragma unroll
+                for (uint32_t q = 0; q < NP; ++q) acc = pair_process<3>(ps[q], ow, lane, 0u, c[q], acc);
+            } else {
+#pragma unroll
+                for (uint32_t q = 0; q < NP; ++q) acc = pair_gather(ps[q], ow, lane, acc);
+            }
+        }
+    }
+    acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
+    if (lane == 0) p.slot[blockIdx.x] = acc;
+}
+
+// Scratch of the flat grid (plans and partial sums, n_dgram x (32 + 4 S) bytes), never allocated
+// per call (per-call hipMallocAsync / hipFreeAsync -- alloc / free nodes in a captured graph --
+// cost c3_reasm ~23 us a call, an event record per call ~24 us: idle device time):
+//  * eager calls: one buffer per calling thread, device and stream, kept across calls and grown
+//    as needed -- calls on one stream are ordered by it, so a buffer is never in use by two calls
+//    at once.  Up to SCR_SLOTS streams per thread; the least recently used is freed (hipFree waits
+//    for the device) when another comes;
+//  * calls captured into a graph: one buffer per capture and captured stream (the captured calls
+//    on one stream are a chain in the graph), allocated outside the capture's rules and owned by
+//    the graph (a user object; freed by the next eager call after the graph is destroyed).  Two
+//    executable instances of one graph must not run concurrently.
+struct ReasmScratch {
+    void* p;
+    size_t n;
+    hipStream_t stream;
+    int dev;
+    uint64_t stamp;
+};
+constexpr int SCR_SLOTS = 8;
+thread_local ReasmScratch t_scratch[SCR_SLOTS];
+thread_local uint64_t t_scratch_clock;
+
+struct CapScratch {
+    unsigned long long id;
+    hipStream_t stream;
+    void* p;
+    size_t n;
+};
+thread_local CapScratch t_cap[SCR_SLOTS];
+thread_local int t_cap_next;
+
+std::mutex g_garbage_mu;
+std::vector<void*> g_garbage;                    // buffers of destroyed graphs, freed by eager calls
+
+void scratch_release(void* p) {                   // graph destructor: no HIP calls allowed here
+    std::lock_guard<std::mutex> lk(g_garbage_mu);
+    g_garbage.push_back(p);
+}
+
+int capture_scratch(hipStream_t s, size_t need, void** out) {
+    hipStreamCaptureStatus cs;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    hipError_t e = hipStreamGetCaptureInfo_v2(s, &cs, &id, &graph, &deps, &ndeps);
+    if (e != hipSuccess) return (int)e;
+    for (int i = 0; i < SCR_SLOTS; ++i)
+        if (t_cap[i].p && t_cap[i].id == id && t_cap[i].stream == s && t_cap[i].n >= need) {
+            *out = t_cap[i].p;
+            return 0;
+        }
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    if ((e = hipThreadExchangeStreamCaptureMode(&mode)) != hipSuccess) return (int)e;
+    void* p = nullptr;
+    e = hipMalloc(&p, need);
+    hipStreamCaptureMode back = mode;
+    (void)hipThreadExchangeStreamCaptureMode(&back);
+    if (e != hipSuccess) return (int)e;
+    hipUserObject_t obj;
+    if ((e = hipUserObjectCreate(&obj, p, scratch_release, 1, hipUserObjectNoDestructorSync)) != hipSuccess) {
+        scratch_release(p);
+        return (int)e;
+    }
+    if ((e = hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove)) != hipSuccess) {
+        (void)hipUserObjectRelease(obj, 1);
+        return (int)e;
+    }
+    t_cap[t_cap_next] = CapScratch{id, s, p, need};
+    t_cap_next = (t_cap_next + 1) % SCR_SLOTS;
+    *out = p;
+    return 0;
+}
+
+int reasm_scratch(hipStream_t s, size_t need, void** out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing(s, &cs);
+    if (e != hipSuccess) return (int)e;
+    if (cs == hipStreamCaptureStatusActive) return capture_scratch(s, need, out);
+    if (cs != hipStreamCaptureStatusNone) return (int)hipErrorStreamCaptureInvalidated;
+    {
+        std::vector<void*> g;
+        {
+            std::lock_guard<std::mutex> lk(g_garbage_mu);
+            g.swap(g_garbage);
+        }
+        for (void* p : g) (void)hipFree(p);
+    }
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return (int)e;
+    ReasmScratch* c = nullptr;
+    for (int i = 0; i < SCR_SLOTS && !c; ++i)
+        if (t_scratch[i].p && t_scratch[i].stream == s && t_scratch[i].dev == dev) c = &t_scratch[i];
+    if (!c) {                                        // an empty slot, else the least recently used
+        c = &t_scratch[0];
+        for (int i = 0; i < SCR_SLOTS; ++i) {
+            if (!t_scratch[i].p) {
+                c = &t_scratch[i];
+                break;
+            }
+            if (t_scratch[i].stamp < c->stamp) c = &t_scratch[i];
+        }
+    }
+    if (c->p && (c->stream != s || c->dev != dev || c->n < need)) {
+        if (c->dev != dev) (void)hipSetDevice(c->dev);
+        (void)hipFree(c->p);
+        if (c->dev != dev) (void)hipSetDevice(dev);
+        c->p = nullptr;
+    }
+    if (!c->p) {
+        const size_t n = need + need / 2u;
+        if ((e = hipMalloc(&c->p, n)) != hipSuccess) {
+            c->p = nullptr;
+            return (int)e;
+        }
+        c->n = n;
+        c->stream = s;
+        c->dev = dev;
+    }
+    c->stamp = ++t_scratch_clock;
+    *out = c->p;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
 
 // v6: 0 IPv4, 1 IPv6; flags: F_NXD (IPv6)
+// flat_min: the flat grid from this many datagrams on (0 = REASM_FLAT_MIN, UINT32_MAX = never)
 int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, const void* frag, uint32_t n_frag,
                                 const uint32_t* groups, uint32_t n_dgram, void* out, uint64_t out_len, const void* out_desc,
-                                uint32_t* o_len, uint16_t* o_l4, uint8_t* verdict, uint32_t flags, void* stream) {
+                                uint32_t* o_len, uint16_t* o_l4, uint8_t* verdict, uint32_t flags, uint32_t flat_min,
+                                void* stream) {
     if (n_dgram == 0) return (int)hipSuccess;
     FragArgs a{static_cast<const uint8_t*>(base), flags, base_len, static_cast<const pico_csum_desc_dev*>(frag),
                groups, n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
-               static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict};
+               static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict, nullptr, nullptr, 0u};
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+#ifndef REASM_FLAT_MIN
+#define REASM_FLAT_MIN 1024u
+#endif
+    // flat grid: IPv4 from REASM_FLAT_MIN datagrams on (IPv6, whose extension-header walk every
+    // flat wave would repeat per fragment ahead of its loads, measured slower: 175.7 vs 133.3 us)
+    const uint32_t fmin = flat_min ? flat_min : (v6 ? UINT32_MAX : REASM_FLAT_MIN);
+    if (n_dgram >= fmin) {
+        // S waves per datagram, FPI fragments each on average
+        const uint64_t its = ((uint64_t)n_frag + 2u * FLAT_NP - 1u) / (2u * FLAT_NP);
+        uint32_t S = (uint32_t)((its + n_dgram - 1u) / n_dgram);
+        S = S < 1u ? 1u : (S > 32u ? 32u : S);
+        const size_t plan_b = (size_t)n_dgram * sizeof(ReasmPlan), need = plan_b + (size_t)n_dgram * S * 4u;
+        void* scratch = nullptr;
+        int e = reasm_scratch(s, need, &scratch);
+        if (e) return e;
+        a.plan = static_cast<ReasmPlan*>(scratch);
+        a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
+        a.S = S;
+        const dim3 fg((unsigned)((uint64_t)n_dgram * S)), fb(64);
+        if (v6) {
+            hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
+            hipLaunchKernelGGL((reassemble_kernel<true, 1, true>), dim3(n_dgram), fb, 0, s, a);
+        } else {
+            hipLaunchKernelGGL((reasm_flat_kernel<false>), fg, fb, 0, s, a);
+            hipLaunchKernelGGL((reassemble_kernel<false, 1, true>), dim3(n_dgram), fb, 0, s, a);
+        }
+        return (int)hipGetLastError();
+    }
     // waves per datagram: 4 each while the batch is small, 1 each once the batch fills the chip's
     // one-wave workgroup slots (16 per CU, LDS-bound): c3_reasm (4096 datagrams) 145.6 vs 149.0 us
     // at 4 waves, 2 waves 165.0 us (2560 slots: a partial second round), ab_frag_wpd.txt
     const int wpd = n_dgram >= 3072u ? 1 : 4;
     const dim3 grid(n_dgram), block(64 * wpd);
-    const hipStream_t s = static_cast<hipStream_t>(stream);
     if (wpd == 1) {
         if (v6) hipLaunchKernelGGL((reassemble_kernel<true, 1>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((reassemble_kernel<false, 1>), grid, block, 0, s, a);

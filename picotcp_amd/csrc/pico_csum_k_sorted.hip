@@ -1474,6 +1474,7 @@ __device__ __forceinline__ void uniform_stream_range(const UniArgs& p, StreamLds
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
         __builtin_amdgcn_wave_barrier();
+        if (st == 0u) STAMP(1);                        // (diagnostic build: the first step's data in)
         uint32_t loc[SCPL];
         uint32_t t = 0;
 #pragma unroll
@@ -1514,7 +1515,10 @@ __global__ __launch_bounds__(64 * WPB, WPS) void csum_uniform_stream_kernel(UniA
     __shared__ StreamLds lds_all[WPB];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t f0 = ((uint64_t)blockIdx.x * WPB + wv) * p.fpw;
+    STAMP(0);
     if (f0 < p.n) uniform_stream_range(p, lds_all[wv], lane, f0);
+    STAMP(2);
+    STAMP(3);
 }
 #endif
 

@@ -19,6 +19,16 @@ from tests.test_gpu_parity import to_dev
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["auto", "flat"])
+def reasm_path(request):
+    """Every case through the launcher's own choice (the flat grid for IPv4 batches of 1024
+    datagrams or more, else one workgroup per datagram) and through the flat grid forced
+    (pico_csum_set_reasm_flat(1))."""
+    batch.set_reasm_flat(1 if request.param == "flat" else 0)
+    yield request.param
+    batch.set_reasm_flat(0)
+
+
 def gpu_reassemble(buf, d, grp, od, out_size, v6=False, nx=False):
     out = torch.zeros(out_size, dtype=torch.uint8, device="cuda:0")
     args = (to_dev(buf), to_dev(d.view(np.uint8)), d.size,
@@ -167,9 +177,10 @@ def test_ipv6_reassembly_limits():
 
 @pytest.mark.parametrize("v6", [False, True])
 @pytest.mark.parametrize("n", [1600, 3200])
-def test_batch_shapes(n, v6):
-    """Batches below and above the launcher's switch to one wave per datagram (3072), with
-    datagrams of more than 64 fragments per wave (the gather's metadata blocks)."""
+def test_batch_shapes(n, v6, reasm_path):
+    """Batches below and above the launcher's switch to one wave per datagram (3072) -- both on
+    the flat grid (>= 1024 datagrams) unless forced off -- with datagrams of more than 64 fragments
+    per wave (the gather's metadata blocks; the flat grid's SLOW plans)."""
     rng = np.random.default_rng(n + v6)
     lens = rng.integers(0, 3000, n)
     lens[rng.integers(0, n, 24)] = rng.integers(8200, 9000, 24)   # 129-141 fragments of 64 B
@@ -182,6 +193,10 @@ def test_batch_shapes(n, v6):
     od, size = layout(lens, shift=4, hdr=40 if v6 else 20)
     wl, wv = check(buf, d, grp, od, size, v6=v6)
     assert (wv != 8).all() and (wl == np.array(lens)).all()
+    if reasm_path == "auto":                             # and one workgroup per datagram
+        batch.set_reasm_flat(2)
+        wl, wv = check(buf, d, grp, od, size, v6=v6)
+        assert (wv != 8).all() and (wl == np.array(lens)).all()
 
 
 @pytest.mark.parametrize("v6", [False, True])
@@ -203,3 +218,81 @@ def test_unit_grid(payload, shift, v6):
     wl, wv = check(buf, d, grp, od, size, v6=v6)
     ok = wv != 8
     assert ok.mean() > 0.9 and (wl[ok] == np.array(lens)[ok]).all()
+
+
+def _flat_case(n, seed):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 6000, n).tolist()
+    buf, off, flen, grp = synth.ipv4_fragments(lens, seed=seed, proto=6, frag_payload=552)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=4)
+    out_o = np.zeros(size, np.uint8)
+    want = O.ipv4_reassemble(buf, d, grp, out_o, od)
+    dev = (to_dev(buf), to_dev(d.view(np.uint8)), d.size,
+           to_dev(np.ascontiguousarray(grp, np.uint32).reshape(-1).view(np.int32)), to_dev(od.view(np.uint8)))
+    return dev, od, size, want, out_o
+
+
+def _check_flat(res, out, od, want, out_o):
+    ol, l4, v = (x.cpu().numpy() for x in res)
+    np.testing.assert_array_equal(v, want[2])
+    np.testing.assert_array_equal(ol.view(np.uint32), want[0])
+    np.testing.assert_array_equal(l4.view(np.uint16), want[1])
+    o_g = out.cpu().numpy()
+    for g in np.flatnonzero(want[2] != 8):
+        o, n = int(od["off"][g]), 20 + int(want[0][g])
+        np.testing.assert_array_equal(o_g[o:o + n], out_o[o:o + n], err_msg=f"datagram {g}")
+
+
+def test_flat_grid_graph_capture():
+    """The flat grid captured into a graph (its scratch then owned by the graph): replays match the
+    oracle, and eager calls afterwards too (after the graph is destroyed as well)."""
+    (b, d, nf, grp, od_d), od, size, want, out_o = _flat_case(1500, 71)
+    outs = [torch.zeros(size, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    res = [batch.ipv4_reassemble_batch(b, d, nf, grp, o, od_d) for o in outs]   # warm (eager)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for o, r in zip(outs, res):
+                batch.ipv4_reassemble_batch(b, d, nf, grp, o, od_d, stream=s, results=r)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        for o, r in zip(outs, res):
+            o.zero_()
+            for x in r:
+                x.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for o, r in zip(outs, res):
+            _check_flat(r, o, od, want, out_o)
+    o = torch.zeros(size, dtype=torch.uint8, device="cuda:0")
+    r = batch.ipv4_reassemble_batch(b, d, nf, grp, o, od_d, stream=s)
+    torch.cuda.synchronize()
+    _check_flat(r, o, od, want, out_o)
+    del g                                                # the graph's scratch freed by the next call
+    torch.cuda.synchronize()
+    o.zero_()
+    r = batch.ipv4_reassemble_batch(b, d, nf, grp, o, od_d)
+    torch.cuda.synchronize()
+    _check_flat(r, o, od, want, out_o)
+
+
+def test_flat_grid_streams_and_sizes():
+    """Calls alternating between two streams (each its own scratch), a larger batch after a smaller
+    one on the same stream (the scratch grows), then the smaller again -- all against the oracle."""
+    small = _flat_case(1100, 73)
+    large = _flat_case(3000, 74)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    runs = []
+    for case, st in ((small, s1), (small, s2), (large, s1), (large, s2), (small, s1)):
+        (b, d, nf, grp, od_d), od, size, want, out_o = case
+        o = torch.zeros(size, dtype=torch.uint8, device="cuda:0")
+        st.wait_stream(torch.cuda.current_stream())
+        r = batch.ipv4_reassemble_batch(b, d, nf, grp, o, od_d, stream=st)
+        runs.append((r, o, case))
+    torch.cuda.synchronize()
+    for r, o, (_, od, size, want, out_o) in runs:
+        _check_flat(r, o, od, want, out_o)

@@ -27,7 +27,7 @@ from picotcp_amd import _lib, batch, synth  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c2tx", "c2v6", "c2raw"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c2tx", "c2v6", "c2raw", "c1stream", "c4stream"])
     ap.add_argument("--n", type=int, default=262144)
     ap.add_argument("--rotate", type=int, default=12)
     ap.add_argument("--wpb", type=int, default=4, help="waves per workgroup of the kernel")
@@ -37,9 +37,18 @@ def main():
     lib.pico_csum_diag_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     dev = torch.device("cuda:0")
     n = a.n
+    uni = a.config in ("c1stream", "c4stream")
+    if a.config == "c4stream":
+        n = 1 << 22
     lens = synth.imix_lengths(n, 3) + (20 if a.config == "c2v6" else 0)
     sets = []
-    for r in range(a.rotate):
+    if uni:           # uniform 1500 B rings on the stream waves (stamps: entry, first step in, end)
+        batch.set_uniform_stream(1, 0)
+    for r in range(a.rotate if not uni else (a.rotate if n <= 262144 else 2)):
+        if uni:
+            b = torch.randint(0, 256, (n * 1500,), dtype=torch.uint8, device=dev)
+            sets.append((b, None))
+            continue
         if a.config == "c2v6":
             buf, net, avail, seeds = synth.ipv6_batch(lens.astype(np.uint32), seed=10 + r, proto=6, eth=True)
             d = batch.desc_to_device(batch.make_desc(net, avail, seeds), dev)
@@ -55,8 +64,10 @@ def main():
     st = torch.zeros(4 * waves, dtype=torch.int64, device=dev)
 
     def launch(i):
-        b, d = sets[i % a.rotate]
-        if a.config == "c2v6":
+        b, d = sets[i % len(sets)]
+        if uni:
+            batch.checksum_uniform(b, 1500, 1500, n)
+        elif a.config == "c2v6":
             batch.ipv6_checksum_batch(b, d, n)
         elif a.config == "c2raw":
             batch.checksum_batch(b, d, n)
