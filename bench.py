@@ -132,6 +132,8 @@ def parse():
     p.add_argument("--shape", default="", help="G,CPL,FPW,U,NT launch override (sweeps)")
     p.add_argument("--stream", default="", help="MODE,FPW the uniform rings' stream waves "
                                                   "(pico_csum_set_uniform_stream: 1 on, 255 off; frames per wave)")
+    p.add_argument("--reasm-flat", type=int, default=0,
+                   help="reassembly grid (pico_csum_set_reasm_flat: 0 auto, 1 flat, 2 one workgroup per datagram)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch the K timed steps one by one from Python instead of replaying them as one "
                         "captured HIP graph")
@@ -706,6 +708,8 @@ def main():
         batch.set_launch_override(*[int(x) for x in a.shape.split(",")])
     if a.stream:
         batch.set_uniform_stream(*[int(x) for x in a.stream.split(",")])
+    if a.reasm_flat:
+        batch.set_reasm_flat(a.reasm_flat)
     cfg = CONFIGS[a.config]
 
     # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)

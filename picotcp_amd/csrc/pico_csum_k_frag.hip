@@ -144,7 +144,22 @@ __device__ __forceinline__ bool frag_parse(const FragArgs& p, const pico_csum_de
         key = ((frag & 0x1FFFu) << 3) | ((frag & 0x2000u) ? 1u << 16 : 0u);
         return hl + tl <= d.len;
     } else {
-        const uint64_t w = ipv6_walk_packed(h, d.len);
+        // the common chain -- the fixed header, a fragment header, the transport -- from loads
+        // issued together (the walk's are a dependent chain); it is exactly what the walk returns
+        // for that chain (net_len 48, M with a payload length not a multiple of 8 dropped)
+        uint64_t w;
+        const uint32_t h6 = ld_u8(h + 6);
+        if (d.len > 43u) {
+            const uint32_t h40 = ld_u8(h + 40), om = (ld_u8(h + 42) << 8) | ld_u8(h + 43);
+            const uint32_t plen = (ld_u8(h + 4) << 8) | ld_u8(h + 5);
+            if (h6 == 44u && (h40 == 6u || h40 == 17u || h40 == 58u))
+                w = ((om & 1u) && (plen & 7u)) ? (uint64_t)(WALK_DROP + 1)
+                                               : ((uint64_t)om << 32) | (uint32_t)(WALK_FRAG + 1) | (48u << 8) | (h40 << 24);
+            else
+                w = ipv6_walk_packed(h, d.len);
+        } else {
+            w = ipv6_walk_packed(h, d.len);
+        }
         const uint32_t om = (uint32_t)(w >> 32);
         hl = ((uint32_t)w >> 8) & 0xFFFFu;
         tl = ((((ld_u8(h + 4) << 8) | ld_u8(h + 5))) - (hl - 40u)) & 0xFFFFu;
@@ -721,7 +736,7 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
 // 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
 // descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
 // or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
-// 115.7 at 4 (105 VGPRs).  IPv6 measured 175.7 us against 133.3 us (the walk): not flat by default.
+// 115.7 at 4 (105 VGPRs).  IPv6 measured 153.0 us against 132.2 us: not flat by default.
 template <bool V6>
 __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
@@ -936,8 +951,9 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
 #ifndef REASM_FLAT_MIN
 #define REASM_FLAT_MIN 1024u
 #endif
-    // flat grid: IPv4 from REASM_FLAT_MIN datagrams on (IPv6, whose extension-header walk every
-    // flat wave would repeat per fragment ahead of its loads, measured slower: 175.7 vs 133.3 us)
+    // flat grid: IPv4 from REASM_FLAT_MIN datagrams on (IPv6 measured slower on it: c3_reasm6 153.0
+    // vs 132.2 us with the common-chain parse, 175.7 vs 133.3 us before it; the walk's code in
+    // the kernel costs 1 % of that, ab_reasm_flat.txt)
     const uint32_t fmin = flat_min ? flat_min : (v6 ? UINT32_MAX : REASM_FLAT_MIN);
     if (n_dgram >= fmin) {
         // S waves per datagram, FPI fragments each on average
