@@ -8,7 +8,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
-TAG=r05z
+TAG=${TAG:-r05z}
 ALL="c1 c2 c2slot c2tx c2tx_nw c2nat c2v6 c2eth c2ethmix c3 c3_64k c3_frag c3_reasm c3_reasm6 c4"
 mkdir -p $O
 cd $R

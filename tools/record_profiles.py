@@ -20,23 +20,35 @@ import sys
 CFGS = ("c1", "c2", "c2slot", "c2ethmix", "c2tx", "c2tx_nw", "c2nat", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3", "c3_64k", "c3_frag", "c4")
 
 
-def timed_kernel_rows(path):
-    """Rows of the timed kernel (the checksum kernel with the most dispatches)."""
-    rows = list(csv.DictReader(open(path)))
-    names = {}
-    for x in rows:
-        if "csum" in x["Kernel_Name"] or "reassemble" in x["Kernel_Name"]:
-            names[x["Kernel_Name"]] = names.get(x["Kernel_Name"], 0) + 1
-    kern = max(names, key=names.get)
-    return kern, [x for x in rows if x["Kernel_Name"] == kern]
+PRODUCT = ("csum", "reassemble", "reasm_")        # the library's kernels
+
+
+def product(name):
+    return any(k in name for k in PRODUCT)
+
+
+def step_kernels(counts):
+    """The kernels of one step: the product kernels with the most dispatches (a step of the IPv4
+    reassembly is two launches, the flat gather and its finish, dispatched equally often)."""
+    top = max(counts.values())
+    return sorted(k for k, v in counts.items() if v == top)
 
 
 def counter_medians(path):
-    kern, rows = timed_kernel_rows(path)
+    """Per counter, the sum over the step's kernels of each kernel's median over its dispatches."""
+    rows = [x for x in csv.DictReader(open(path)) if product(x["Kernel_Name"])]
+    disp = {}
+    for x in rows:
+        disp.setdefault(x["Kernel_Name"], set()).add(x.get("Dispatch_Id", x.get("Correlation_Id")))
+    kerns = step_kernels({k: len(v) for k, v in disp.items()})
     by = {}
     for x in rows:
-        by.setdefault(x["Counter_Name"], []).append(float(x["Counter_Value"]))
-    return kern, {k: statistics.median(v) for k, v in by.items()}
+        if x["Kernel_Name"] in kerns:
+            by.setdefault((x["Kernel_Name"], x["Counter_Name"]), []).append(float(x["Counter_Value"]))
+    med = {}
+    for (k, c), v in by.items():
+        med[c] = med.get(c, 0.0) + statistics.median(v)
+    return " + ".join(kerns), med
 
 
 def bench_line(path):
@@ -60,23 +72,29 @@ def timed_trace(src, tcfg, tag, bench, dst):
         return None
     shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{tcfg}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
-    rows = [r for r in rows if "csum" in r["Name"] or "reassemble" in r["Name"]]
+    rows = [r for r in rows if product(r["Name"])]
     tr = os.path.join(d, "run_kernel_trace.csv")
     same = bench_line(os.path.join(src, f"prof_{tcfg}_{tag}.log"))
     ref = same or bench
     if not (rows and os.path.exists(tr) and ref):
         return None
-    # the timed region: the last `steps` dispatches of the timed kernel (the stats file's average
-    # also holds the setup and verification launches of the same kernel)
-    top = max(rows, key=lambda r: int(r["Calls"]))["Name"]
-    ts = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]))
-                for x in csv.DictReader(open(tr)) if x["Kernel_Name"] == top)
-    last = ts[-ref["steps"]:]
-    trace_us = sum(e - b for b, e in last) / len(last) / 1e3
-    bracket_us = (last[-1][1] - last[0][0]) / len(last) / 1e3
+    # the timed region: the last `steps` dispatches of the step's kernels (the stats file's average
+    # also holds the setup and verification launches); a step of several kernels is their sum
+    tops = step_kernels({r["Name"]: int(r["Calls"]) for r in rows})
+    trace = [x for x in csv.DictReader(open(tr)) if x["Kernel_Name"] in tops]
+    trace_us, firsts, ends, n_ts = 0.0, [], [], 0
+    for k in tops:
+        ts = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in trace if x["Kernel_Name"] == k)
+        last = ts[-ref["steps"]:]
+        trace_us += sum(e - b for b, e in last) / len(last) / 1e3
+        firsts.append(last[0][0])
+        ends.append(last[-1][1])
+        n_ts = len(ts)
+    bracket_us = (max(ends) - min(firsts)) / len(last) / 1e3
     algo = ref["roofline"]["algorithmic_bytes_per_launch"]
     peak = ref["roofline"]["peak"]
-    out = {"kernel": top, "timed_dispatches": len(last), "dispatches_total": len(ts),
+    top = " + ".join(tops)
+    out = {"kernel": top, "timed_dispatches": len(last), "dispatches_total": n_ts,
            "trace_avg_us": round(trace_us, 3), "trace_bracket_us": round(bracket_us, 3),
            "frac_from_trace": round(algo / (trace_us * 1e3) / peak, 4),
            "frac_from_trace_bracket": round(algo / (bracket_us * 1e3) / peak, 4),
