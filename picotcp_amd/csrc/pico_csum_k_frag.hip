@@ -12,7 +12,7 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// IPv4 batches of >= 1024 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
+// Batches of >= 1024 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
 // the gather spread over ~one wave per four fragments, the plan and the sums brought together
 // after it).  Otherwise -- and for a flat-grid datagram the plan could not settle -- one workgroup
 // (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are a contiguous
@@ -736,13 +736,21 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
 // 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
 // descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
 // or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
-// 115.7 at 4 (105 VGPRs).  IPv6 measured 153.0 us against 132.2 us: not flat by default.
+// 115.7 at 4 (105 VGPRs).  IPv6: planners first (below), 129.8 us against 132.2 for one
+// workgroup per datagram.
 template <bool V6>
 __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.S;
-    const uint32_t g = blockIdx.x / S, s = blockIdx.x - g * S;
+    // IPv6: workgroups [0, n_dgram) plan datagram blockIdx.x and gather nothing -- dispatched
+    // first, so no plan lands in the launch's tail (c3_reasm6 129.8 us against 152.9 with the plan
+    // in each datagram's wave 0); the rest gather, S per datagram.  IPv4: wave 0 of each datagram's
+    // S plans and gathers (115.3 us against 118.0 with planners first)
+    constexpr bool PF = V6;
+    const bool planner = PF && blockIdx.x < p.n_dgram;
+    const uint32_t gb = PF ? (planner ? 0u : blockIdx.x - p.n_dgram) : blockIdx.x;
+    const uint32_t g = planner ? blockIdx.x : gb / S, s = planner ? 0u : gb - g * S;
     if (g >= p.n_dgram) return;
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
@@ -750,7 +758,8 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
                       (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < HDR;
     uint8_t* t = p.out + od.off + HDR;
     const uint32_t cap = od.len - HDR;
-    if (s == 0) plan_datagram<V6>(p, g, first, cnt, bad0, t, cap, lane);
+    if (PF ? planner : s == 0) plan_datagram<V6>(p, g, first, cnt, bad0, t, cap, lane);
+    if (planner) return;
     uint32_t acc = 0;
     if (!bad0 && cnt <= FLAT_MAXF) {
         const uint64_t tb = reinterpret_cast<uintptr_t>(t);
@@ -806,7 +815,7 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
         }
     }
     acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
-    if (lane == 0) p.slot[blockIdx.x] = acc;
+    if (lane == 0) p.slot[(uint64_t)g * S + s] = acc;
 }
 
 // Scratch of the flat grid (plans and partial sums, n_dgram x (32 + 4 S) bytes), never allocated
@@ -951,10 +960,8 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
 #ifndef REASM_FLAT_MIN
 #define REASM_FLAT_MIN 1024u
 #endif
-    // flat grid: IPv4 from REASM_FLAT_MIN datagrams on (IPv6 measured slower on it: c3_reasm6 153.0
-    // vs 132.2 us with the common-chain parse, 175.7 vs 133.3 us before it; the walk's code in
-    // the kernel costs 1 % of that, ab_reasm_flat.txt)
-    const uint32_t fmin = flat_min ? flat_min : (v6 ? UINT32_MAX : REASM_FLAT_MIN);
+    // flat grid from REASM_FLAT_MIN datagrams on
+    const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
     if (n_dgram >= fmin) {
         // S waves per datagram, FPI fragments each on average
         const uint64_t its = ((uint64_t)n_frag + 2u * FLAT_NP - 1u) / (2u * FLAT_NP);
@@ -967,7 +974,7 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
         a.plan = static_cast<ReasmPlan*>(scratch);
         a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
         a.S = S;
-        const dim3 fg((unsigned)((uint64_t)n_dgram * S)), fb(64);
+        const dim3 fg((unsigned)((uint64_t)n_dgram * (v6 ? S + 1u : S))), fb(64);
         if (v6) {
             hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
             hipLaunchKernelGGL((reassemble_kernel<true, 1, true>), dim3(n_dgram), fb, 0, s, a);

@@ -21,8 +21,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True, params=["auto", "flat"])
 def reasm_path(request):
-    """Every case through the launcher's own choice (the flat grid for IPv4 batches of 1024
-    datagrams or more, else one workgroup per datagram) and through the flat grid forced
+    """Every case through the launcher's own choice (the flat grid for batches of 1024 datagrams
+    or more, else one workgroup per datagram) and through the flat grid forced
     (pico_csum_set_reasm_flat(1))."""
     batch.set_reasm_flat(1 if request.param == "flat" else 0)
     yield request.param
