@@ -7,7 +7,9 @@ rounds and at the end.  Run on a C2 batch (rotating copies, the stamps of the la
     PICO_CSUM_LIB=picotcp_amd/diag/libpicocsum_stamps.so python tools/stamps.py --config c2
 
 Prints the kernel span and, per phase, percentiles over the waves of its start / duration,
-plus how much of the span the slowest waves' tail takes."""
+plus how much of the span the slowest waves' tail takes.  --config c1stream / c4stream: the
+uniform rings' stream waves (csum_uniform_stream_kernel forced on) on C1 / C4 rings -- slots 0 and
+3 the entry and end, 1 when the first step's data is in, 2 = 3."""
 from __future__ import annotations
 
 import argparse
