@@ -95,7 +95,7 @@ struct FragArgs {
     uint32_t* o_len;
     uint16_t* o_l4;
     uint8_t* verdict;
-    // flat grid (reasm_flat_kernel, then reassemble_kernel<V6, 1, true>): S waves per datagram,
+    // flat grid (reasm_flat_kernel, then reasm_finish_kernel): S waves per datagram,
     // one plan per datagram, one partial sum per wave
     struct ReasmPlan* plan;
     uint32_t* slot;
@@ -201,35 +201,13 @@ __device__ __forceinline__ uint32_t reasm_verdict(uint32_t flags, uint32_t len, 
     return v;
 }
 
-// WPD waves per datagram (1 or 4; the launcher picks it from the batch size)
-// FIN: the flat grid's finish -- a datagram whose plan is GOOD or BAD gets its results from the
-// plan and the waves' partial sums; a SLOW one runs the whole path below.
-template <bool V6, int WPD, bool FIN = false>
-__global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
+// Datagram g on the workgroup (WPD waves: 1 or 4; the launcher picks it from the batch size),
+// L its LDS tables; g < n_dgram
+template <bool V6, int WPD>
+__device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, FragLds& L) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;          // PICO_SIZE_IP6HDR / PICO_SIZE_IP4HDR
     constexpr uint32_t NT = 64u * WPD;
-    __shared__ FragLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t g = blockIdx.x;
-    if (g >= p.n_dgram) return;                       // workgroup-uniform
-    if constexpr (FIN) {
-        const uint32_t state = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.plan[g].state);
-        if (state != PLAN_SLOW) {
-            if (wv == 0) {
-                const uint32_t sv = lane < p.S ? p.slot[(uint64_t)g * p.S + lane] : 0u;
-                const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(sv), 63);
-                if (lane == 0) {
-                    const ReasmPlan r = p.plan[g];
-                    uint32_t l4 = 0, v = V_MALFORMED;
-                    if (state == PLAN_GOOD) v = reasm_verdict<V6>(p.flags, r.len, r.proto, r.pseudo, sum, r.w0, r.w1, l4);
-                    if (p.o_len) p.o_len[g] = state == PLAN_GOOD ? r.len : 0u;
-                    if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
-                    if (p.verdict) p.verdict[g] = (uint8_t)v;
-                }
-            }
-            return;
-        }
-    }
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
     const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
@@ -554,6 +532,43 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     }
 }
 
+template <bool V6, int WPD>
+__global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
+    __shared__ FragLds L;
+    if (blockIdx.x < p.n_dgram) reassemble_one<V6, WPD>(p, blockIdx.x, L);
+}
+
+// The flat grid's finish, one lane per datagram: a GOOD or BAD plan gets its results from the
+// plan and the S partial sums; the wave then runs the one-wave path over each SLOW datagram of
+// its 64 in turn.  (One one-wave workgroup per datagram instead: 4.9 us in the trace.)
+template <bool V6>
+__global__ __launch_bounds__(64) void reasm_finish_kernel(FragArgs p) {
+    __shared__ FragLds L;
+    const uint32_t lane = threadIdx.x, g0 = blockIdx.x * 64u, g = g0 + lane;
+    const bool in = g < p.n_dgram;
+    uint32_t state = PLAN_SLOW;
+    if (in) {
+        const ReasmPlan r = p.plan[g];
+        state = r.state;
+        if (state != PLAN_SLOW) {
+            uint32_t sum = 0;
+            for (uint32_t k = 0; k < p.S; ++k) sum += p.slot[(uint64_t)g * p.S + k];
+            uint32_t l4 = 0, v = V_MALFORMED;
+            if (state == PLAN_GOOD) v = reasm_verdict<V6>(p.flags, r.len, r.proto, r.pseudo, sum, r.w0, r.w1, l4);
+            if (p.o_len) p.o_len[g] = state == PLAN_GOOD ? r.len : 0u;
+            if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
+            if (p.verdict) p.verdict[g] = (uint8_t)v;
+        }
+    }
+    uint64_t slow = __builtin_amdgcn_ballot_w64(in && state == PLAN_SLOW);
+    while (slow) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(slow);
+        slow &= slow - 1u;
+        reassemble_one<V6, 1>(p, g0 + j, L);
+        __syncthreads();                              // L is the next one's
+    }
+}
+
 // ---------------------------------------------------------------- flat grid
 //
 // Large batches: S one-wave workgroups per datagram (S ~ its fragment pairs), each gathering
@@ -561,7 +576,7 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
 // headers, so the dispatcher balances the gather over the whole batch instead of one wave walking
 // a whole datagram; wave s = 0 also plans the datagram (its fragments one per lane: dedup,
 // completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
-// (reassemble_kernel<V6, 1, true>) adds them.  A datagram with repeated offsets or more than
+// (reasm_finish_kernel) adds them.  A datagram with repeated offsets or more than
 // FLAT_MAXF fragments is gathered again there by the one-wave path (its flat-grid bytes may hold
 // a later arrival's copy; the region past the reassembled datagram is unspecified).
 
@@ -977,10 +992,10 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
         const dim3 fg((unsigned)((uint64_t)n_dgram * (v6 ? S + 1u : S))), fb(64);
         if (v6) {
             hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
-            hipLaunchKernelGGL((reassemble_kernel<true, 1, true>), dim3(n_dgram), fb, 0, s, a);
+            hipLaunchKernelGGL((reasm_finish_kernel<true>), dim3((n_dgram + 63u) / 64u), fb, 0, s, a);
         } else {
             hipLaunchKernelGGL((reasm_flat_kernel<false>), fg, fb, 0, s, a);
-            hipLaunchKernelGGL((reassemble_kernel<false, 1, true>), dim3(n_dgram), fb, 0, s, a);
+            hipLaunchKernelGGL((reasm_finish_kernel<false>), dim3((n_dgram + 63u) / 64u), fb, 0, s, a);
         }
         return (int)hipGetLastError();
     }
