@@ -110,7 +110,14 @@ struct ReasmPlan {
 };
 constexpr uint32_t PLAN_GOOD = 0u, PLAN_BAD = 1u, PLAN_SLOW = 2u;
 constexpr uint32_t FLAT_MAXF = 64u;          // fragments a plan holds (one per lane)
-constexpr uint32_t FLAT_NP = 2u;             // fragment pairs a flat-grid wave gathers at once
+constexpr uint32_t FLAT_NP = 2u;
+// Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
+// c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
+// 130.5 / 143.6 -- the planners then end in the launch's tail)
+__host__ __device__ __forceinline__ uint32_t plan_per(uint32_t n_dgram) {
+    const uint32_t q = n_dgram / 512u;
+    return q < 1u ? 1u : (q > 8u ? 8u : q);
+}             // fragment pairs a flat-grid wave gathers at once
 
 struct FragLds {
     uint32_t key[FRAG_MAX];   // offset | MF << 16 | dup << 24
@@ -571,16 +578,16 @@ __global__ __launch_bounds__(64) void reasm_finish_kernel(FragArgs p) {
 
 // ---------------------------------------------------------------- flat grid
 //
-// Large batches: S one-wave workgroups per datagram (S ~ its fragment pairs), each gathering
-// fragment pairs s, s + S, ... of its datagram at their own offsets straight from their own
-// headers, so the dispatcher balances the gather over the whole batch instead of one wave walking
-// a whole datagram; wave s = 0 also plans the datagram (its fragments one per lane: dedup,
-// completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
+// Large batches: S one-wave workgroups per datagram (S ~ its fragments / 4), each gathering
+// fragments 4 s, ... of its datagram at their own offsets straight from their own headers, so the
+// dispatcher balances the gather over the whole batch instead of one wave walking a whole
+// datagram; planner workgroups dispatched ahead of them plan the datagrams (a datagram's fragments
+// one per lane: dedup, completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
 // (reasm_finish_kernel) adds them.  A datagram with repeated offsets or more than
 // FLAT_MAXF fragments is gathered again there by the one-wave path (its flat-grid bytes may hold
 // a later arrival's copy; the region past the reassembled datagram is unspecified).
 
-// wave 0 of the datagram's slice: pico_fragments_check_complete on registers (lane j: fragment j)
+// a planner: pico_fragments_check_complete on registers (lane j: fragment j)
 template <bool V6>
 __device__ __forceinline__ void plan_datagram(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, bool bad0,
                                               uint8_t* t, uint32_t cap, uint32_t lane) {
@@ -746,7 +753,8 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
     return acc;
 }
 
-// The flat grid: S one-wave workgroups per datagram; wave s takes fragments FPI s, ... in groups
+// The flat grid: planner workgroups, then S one-wave workgroups per datagram; wave s takes
+// fragments FPI s, ... in groups
 // of FPI = 2 FLAT_NP (two pairs' loads in flight).  c3_reasm (profiles/r05/ab_reasm_flat.txt):
 // 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
 // descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
@@ -758,14 +766,24 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.S;
-    // IPv6: workgroups [0, n_dgram) plan datagram blockIdx.x and gather nothing -- dispatched
-    // first, so no plan lands in the launch's tail (c3_reasm6 129.8 us against 152.9 with the plan
-    // in each datagram's wave 0); the rest gather, S per datagram.  IPv4: wave 0 of each datagram's
-    // S plans and gathers (115.3 us against 118.0 with planners first)
-    constexpr bool PF = V6;
-    const bool planner = PF && blockIdx.x < p.n_dgram;
-    const uint32_t gb = PF ? (planner ? 0u : blockIdx.x - p.n_dgram) : blockIdx.x;
-    const uint32_t g = planner ? blockIdx.x : gb / S, s = planner ? 0u : gb - g * S;
+    // Workgroups [0, npl) plan plan_per datagrams each and gather nothing -- dispatched first, so
+    // no plan lands in the launch's tail and the planners hold few of the slots (with the plan in
+    // each datagram's wave 0 instead: c3_reasm6 152.9 us, c3_reasm 115.3); the rest gather, S per
+    // datagram.
+    const uint32_t per = plan_per(p.n_dgram), npl = (p.n_dgram + per - 1u) / per;   // planner workgroups
+    if (blockIdx.x < npl) {                           // per datagrams in turn
+        for (uint32_t g = blockIdx.x * per; g < min(p.n_dgram, (blockIdx.x + 1u) * per); ++g) {
+            const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
+            const pico_csum_desc_dev od = p.odesc[g];
+            const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
+                              (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off ||
+                              od.len < HDR;
+            plan_datagram<V6>(p, g, first, cnt, bad0, p.out + od.off + HDR, od.len - HDR, lane);
+        }
+        return;
+    }
+    const uint32_t gb = blockIdx.x - npl;
+    const uint32_t g = gb / S, s = gb - g * S;
     if (g >= p.n_dgram) return;
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
@@ -773,8 +791,6 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
                       (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < HDR;
     uint8_t* t = p.out + od.off + HDR;
     const uint32_t cap = od.len - HDR;
-    if (PF ? planner : s == 0) plan_datagram<V6>(p, g, first, cnt, bad0, t, cap, lane);
-    if (planner) return;
     uint32_t acc = 0;
     if (!bad0 && cnt <= FLAT_MAXF) {
         const uint64_t tb = reinterpret_cast<uintptr_t>(t);
@@ -988,7 +1004,8 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
             a.plan = static_cast<ReasmPlan*>(scratch);
             a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
             a.S = S;
-            const dim3 fg((unsigned)((uint64_t)n_dgram * (v6 ? S + 1u : S))), fb(64);
+            const uint32_t per = plan_per(n_dgram);
+        const dim3 fg((unsigned)((uint64_t)n_dgram * S + (n_dgram + per - 1u) / per)), fb(64);
             if (v6) {
                 hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
                 hipLaunchKernelGGL((reasm_finish_kernel<true>), dim3((n_dgram + 63u) / 64u), fb, 0, s, a);
