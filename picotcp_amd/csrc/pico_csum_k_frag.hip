@@ -999,13 +999,14 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
         uint32_t S = (uint32_t)((its + n_dgram - 1u) / n_dgram);
         S = S < 1u ? 1u : (S > 32u ? 32u : S);
         const size_t plan_b = (size_t)n_dgram * sizeof(ReasmPlan), need = plan_b + (size_t)n_dgram * S * 4u;
+        const uint32_t per = plan_per(n_dgram);
+        const uint64_t blocks = (uint64_t)n_dgram * S + (n_dgram + per - 1u) / per;   // planners + gather
         void* scratch = nullptr;
-        if (reasm_scratch(s, need, &scratch) == 0) {
+        if (blocks <= 0x7FFFFFFFu && reasm_scratch(s, need, &scratch) == 0) {
             a.plan = static_cast<ReasmPlan*>(scratch);
             a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
             a.S = S;
-            const uint32_t per = plan_per(n_dgram);
-        const dim3 fg((unsigned)((uint64_t)n_dgram * S + (n_dgram + per - 1u) / per)), fb(64);
+            const dim3 fg((unsigned)blocks), fb(64);
             if (v6) {
                 hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
                 hipLaunchKernelGGL((reasm_finish_kernel<true>), dim3((n_dgram + 63u) / 64u), fb, 0, s, a);
@@ -1015,7 +1016,8 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
             }
             return (int)hipGetLastError();
         }
-        // no scratch (out of memory, or a capture state the stream query refuses): the same
+        // no scratch (out of memory, or a capture state the stream query refuses) or a grid past
+        // 2^31 workgroups: the same
         // results from one workgroup per datagram, which needs none
         (void)hipGetLastError();
     }
