@@ -406,9 +406,14 @@ def cpu_baseline_fused(host, kind: str, tx: bool, target_s: float, nat=None):
 
 
 def cpu_baseline_frag(st, target_s: float, v6: bool = False):
-    """The oracle's reassembly restatement (memcpy gather + pico_checksum of the reassembled
-    transport, as pico_fragments_reassemble + pico_transport_crc_check do) on 1 host core
-    over the first 256 datagrams of the batch."""
+    """The reference's own fragment path on 1 host core over the first 256 datagrams of the batch:
+    oracle/_ref/libref_rx_O3.so (the reference stack at -O3; rr_reasm_batch: every fragment into a
+    frame of its own, pico_ipv4_process_in / pico_ipv6_extension_headers, pico_ipv4/6_process_frag,
+    pico_fragments_reassemble, pico_transport_crc_check on the datagram handed on, a
+    pico_stack_tick per datagram; the stack is not thread-safe, hence one thread).  The IPv4
+    fragments' header checksums (zero in the synthetic batch, which the kernels do not check)
+    are filled in on the host copy first, as pico_ipv4_process_in drops a bad one.  Without the
+    reference build: the oracle's restatement (kind "port")."""
     from oracle import oracle as O
     fn = O.ipv6_reassemble if v6 else O.ipv4_reassemble
     b, d, gr, o, od, nfr, payload = st
@@ -419,9 +424,30 @@ def cpu_baseline_frag(st, target_s: float, v6: bool = False):
     desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
     hi = int(desc["off"][-1]) + int(desc["len"][-1])
     host = b[:hi].cpu().numpy()
+    nbytes = payload // n * k
+    if O.ref_reasm_available():
+        host = host.copy()
+        offs = desc["off"].astype(np.uint64)
+        if not v6:
+            O.fix_ipv4_header_crcs(host, offs)
+        o0 = int(offs[0])
+        O.ref_reasm_link(v6, bytes(host[o0 + 24:o0 + 40]) if v6 else bytes(host[o0 + 16:o0 + 20]))
+        secs, done, chk = O.ref_reasm_batch(v6, host, offs, desc["len"], grp)      # (warm)
+        reps = max(3, int(target_s / max(secs, 1e-3)))
+        times = []
+        for _ in range(reps):
+            secs, done, chk = O.ref_reasm_batch(v6, host, offs, desc["len"], grp)
+            times.append(secs)
+        dt = float(np.median(times))
+        return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "reference",
+                "sample": f"first {k} datagrams ({nbytes / 2**20:.0f} MiB of payload, {nf_used} fragments), the "
+                          f"reference's {'IPv6' if v6 else 'IPv4'} fragment path (oracle/_ref/libref_rx_O3.so "
+                          f"rr_reasm_batch: frame per fragment, {'pico_ipv6_extension_headers' if v6 else 'pico_ipv4_process_in'}, "
+                          f"pico_fragments_reassemble, pico_transport_crc_check), gcc -O3, 1 thread (the stack is "
+                          f"not thread-safe), median of {reps} passes; {done} reassembled, {chk} transport checks "
+                          f"passed"}
     odh = od.cpu().numpy().view(batch.DESC_DTYPE)[:k]
     outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
-    nbytes = payload // n * k
     t0 = time.perf_counter()
     fn(host, desc, grp, outh, odh)
     reps = max(1, int(target_s / max(time.perf_counter() - t0, 1e-3)))

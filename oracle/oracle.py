@@ -317,3 +317,93 @@ def ref_callers_batch(base: np.ndarray, desc: np.ndarray, mode: int, threads: in
     if rc != 0:
         raise RuntimeError(f"rc_batch_mt failed ({rc})")
     return secs, on, ol
+
+
+REF_RX_O3_SO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libref_rx_O3.so")
+
+
+class _quiet:
+    """fds 1 and 2 to /dev/null around calls into the reference stack, whose debug output (device
+    and protocol registration, timer-heap warnings) must not reach a caller's stdout (bench.py
+    prints one JSON line there); the C stdio buffers are flushed before the fds come back."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        sys.stderr.flush()
+        self.saved = (os.dup(1), os.dup(2))
+        self.null = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(self.null, 1)
+        os.dup2(self.null, 2)
+        return self
+
+    def __exit__(self, *exc):
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(self.saved[0], 1)
+        os.dup2(self.saved[1], 2)
+        for f in (*self.saved, self.null):
+            os.close(f)
+        return False
+
+
+def ref_reasm_available() -> bool:
+    return os.path.exists(REF_RX_O3_SO)
+
+
+def ref_reasm_batch(v6: bool, base: np.ndarray, offs: np.ndarray, lens: np.ndarray, groups: np.ndarray):
+    """The reference's own fragment path (oracle/ref_rx_driver.c rr_reasm_batch over the compiled
+    reference stack at -O3: each fragment into a pico_frame, pico_ipv4_process_in /
+    pico_ipv6_extension_headers, pico_ipv4/6_process_frag's tree and pico_fragments_reassemble,
+    pico_transport_crc_check on the datagram handed on) over every group, on the calling thread.
+    The datagrams' destination must be a local link (ref_reasm_link).  Returns (seconds,
+    datagrams reassembled, transport checks passed)."""
+    import time
+    if "rx3" not in _rlibs:
+        L = ctypes.CDLL(REF_RX_O3_SO)
+        L.rr_init.restype = ctypes.c_int
+        L.rr_ipv4_link.argtypes = [_u32]
+        L.rr_ipv6_link.argtypes = [_vp]
+        L.rr_reasm_batch.restype = ctypes.c_int
+        L.rr_reasm_batch.argtypes = [ctypes.c_int, _vp, _vp, _vp, _vp, _u32, _vp]
+        with _quiet():
+            rc = L.rr_init()
+        if rc != 0:
+            raise RuntimeError("rr_init failed")
+        _rlibs["rx3"] = L
+    L = _rlibs["rx3"]
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    groups = np.ascontiguousarray(groups, np.uint32)
+    chk = np.zeros(1, np.uint32)
+    with _quiet():
+        t0 = time.perf_counter()
+        done = L.rr_reasm_batch(int(v6), _p(base), _p(offs), _p(lens), _p(groups), groups.size // 2, _p(chk))
+        secs = time.perf_counter() - t0
+    return secs, int(done), int(chk[0])
+
+
+def ref_reasm_link(v6: bool, addr: bytes) -> None:
+    """Make `addr` (4 bytes as on the wire, or 16) a local link of the reference stack."""
+    ref_reasm_batch(v6, np.zeros(1, np.uint8), np.zeros(0), np.zeros(0), np.zeros(0))   # (loads it)
+    L = _rlibs["rx3"]
+    with _quiet():
+        if v6:
+            a = np.frombuffer(addr, np.uint8).copy()
+            L.rr_ipv6_link(_p(a))
+        else:
+            L.rr_ipv4_link(int.from_bytes(addr, "little"))
+
+
+def fix_ipv4_header_crcs(buf: np.ndarray, offs: np.ndarray) -> None:
+    """Store the header checksum (RFC 1071 over the 20-byte header, the field zeroed first) of the
+    IPv4 header at each offset, in place: what a sender's pico_ipv4_frame_push leaves there."""
+    offs = np.asarray(offs, np.int64)
+    idx = offs[:, None] + np.arange(20)[None, :]
+    h = buf[idx].astype(np.uint32)
+    h[:, 10] = h[:, 11] = 0
+    s = ((h[:, 0::2] << 8) | h[:, 1::2]).sum(axis=1)
+    while (s >> 16).any():
+        s = (s & 0xFFFF) + (s >> 16)
+    c = (~s) & 0xFFFF
+    buf[offs + 10] = (c >> 8).astype(np.uint8)
+    buf[offs + 11] = (c & 0xFF).astype(np.uint8)

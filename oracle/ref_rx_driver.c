@@ -125,6 +125,8 @@ int rr_take_delivered(int *check);
 int rr_ipv6_rx(const uint8_t *d, uint32_t avail, uint32_t *net_len, uint32_t *proto);
 int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, uint32_t n, uint8_t *out,
              uint32_t cap, uint32_t *out_len, uint32_t *module, int *check);
+int rr_reasm_batch(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, const uint32_t *groups,
+                   uint32_t n_dgram, uint32_t *checked);
 
 static struct pico_device *g_dev, *g_edev;
 static int g_arp;
@@ -238,12 +240,16 @@ int rr_ipv4_link(uint32_t addr)
 
 #define RR_PAD 70000u   /* zero bytes behind avail: a read past avail is defined (callers avoid it) */
 
+static int g_lean;              /* rr_reasm_batch: frames as a driver allocates them, no padding */
+
 static struct pico_frame *mk(const uint8_t *d, uint32_t avail)
 {
-    struct pico_frame *f = pico_frame_alloc(avail + RR_PAD);
+    const uint32_t pad = g_lean ? 0u : RR_PAD;
+    struct pico_frame *f = pico_frame_alloc(avail + pad);
     if (!f)
         return NULL;
-    memset(f->buffer, 0, avail + RR_PAD);
+    if (pad)
+        memset(f->buffer, 0, avail + pad);
     memcpy(f->buffer, d, avail);
     f->buffer_len = avail;
     f->start = f->buffer;
@@ -391,7 +397,7 @@ int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *
         return 0;
     *out_len = full->transport_len;
     *module = (uint32_t)g_deliv_proto;
-    if ((uint32_t)full->net_len + full->transport_len <= cap)
+    if (out && (uint32_t)full->net_len + full->transport_len <= cap)
         memcpy(out, full->net_hdr, (size_t)full->net_len + full->transport_len);
     if (g_deliv_proto == 6 || g_deliv_proto == 17) {
         *check = rr_transport_crc_check(full);               /* discards full when it fails */
@@ -402,6 +408,33 @@ int rr_reasm(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *
         pico_frame_discard(full);
     }
     return 1;
+}
+
+/* rr_reasm over n_dgram datagrams (groups: first fragment, count per datagram), nothing copied
+ * out: the reference's fragment path as a timed CPU baseline (bench.py) -- each fragment copied
+ * into a frame of its own size as pico_stack_recv does (not the padded, zero-filled frames the
+ * fixture runs use) -- with one
+ * pico_stack_tick per datagram as the stack's main loop runs it (it retires the cancelled
+ * expiry timers, which would otherwise pile up in the timer heap).  Returns the number of
+ * datagrams reassembled; *checked = how many of them passed pico_transport_crc_check. */
+int rr_reasm_batch(int v6, const uint8_t *base, const uint64_t *offs, const uint32_t *lens, const uint32_t *groups,
+                   uint32_t n_dgram, uint32_t *checked)
+{
+    uint32_t g, done = 0, ok = 0, len, module;
+    int check;
+    g_lean = 1;                 /* (well-formed batches: no read past a fragment's bytes) */
+    for (g = 0; g < n_dgram; g++) {
+        const uint32_t first = groups[2 * g], cnt = groups[2 * g + 1];
+        check = 0;
+        if (rr_reasm(v6, base, offs + first, lens + first, cnt, NULL, 0, &len, &module, &check) == 1) {
+            done++;
+            ok += check == 1;
+        }
+        pico_stack_tick();
+    }
+    g_lean = 0;
+    *checked = ok;
+    return (int)done;
 }
 
 /* An Ethernet device with the given MAC (pico_device_init with a MAC allocates dev->eth). */

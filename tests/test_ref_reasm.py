@@ -89,3 +89,34 @@ def test_reference_rerun_live(fam):
         np.testing.assert_array_equal(rout[:H + rl.value], c[p + "exp_out"][o:o + H + rl.value])
         if rm.value in (6, 17) and rc.value >= 0:
             assert want_v == (1 if rc.value else 4)
+
+
+@pytest.mark.skipif(not O.ref_reasm_available(), reason="oracle/_ref/libref_rx_O3.so not built (needs /root/reference)")
+@pytest.mark.parametrize("v6", [False, True])
+def test_reference_batch_baseline(v6, capfd):
+    """bench.py's reassembly CPU baseline: the -O3 reference stack's rr_reasm_batch reassembles
+    and transport-checks every datagram of a synthetic batch (IPv4 header checksums filled in, as
+    the baseline does), the oracle agreeing, and none of the stack's debug output reaches
+    stdout."""
+    from picotcp_amd import synth
+    lens = [64512, 3000, 2961, 20000] * 4              # (fragmented: bench.py's batches are)
+    if v6:
+        buf, off, flen, grp = synth.ipv6_fragments(lens, seed=9, proto=6, frag_payload=1448)
+    else:
+        buf, off, flen, grp = synth.ipv4_fragments(lens, seed=9, proto=6, frag_payload=1480)
+        O.fix_ipv4_header_crcs(buf, off)
+    d = np.zeros(off.size, O.DESC_DTYPE)
+    d["off"], d["len"] = off, flen
+    od = np.zeros(len(lens), O.DESC_DTYPE)
+    H = 40 if v6 else 20
+    od["off"] = np.arange(len(lens), dtype=np.uint64) * 65600
+    od["len"] = 65600
+    out = np.zeros(65600 * len(lens), np.uint8)
+    wl, w4, wv = (O.ipv6_reassemble if v6 else O.ipv4_reassemble)(buf, d, grp, out, od)
+    o0 = int(off[0])
+    O.ref_reasm_link(v6, bytes(buf[o0 + 24:o0 + 40]) if v6 else bytes(buf[o0 + 16:o0 + 20]))
+    secs, done, chk = O.ref_reasm_batch(v6, buf, off, flen, grp)
+    assert done == len(lens) and (wv != 8).all()
+    assert chk == int((wv == 1).sum()) == len(lens)
+    assert secs > 0
+    assert capfd.readouterr().out == ""
