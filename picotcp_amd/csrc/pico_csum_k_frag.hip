@@ -110,7 +110,15 @@ struct ReasmPlan {
 };
 constexpr uint32_t PLAN_GOOD = 0u, PLAN_BAD = 1u, PLAN_SLOW = 2u;
 constexpr uint32_t FLAT_MAXF = 64u;          // fragments a plan holds (one per lane)
-constexpr uint32_t FLAT_NP = 2u;
+#ifndef REASM_NP4
+#define REASM_NP4 2u
+#endif
+#ifndef REASM_NP6
+#define REASM_NP6 3u
+#endif
+// fragment pairs a flat-grid wave gathers at once (their loads in flight together): IPv4 2
+// (3: 113.2 vs 113.4 us, no gain), IPv6 3 (120.9 us; 2: 128.0, 4: 122.2 at 118 VGPRs)
+__host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 : REASM_NP4; }
 // Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
 // c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
 // 130.5 / 143.6 -- the planners then end in the launch's tail)
@@ -755,7 +763,7 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
 
 // The flat grid: planner workgroups, then S one-wave workgroups per datagram; wave s takes
 // fragments FPI s, ... in groups
-// of FPI = 2 FLAT_NP (two pairs' loads in flight).  c3_reasm (profiles/r05/ab_reasm_flat.txt):
+// of FPI = 2 flat_np (its pairs' loads in flight together).  c3_reasm (profiles/r05/ab_reasm_flat.txt):
 // 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
 // descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
 // or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
         const uint64_t tb = reinterpret_cast<uintptr_t>(t);
         const Window ow = make_window(tb, cap);
         auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
-        constexpr uint32_t NP = FLAT_NP, FPI = 2u * NP;          // pairs / fragments per iteration
+        constexpr uint32_t NP = flat_np(V6), FPI = 2u * NP;      // pairs / fragments per iteration
         for (uint32_t j0 = FPI * s; j0 < cnt; j0 += FPI * S) {
             // lanes 0..FPI-1 read fragments j0, ..., j0 + FPI - 1; a fragment is gathered when it
             // parses and the output region holds it (repeated offsets too: SLOW plans are gathered
@@ -995,7 +1003,8 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
     if (n_dgram >= fmin) {
         // S waves per datagram, FPI fragments each on average
-        const uint64_t its = ((uint64_t)n_frag + 2u * FLAT_NP - 1u) / (2u * FLAT_NP);
+        const uint32_t fpi = 2u * flat_np(v6 != 0);
+        const uint64_t its = ((uint64_t)n_frag + fpi - 1u) / fpi;
         uint32_t S = (uint32_t)((its + n_dgram - 1u) / n_dgram);
         S = S < 1u ? 1u : (S > 32u ? 32u : S);
         const size_t plan_b = (size_t)n_dgram * sizeof(ReasmPlan), need = plan_b + (size_t)n_dgram * S * 4u;
