@@ -31,7 +31,9 @@
 //   3. gather: two fragments' payloads per step (a wave's fragments w, w + 4, ... in pairs), in
 //      16-byte units on the output's 16-byte lines, 3 x 64 units per wave per step (two 1480-byte
 //      payloads): one byte-unaligned 16-byte load per unit through one buffer window over both
-//      payloads (out-of-range slots read zeros, no branches); v_dot2 sums on the
+//      payloads (out-of-range slots read zeros, no branches; cached loads -- neighbouring units
+//      share lines: non-temporal ones measured 123.4 / 132.2 us against 119.0 / 127.2 one
+//      workgroup per datagram, profiles/r05/ab_reasm_flat.txt); v_dot2 sums on the
 //      fly (every unit is a whole number of checksum words); a
 //      workgroup reduction at the end.  Software-pipelined over two register sets: the next
 //      step's loads are issued before this step's stores, and the stores are a fixed sequence
@@ -445,7 +447,7 @@ __device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, Fr
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x, v = inb ? st.vb : st.va;
                 const bool ok = st.valid && x < st.nt;
-                c0[k] = load_win<true>(win, ok ? v + 16u * u : WIN_OOB);   // byte-unaligned: the unit's 16 bytes
+                c0[k] = load_win<false>(win, ok ? v + 16u * u : WIN_OOB);   // byte-unaligned: the unit's 16 bytes
             }
         };
         auto process = [&](const Step& st, const uint4 (&c0)[U]) {
@@ -709,7 +711,7 @@ __device__ __forceinline__ void pair_issue(const PairStep& q, uint32_t lane, uin
         const uint32_t x = u0 + 64u * k + lane;
         const bool inb = x >= q.na;
         const uint32_t u = inb ? x - q.na : x, v = inb ? q.vb : q.va;
-        c0[k] = load_win<true>(win, x < q.nt ? v + 16u * u : WIN_OOB);
+        c0[k] = load_win<false>(win, x < q.nt ? v + 16u * u : WIN_OOB);   // (cached: see reasm_flat_kernel)
     }
 }
 
@@ -767,8 +769,8 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
 // 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
 // descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
 // or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
-// 115.7 at 4 (105 VGPRs).  IPv6: planners first (below), 129.8 us against 132.2 for one
-// workgroup per datagram.
+// 115.7 at 4 (105 VGPRs).  The payload loads are cached, not non-temporal: the byte-unaligned
+// 16-byte loads of neighbouring units share lines (113.8 -> 108.9 us, IPv6 121.3 -> 118.3).
 template <bool V6>
 __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
