@@ -32,7 +32,7 @@ __device__ __forceinline__ void copy_pair(__amdgpu_buffer_rsrc_t sr, __amdgpu_bu
             const uint32_t x = x0 + 64u * k + lane;
             const bool b = x >= na;
             const uint64_t o = (b ? sb : sa) + 16u * (b ? x - na : x);
-            v[k] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(x < nt ? (uint32_t)o : 0x80000000u), 0, 2);
+            v[k] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(x < nt ? (uint32_t)o : 0x80000000u), 0, 0);   // cached (as the product)
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
