@@ -930,8 +930,8 @@ def main():
                          "kernel_avg_us": round(kern_ms * 1e3, 2), "kernel_avg_us_max_rank": round(kern_max_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": algo_bytes},
         }
-        if cfg["kind"] == "frag":         # batches of >= 1024 datagrams: flat gather + finish
-            flat = a.reasm_flat == 1 or (a.reasm_flat == 0 and n >= 1024)
+        if cfg["kind"] == "frag":         # batches of >= 512 datagrams: flat gather + finish
+            flat = a.reasm_flat == 1 or (a.reasm_flat == 0 and n >= 512)
             out["roofline"]["kernels_per_step"] = 2 if flat else 1
         if ver is not None:
             out["verified"] = ver

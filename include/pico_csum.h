@@ -328,7 +328,7 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
  * The bytes of an output region are unspecified when its datagram is not reassembled (the
  * gather starts before completeness is known) and past the reassembled datagram's end (a
  * repeated offset's later arrival may have been gathered there); no byte outside the region is
- * written.  Any of the three output pointers may be NULL.  Batches of 1024 datagrams or more run
+ * written.  Any of the three output pointers may be NULL.  Batches of 512 datagrams or more run
  * on a flat grid whose per-datagram plans and partial sums live in library scratch (about
  * 32 + fragments bytes a datagram): per calling thread and stream, kept across calls; in
  * a call captured into a graph, owned by that graph -- two executable instances of one captured
@@ -438,7 +438,7 @@ int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
 
 /* Tuning knob (tests / bench sweeps), per calling thread: the reassembly batches' flat grid
  * (pico_ipv4_reassemble_batch_dev / pico_ipv6_reassemble_batch_dev) -- 0 = automatic (batches
- * of 1024 datagrams or more), 1 = always, 2 = never (one workgroup per datagram).  Results never
+ * of 512 datagrams or more), 1 = always, 2 = never (one workgroup per datagram).  Results never
  * depend on it. */
 int pico_csum_set_reasm_flat(uint32_t mode);
 

@@ -339,7 +339,7 @@ def set_host_in_place(on: bool = True) -> None:
 
 def set_reasm_flat(mode: int = 0) -> None:
     """Reassembly batches' flat grid (tests / bench sweeps, this thread): 0 automatic (batches from
-    1024 datagrams), 1 always, 2 never.  Results never depend on it."""
+    512 datagrams), 1 always, 2 never.  Results never depend on it."""
     _lib.check("pico_csum_set_reasm_flat", _lib.load().pico_csum_set_reasm_flat(mode))
 
 

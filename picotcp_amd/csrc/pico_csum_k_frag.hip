@@ -12,7 +12,7 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// Batches of >= 1024 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
+// Batches of >= 512 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
 // the gather spread over ~one wave per four fragments, the plan and the sums brought together
 // after it).  Otherwise -- and for a flat-grid datagram the plan could not settle -- one workgroup
 // (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are a contiguous
@@ -999,9 +999,11 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
                static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict, nullptr, nullptr, 0u};
     const hipStream_t s = static_cast<hipStream_t>(stream);
 #ifndef REASM_FLAT_MIN
-#define REASM_FLAT_MIN 1024u
+#define REASM_FLAT_MIN 512u
 #endif
-    // flat grid from REASM_FLAT_MIN datagrams on
+    // flat grid from REASM_FLAT_MIN datagrams on (64512-byte datagrams, flat vs one workgroup per
+    // datagram: 256 19.2 vs 18.7 us, 512 22.6 vs 23.9, 1024 35.4 vs 36.9;
+    // profiles/r05/ab_reasm_small_batches.txt)
     const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
     if (n_dgram >= fmin) {
         // S waves per datagram, FPI fragments each on average

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True, params=["auto", "flat"])
 def reasm_path(request):
-    """Every case through the launcher's own choice (the flat grid for batches of 1024 datagrams
+    """Every case through the launcher's own choice (the flat grid for batches of 512 datagrams
     or more, else one workgroup per datagram) and through the flat grid forced
     (pico_csum_set_reasm_flat(1))."""
     batch.set_reasm_flat(1 if request.param == "flat" else 0)
@@ -179,7 +179,7 @@ def test_ipv6_reassembly_limits():
 @pytest.mark.parametrize("n", [1600, 3200])
 def test_batch_shapes(n, v6, reasm_path):
     """Batches below and above the launcher's switch to one wave per datagram (3072) -- both on
-    the flat grid (>= 1024 datagrams) unless forced off -- with datagrams of more than 64 fragments
+    the flat grid (>= 512 datagrams) unless forced off -- with datagrams of more than 64 fragments
     per wave (the gather's metadata blocks; the flat grid's SLOW plans)."""
     rng = np.random.default_rng(n + v6)
     lens = rng.integers(0, 3000, n)

@@ -33,7 +33,10 @@ def main():
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rotate", type=int, default=4)
+    ap.add_argument("--reasm-flat", type=int, default=0, help="pico_csum_set_reasm_flat mode for the reassembly")
+    ap.add_argument("--only-reasm", action="store_true", help="time the reassembly alone")
     a = ap.parse_args()
+    batch.set_reasm_flat(a.reasm_flat)
     dev = torch.device("cuda:0")
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "bin", "libgather_ceiling.so"))
     lib.gather_ceiling_launch.restype = ctypes.c_int
@@ -93,13 +96,14 @@ def main():
 
     payload = sets[0][0][6]
     res = {}
+    fns = (("reassemble", reasm),) if a.only_reasm else (
+        ("reassemble", reasm), ("bare_gather", gather(0)), ("bare_gather_4frag_steps", gather(1)),
+        ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)), ("sequential_copy", copy))
     for rnd in range(3):
-        for name, f in (("reassemble", reasm), ("bare_gather", gather(0)), ("bare_gather_4frag_steps", gather(1)),
-                        ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)),
-                        ("sequential_copy", copy)):
+        for name, f in fns:
             res.setdefault(name, []).append(timed(f))
     out = {"layout": ("ipv6" if a.v6 else "ipv4") + (" interleaved" if a.interleave else " datagram-major"),
-           "datagrams": a.n, "payload_bytes": payload}
+           "datagrams": a.n, "payload_bytes": payload, "reasm_flat": a.reasm_flat}
     for name, v in res.items():
         us = float(np.median(v))
         out[name + "_us"] = round(us, 2)
