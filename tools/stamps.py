@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--n", type=int, default=262144)
     ap.add_argument("--rotate", type=int, default=12)
     ap.add_argument("--wpb", type=int, default=4, help="waves per workgroup of the kernel")
+    ap.add_argument("--balanced", action="store_true",
+                    help="every group of 64 datagrams the same size multiset (tools/balance_probe.py)")
     a = ap.parse_args()
     lib = _lib.load()
     lib.pico_csum_diag_set_stamps.restype = ctypes.c_int
@@ -43,6 +45,10 @@ def main():
     if a.config == "c4stream":
         n = 1 << 22
     lens = synth.imix_lengths(n, 3) + (20 if a.config == "c2v6" else 0)
+    if a.balanced:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from balance_probe import balanced_lengths
+        lens = balanced_lengths(n, 3) + (20 if a.config == "c2v6" else 0)
     sets = []
     if uni:           # uniform 1500 B rings on the stream waves (stamps: entry, first step in, end)
         batch.set_uniform_stream(1, 0)
@@ -111,7 +117,7 @@ def main():
                                "late_share": round(float((late & (xcd == x)).sum() / max(1, late.sum())), 3)}
                               for x in range(8)]
     for o in out:
-        print(json.dumps({"config": a.config, **o}))
+        print(json.dumps({"config": a.config + ("_balanced" if a.balanced else ""), **o}))
 
 
 if __name__ == "__main__":
