@@ -38,6 +38,7 @@ oracle/_ref) on the host cores over a bounded sample of the same frames.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -109,6 +110,10 @@ CONFIGS = {
                         workload="C3 reassembly, fragments of the 4K datagrams interleaved as a NIC receives "
                                  "concurrent flows (fragment k of every datagram, then k + 1, ...), otherwise as "
                                  "c3_reasm"),
+    "c3_reasm_576": dict(kind="frag", frames=4096, frame_bytes=64512, frag_payload=552,
+                         workload="C3 reassembly over a 576 B MTU: 4K x 64512 B IPv4/TCP datagrams arriving as 552 B "
+                                  "fragments (117 per datagram: past the flat grid's 64 a wave, one workgroup per "
+                                  "datagram), otherwise as c3_reasm"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -210,12 +215,15 @@ FRAG = 1480                 # IPv4 fragment payload (MTU 1500 - 20 B header)
 FRAG6 = 1448                # IPv6 fragment payload (MTU 1500 - 40 B header - 8 B fragment header, 8-aligned)
 
 
-def make_frag(n, tl, device, seed, v6=False, interleave=False):
+def make_frag(n, tl, device, seed, v6=False, interleave=False, frag_payload=0):
     """n IPv4/TCP (IPv6/TCP) datagrams of tl transport bytes as in-order 1480 B (1448 B)
-    fragments, each behind a 14 B gap, built on the device (vectorized); the TCP checksum made
-    valid with one untimed reassembly pass.  Returns (buffer, fragment descriptors, groups, out,
-    out descriptors, fragment count, payload bytes)."""
+    fragments (frag_payload: another payload size, a multiple of 8), each behind a 14 B gap, built
+    on the device (vectorized); the TCP checksum made valid with one untimed reassembly pass.
+    Returns (buffer, fragment descriptors, groups, out, out descriptors, fragment count, payload
+    bytes)."""
     fr, hl = (FRAG6, 48) if v6 else (FRAG, 20)
+    if frag_payload:
+        fr = frag_payload
     nf = -(-tl // fr)
     pl = np.full(nf, fr, np.int64)
     pl[-1] = tl - fr * (nf - 1)
@@ -466,8 +474,8 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
     for rotation slot 0 against the CPU oracle (oracle/pico_csum_oracle.c, the checker; never
     the measured path).  uniform: every frame of the batch (the restatement on `threads`
     pthreads); fused IPv4 / IPv6 / Ethernet: every datagram, on the device buffer as the timed
-    steps left it (TX: the values and the crc fields written in place); reassembly: the first
-    256 datagrams (lengths, checksums, verdicts and the reassembled bytes)."""
+    steps left it (TX: the values and the crc fields written in place); reassembly: every
+    datagram (lengths, checksums, verdicts and the reassembled bytes)."""
     from oracle import oracle as O
     t0 = time.perf_counter()
     if kind == "uniform":
@@ -480,7 +488,7 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
     elif kind == "frag":
         b, d, gr, o, od, nfr, payload = slot
         n = gr.numel() // 2
-        k = min(n, 256)
+        k = n
         grp = gr.cpu().numpy().view(np.uint32)[:2 * k]
         nf_used = int(grp[-2] + grp[-1])
         desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
@@ -498,7 +506,7 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
                 a = int(odh["off"][g])
                 bad += int(not np.array_equal(gout[a:a + H + int(wl[g])], outh[a:a + H + int(wl[g])]))
         frames = k
-        what = (f"first 256 datagrams: lengths, checksums, verdicts and reassembled bytes vs "
+        what = (f"every datagram ({k}): lengths, checksums, verdicts and reassembled bytes vs "
                 f"oracle_ipv{6 if v6 else 4}_reassemble")
     else:
         b, d = slot[0], slot[1]
@@ -539,24 +547,65 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
     return {"frames": frames, "mismatches": bad, "checker": what, "seconds": round(time.perf_counter() - t0, 2)}
 
 
+def seq_copy_lib():
+    """tools/bin/libgather_ceiling.so (a measurement aid built by __graft_entry__.build(), never the
+    product): its seq_copy_launch is the hand-written sequential copy the reassembly is priced
+    against.  None when it is not built."""
+    path = os.path.join(ROOT, "tools", "bin", "libgather_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.seq_copy_launch.restype = ctypes.c_int
+    lib.seq_copy_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint64, ctypes.c_void_p]
+    return lib
+
+
+# (variant, units per lane, workgroups): 0 non-temporal loads + stores, 1 cached, 2 nt loads + cached
+# stores; workgroups 0 = one trip each, else a striding grid (8192 = 32 per CU)
+SEQ_COPY_SHAPES = ((0, 4, 0), (0, 8, 0), (1, 4, 0), (2, 4, 0), (0, 4, 8192), (2, 8, 8192))
+
+
 def copy_ceiling(nbytes: int, dev) -> dict:
-    """The device's own contiguous copy (torch copy_ = a HIP D2D copy kernel) of the payload bytes the
-    reassembly moves (read + write), timed the same way: the practical ceiling of a gather."""
+    """The device's own contiguous copy of the payload bytes the reassembly moves (read + write),
+    timed the same way: the practical ceiling of a gather.  A hand-written 16-byte-per-lane copy
+    (tools/gather_ceiling.hip seq_copy, several shapes, the fastest reported); torch copy_ beside it."""
+    nbytes &= ~15
     rot = max(3, -(-(1 << 30) // nbytes))
     src = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(rot)]
     dst = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(rot)]
-    for i in range(10):
-        dst[i % rot].copy_(src[i % rot])
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    k = 50
-    for i in range(k):
-        dst[i % rot].copy_(src[i % rot])
-    ev1.record()
-    torch.cuda.synchronize(dev)
-    us = ev0.elapsed_time(ev1) / k * 1e3
-    return {"copy_us": round(us, 2), "copy_GBs": round(2 * nbytes / us / 1e3, 1),
-            "what": f"torch copy_ of {nbytes} B (read + write), {rot} rotating buffers, HIP events"}
+    stream = torch.cuda.current_stream(dev)
+    lib = seq_copy_lib()
+
+    def timed(f, k=30):
+        for i in range(5):
+            f(i)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for i in range(k):
+            f(i)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        return ev0.elapsed_time(ev1) / k * 1e3
+
+    shapes = {}
+    if lib is not None:
+        h = ctypes.c_void_p(stream.cuda_stream)
+        for var, u, blocks in SEQ_COPY_SHAPES:
+            def f(i, var=var, u=u, blocks=blocks):
+                assert lib.seq_copy_launch(var, u, blocks, dst[i % rot].data_ptr(), src[i % rot].data_ptr(), nbytes, h) == 0
+            shapes[f"v{var}_u{u}_g{blocks}"] = round(timed(f), 2)
+    torch_us = timed(lambda i: dst[i % rot].copy_(src[i % rot]))
+    if shapes:
+        best = min(shapes, key=shapes.get)
+        us = shapes[best]
+        what = (f"hand-written 16 B/lane copy (tools/gather_ceiling.hip seq_copy, fastest of {len(shapes)} shapes: "
+                f"{best}) of {nbytes} B (read + write), {rot} rotating buffers, HIP events")
+    else:
+        us = torch_us
+        what = f"torch copy_ of {nbytes} B (read + write), {rot} rotating buffers, HIP events (seq_copy not built)"
+    return {"copy_us": round(us, 2), "copy_GBs": round(2 * nbytes / us / 1e3, 1), "what": what,
+            "shapes_us": shapes, "torch_copy_us": round(torch_us, 2)}
 
 
 def e2e_rate_desc(host):
@@ -805,7 +854,8 @@ def main():
         n, ln = cfg["frames"], cfg["frame_bytes"]
         rot = a.rotate or max(2, rotation(2 * n * ln))
         v6 = bool(cfg.get("v6"))
-        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6, bool(cfg.get("interleave"))) for i in range(rot)]
+        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6, bool(cfg.get("interleave")), cfg.get("frag_payload", 0))
+                for i in range(rot)]
         res = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 

@@ -51,8 +51,9 @@ extern "C" {
  *   2: V_FRAG, the reference's IPv6 byte-9 dispatch by default;
  *   3: F_NXTHDR_DISPATCH moved to 0x8 (bit 0x4 -- ABI 1's F_REF_DISPATCH, the opposite meaning --
  *      is rejected with -EINVAL); the forwarding batch takes the host's link addresses and a
- *      carried state (pico_ipv4_pre_forward_checks in full). */
-#define PICO_CSUM_ABI_VERSION 3
+ *      carried state (pico_ipv4_pre_forward_checks in full);
+ *   4: pico_csum_release_thread_scratch; the reassembly's flat-grid scratch is freed at thread exit. */
+#define PICO_CSUM_ABI_VERSION 4
 
 /* picoTCP pico_err values used here (include/pico_protocol.h:27,31,38 + ENODEV) */
 #define PICO_CSUM_EIO     5
@@ -329,10 +330,12 @@ int pico_ipv4_nat_batch_dev(void *d_base, uint64_t base_len, const struct pico_c
  * gather starts before completeness is known) and past the reassembled datagram's end (a
  * repeated offset's later arrival may have been gathered there); no byte outside the region is
  * written.  Any of the three output pointers may be NULL.  Batches of 512 datagrams or more run
- * on a flat grid whose per-datagram plans and partial sums live in library scratch (about
- * 32 + fragments bytes a datagram): per calling thread and stream, kept across calls; in
- * a call captured into a graph, owned by that graph -- two executable instances of one captured
- * graph must not run concurrently (pico_csum_set_reasm_flat selects the grid). */
+ * on a flat grid whose per-datagram tallies live in library scratch (8 bytes a datagram, kept
+ * zero between calls): per calling thread and stream, kept across calls and freed when the
+ * thread exits or calls pico_csum_release_thread_scratch; in a call captured into a graph,
+ * owned by that graph (freed after the graph is destroyed, by the next eager call or release)
+ * -- two executable instances of one captured graph must not run concurrently
+ * (pico_csum_set_reasm_flat selects the grid). */
 int pico_ipv4_reassemble_batch_dev(const void *d_base, uint64_t base_len, const struct pico_csum_desc *d_frag,
                                    uint32_t n_frag, const uint32_t *d_groups, uint32_t n_dgram, void *d_out,
                                    uint64_t out_len, const struct pico_csum_desc *d_out_desc, uint32_t *d_out_len,
@@ -361,7 +364,9 @@ int pico_ipv6_reassemble_batch_dev(const void *d_base, uint64_t base_len, const 
 
 /* ---------------------------------------------------------------- layer 3 */
 
-struct pico_csum_ctx;   /* device, two streams, double-buffered staging */
+struct pico_csum_ctx;   /* device, three streams and staging slots (the uniform ring alternates two;
+                         * staged descriptor batches rotate over three, the third staging buffer
+                         * allocated on their first call) */
 
 struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes);
 void pico_csum_ctx_destroy(struct pico_csum_ctx *ctx);
@@ -441,6 +446,13 @@ int pico_csum_set_uniform_stream(uint32_t mode, uint32_t frames_per_wave);
  * of 512 datagrams or more), 1 = always, 2 = never (one workgroup per datagram).  Results never
  * depend on it. */
 int pico_csum_set_reasm_flat(uint32_t mode);
+
+/* Frees the calling thread's reassembly scratch (the flat grid's tallies, one buffer per stream
+ * the thread launched on) and the scratch of captured graphs destroyed since; the thread's next
+ * flat-grid call allocates again.  A thread's scratch is also freed when the thread exits.  Call
+ * it with no reassembly of this thread still running on the device (hipFree waits for the device).
+ * Returns 0, or -PICO_CSUM_ENODEV without a device. */
+int pico_csum_release_thread_scratch(void);
 
 #ifdef __cplusplus
 }

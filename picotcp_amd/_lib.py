@@ -48,6 +48,7 @@ EXPORTED = (
     "pico_csum_set_uniform_stream",
     "pico_csum_set_host_in_place",
     "pico_csum_set_reasm_flat",
+    "pico_csum_release_thread_scratch",
 )
 
 F_WRITE = 0x1
@@ -55,7 +56,7 @@ F_TX = 0x2
 F_NXTHDR_DISPATCH = 0x8   # IPv6 RX: TCP / UDP by next header, not the reference's byte 9 (include/pico_csum.h)
 V_ACCEPT, V_NET_BAD, V_L4_BAD, V_MALFORMED, V_EXPIRED = 1, 2, 4, 8, 16
 V_FRAG = 16                # RX / TX batches (V_EXPIRED: the forwarding batch)
-ABI_VERSION = 3
+ABI_VERSION = 4
 V_DROP_L2, V_ARP, V_IPV6 = 32, 64, 128
 V_UNTOUCHED = 32            # NAT batch (same bit as V_DROP_L2)
 V_LOCAL_SRC, V_DUPLICATE = 32, 64   # forwarding batch (same bits as V_DROP_L2 / V_ARP)
@@ -123,6 +124,8 @@ def load() -> ctypes.CDLL:
         sig("pico_csum_set_host_in_place", ctypes.c_int, u32)
     if hasattr(lib, "pico_csum_set_reasm_flat"):
         sig("pico_csum_set_reasm_flat", ctypes.c_int, u32)
+    if hasattr(lib, "pico_csum_release_thread_scratch"):
+        sig("pico_csum_release_thread_scratch", ctypes.c_int)
     del u8p
     if lib.pico_csum_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {lib.pico_csum_abi_version()}, this binding {ABI_VERSION}: rebuild it")

@@ -44,6 +44,7 @@ int pico_csum_launch_reassemble(int v6, const void *base, uint64_t base_len, con
                                 const uint32_t *groups, uint32_t n_dgram, void *out, uint64_t out_len, const void *out_desc,
                                 uint32_t *o_len, uint16_t *o_l4, uint8_t *verdict, uint32_t flags, uint32_t flat_min,
                                 void *stream);
+int pico_csum_reasm_release_thread(void);
 
 /* ------------------------------------------------------------------ errors */
 
@@ -155,6 +156,16 @@ int pico_csum_set_reasm_flat(uint32_t mode)
         return fail(PICO_CSUM_EINVAL, "reassembly flat-grid mode must be 0 (auto), 1 (always) or 2 (never)");
     g_reasm_flat = mode;
     return 0;
+}
+
+int pico_csum_release_thread_scratch(void)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return fail(PICO_CSUM_ENODEV, "pico_csum_release_thread_scratch: no HIP device");
+    }
+    return pico_csum_reasm_release_thread() ? fail(PICO_CSUM_EIO, "pico_csum_release_thread_scratch failed") : 0;
 }
 
 int pico_csum_set_host_in_place(uint32_t on)
@@ -577,8 +588,10 @@ int pico_ipv6_reassemble_batch_dev(const void *d_base, uint64_t base_len, const 
 #define CTX_MAX_DESC(staging) ((staging) / 64u + 64u)
 
 /* staging slots (a buffer, a stream, an event each): the uniform ring alternates slots 0 and 1 (its
- * chunks need no per-chunk host work); descriptor batches rotate over all NSLOT, so the host loop
- * waits on the chunk three back, not two (r05: C2 staged) */
+ * chunks need no per-chunk host work); staged descriptor batches rotate over all NSLOT, so the host
+ * loop waits on the chunk three back, not two (r05: C2 staged).  The third slot's
+ * staging buffer is allocated when a staged descriptor batch first needs it (the uniform ring and
+ * the in-place descriptor path never do). */
 #define NSLOT 3
 
 struct pico_csum_ctx {
@@ -618,7 +631,7 @@ struct pico_csum_ctx *pico_csum_ctx_create(int device, uint64_t staging_bytes)
     c->staging = staging_bytes;
     if (hipSetDevice(device) != hipSuccess) { fail(PICO_CSUM_ENODEV, "hipSetDevice(%d)", device); free(c); return NULL; }
     for (i = 0; i < NSLOT; i++) {
-        if (hipMalloc(&c->d_buf[i], staging_bytes) != hipSuccess ||
+        if ((i < 2 && hipMalloc(&c->d_buf[i], staging_bytes) != hipSuccess) ||
             hipMalloc((void **)&c->d_out[i], 2u * CTX_MAX_FRAMES(staging_bytes)) != hipSuccess ||
             hipStreamCreateWithFlags(&c->st[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess) {
@@ -968,6 +981,10 @@ static int desc_batch_host(struct pico_csum_ctx *c, int mode, const void *base, 
             if (too_big(c, &desc[i], base_len))
                 return fail(PICO_CSUM_EINVAL, "%s: frame %u of %u bytes exceeds the staging buffer", what, i,
                             desc[i].len);
+    if (!c->d_buf[NSLOT - 1] && hipMalloc(&c->d_buf[NSLOT - 1], c->staging) != hipSuccess) {
+        c->d_buf[NSLOT - 1] = NULL;
+        return fail(PICO_CSUM_ENOMEM, "%s: third staging buffer (%llu B)", what, (unsigned long long)c->staging);
+    }
     i = 0;
 #define FLUSH(bb) flush_results(c, bb, out, out_net, out_l4, verdict)
 #define TRY(call, msg)                                                                             \

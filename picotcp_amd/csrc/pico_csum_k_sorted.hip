@@ -852,11 +852,13 @@ __device__ __forceinline__ uint32_t pairing(uint32_t v, bool odd) {
 // anything else needs the extension-header walk: the sorted rounds).  ETH: the Ethernet batch
 // (MODE 3): IPv4 and IPv6 behind the 14-byte header (ARP / dropped frames need no sums; a wave
 // holding an IPv6 datagram that needs the extension-header walk falls back after the loop).
+// (eth6_field, uniform64, lds_pair: used by the fused modes' stream waves only -- the RAW-mode
+// translation unit, SORTED_MODE 0, instantiates none of them.)
 // MODE 3 stream, an IPv6 frame: where the transport field the finish reads lies (relative to the
 // transport start; NONE = none) -- RX: the UDP crc (present?) when byte 9 (the reference's dispatch,
 // or with F_NXD the next header) says UDP, the ICMPv6 type; TX: the crc field to compute
 // (sorted_batch's MODE 2 rules)
-__device__ __forceinline__ uint32_t eth6_field(bool tx, uint32_t nh, uint32_t b9, bool nxd) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t eth6_field(bool tx, uint32_t nh, uint32_t b9, bool nxd) {
     if (!tx) {
         const bool ref17 = !nxd && b9 == 17u;
         if (nh == 6u && !ref17) return NONE;
@@ -883,7 +885,7 @@ __device__ __forceinline__ uint32_t hw_range_sum(const uint4 (&hw)[HW], uint32_t
     return s;
 }
 
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
@@ -899,7 +901,7 @@ __device__ __forceinline__ void lds_words(const uint32_t* wl, uint32_t pos, uint
 #pragma unroll
     for (int m = 0; m < NW; ++m) H[m] = __builtin_amdgcn_alignbyte(E[m + 1], E[m], sh);
 }
-__device__ __forceinline__ uint32_t lds_pair(const uint32_t* wl, uint32_t pos) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t lds_pair(const uint32_t* wl, uint32_t pos) {
     const uint32_t q = pos >> 2;
     return __builtin_amdgcn_alignbyte(wl[q + 1], wl[q], pos & 3u) & 0xFFFFu;
 }

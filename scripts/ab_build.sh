@@ -9,7 +9,7 @@ NAME=$1; TU=$2; shift 2
 make -s -j8 -C $R/picotcp_amd/csrc
 B=$R/build/csrc; H=$R/picotcp_amd/csrc
 mkdir -p $R/ablib $B/ab
-HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include"
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include -I$R/picotcp_amd/csrc"
 case $TU in
   sorted_fused)
     SRC=${SRC:-$H/pico_csum_k_sorted.hip}

@@ -50,9 +50,9 @@ def test_reference_symbol_signatures_are_drop_in():
 
 
 def test_abi_version():
-    assert _lib.load().pico_csum_abi_version() == _lib.ABI_VERSION == 3
+    assert _lib.load().pico_csum_abi_version() == _lib.ABI_VERSION == 4
     src = open(HEADER).read()
-    assert re.search(r"#define PICO_CSUM_ABI_VERSION 3\b", src)
+    assert re.search(r"#define PICO_CSUM_ABI_VERSION 4\b", src)
     for name, val in (("F_NXTHDR_DISPATCH", 8), ("V_FRAG", 16), ("V_EXPIRED", 16), ("V_MALFORMED", 8),
                       ("V_LOCAL_SRC", 32), ("V_DUPLICATE", 64)):
         m = re.search(rf"#define PICO_CSUM_{name}\s+(0x[0-9a-fA-F]+|[0-9]+)u", src)

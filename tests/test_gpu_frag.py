@@ -296,3 +296,42 @@ def test_flat_grid_streams_and_sizes():
     torch.cuda.synchronize()
     for r, o, (_, od, size, want, out_o) in runs:
         _check_flat(r, o, od, want, out_o)
+
+
+def _with_retransmits(buf, off, flen, grp, seed, per=(1, 3)):
+    """Every datagram gets per[0]..per[1] retransmitted fragments: a copy of one of its fragments
+    (same header, different payload bytes) at a random place in its arrival order -- before the
+    original (the copy is then the kept one) or after it (rejected by pico_tree_insert)."""
+    rng = np.random.default_rng(seed)
+    extra, new_off, new_len, new_grp = [], [], [], []
+    pos = buf.size
+    for first, cnt in grp:
+        orig = [(int(off[first + k]), int(flen[first + k])) for k in range(cnt)]
+        order = list(orig)
+        for _ in range(int(rng.integers(per[0], per[1] + 1)) if cnt else 0):
+            o, n = orig[int(rng.integers(0, cnt))]
+            f = buf[o:o + n].copy()
+            f[20:] = rng.integers(0, 256, n - 20, dtype=np.uint8)     # (IPv4: the payload behind 20 B)
+            extra.append(f)
+            order.insert(int(rng.integers(0, len(order) + 1)), (pos, n))
+            pos += n
+        new_grp.append((len(new_off), len(order)))
+        new_off += [o for o, _ in order]
+        new_len += [n for _, n in order]
+    nb = np.concatenate([buf] + extra + [np.zeros(16, np.uint8)])
+    return nb, np.array(new_off, np.uint64), np.array(new_len, np.uint32), np.array(new_grp, np.uint32)
+
+
+@pytest.mark.parametrize("payload", [1480, 552])
+def test_flat_grid_retransmits(payload):
+    """A batch of 700 datagrams (the flat grid under both fixture settings), every one with 1-3
+    retransmitted fragments carrying different payload bytes, arrival shuffled: the earliest
+    arrival of each offset is kept, as the reference's fragment tree does, on every datagram."""
+    rng = np.random.default_rng(payload)
+    lens = rng.integers(1, 20000, 700).tolist()
+    buf, off, flen, grp = synth.ipv4_fragments(lens, seed=payload, proto=6, frag_payload=payload)
+    buf, off, flen, grp = _with_retransmits(buf, off, flen, grp, seed=payload + 1)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=4)
+    wl, wv = check(buf, d, grp, od, size)
+    assert (wv != 8).mean() > 0.9

@@ -95,3 +95,51 @@ extern "C" int gather_ceiling_launch(int mode, const void* src, uint64_t src_len
 #undef GC_ARGS
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- the sequential copy ceiling
+//
+// The device's own contiguous copy of n bytes, hand-written (VERDICT r05 Missing #3: torch copy_
+// reached 5.38-5.40 TB/s on the reassembly's bytes; MI355X_MICROARCH.md measures a float4 copy at
+// 6.29 TB/s).  Each lane moves U 16-byte units per trip, a wave 1 KiB a unit row, all U loads issued
+// before the stores; a grid of `blocks` workgroups of 256 threads strides over the buffer.
+// VARIANT: 0 non-temporal loads and stores, 1 cached loads and stores, 2 non-temporal loads with
+// cached stores.  n must be a multiple of 16 (the caller copies the tail, if any, itself).
+template <int U, int VARIANT>
+__global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * U;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256u * U + threadIdx.x; b < n16; b += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t i = b + 256u * k;
+            if (i < n16) v[k] = VARIANT == 1 ? src[i] : __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint64_t i = b + 256u * k;
+            if (i < n16) {
+                if (VARIANT == 0) __builtin_nontemporal_store(v[k], dst + i);
+                else dst[i] = v[k];
+            }
+        }
+    }
+}
+
+// variant as above; u: units per lane per trip (4 or 8); blocks: workgroups (0 = one trip each)
+extern "C" int seq_copy_launch(int variant, int u, uint32_t blocks, void* dst, const void* src, uint64_t n, void* stream) {
+    if (n & 15u) return (int)hipErrorInvalidValue;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t n16 = n >> 4;
+    const uint64_t per = 256u * (uint64_t)(u == 8 ? 8 : 4);
+    const uint32_t g = blocks ? blocks : (uint32_t)((n16 + per - 1u) / per);
+    u32x4* d = static_cast<u32x4*>(dst);
+    const u32x4* sr = static_cast<const u32x4*>(src);
+#define SC(UU, VV) hipLaunchKernelGGL((seq_copy<UU, VV>), dim3(g), dim3(256), 0, s, d, sr, n16)
+    if (u == 8) {
+        if (variant == 0) SC(8, 0); else if (variant == 1) SC(8, 1); else SC(8, 2);
+    } else {
+        if (variant == 0) SC(4, 0); else if (variant == 1) SC(4, 1); else SC(4, 2);
+    }
+#undef SC
+    return (int)hipGetLastError();
+}

@@ -39,6 +39,9 @@ def main():
     batch.set_reasm_flat(a.reasm_flat)
     dev = torch.device("cuda:0")
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "bin", "libgather_ceiling.so"))
+    lib.seq_copy_launch.restype = ctypes.c_int
+    lib.seq_copy_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint64, ctypes.c_void_p]
     lib.gather_ceiling_launch.restype = ctypes.c_int
     lib.gather_ceiling_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4 + \
         [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
@@ -82,6 +85,13 @@ def main():
         (buf, d_desc, d_grp, out, d_od, nfr, payload), _, _ = sets[i % a.rotate]
         out[:payload].copy_(buf[:payload])
 
+    def seq_copy(var, u, blocks):             # the hand-written sequential copy (bench.copy_ceiling)
+        def f(i):
+            (buf, d_desc, d_grp, out, d_od, nfr, payload), _, _ = sets[i % a.rotate]
+            assert lib.seq_copy_launch(var, u, blocks, out.data_ptr(), buf.data_ptr(), payload & ~15,
+                                       ctypes.c_void_p(s.cuda_stream)) == 0
+        return f
+
     def timed(f):
         for i in range(5):
             f(i)
@@ -98,7 +108,9 @@ def main():
     res = {}
     fns = (("reassemble", reasm),) if a.only_reasm else (
         ("reassemble", reasm), ("bare_gather", gather(0)), ("bare_gather_4frag_steps", gather(1)),
-        ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)), ("sequential_copy", copy))
+        ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)), ("sequential_copy_torch", copy),
+        ("sequential_copy_nt", seq_copy(0, 4, 0)), ("sequential_copy_cached", seq_copy(1, 4, 0)),
+        ("sequential_copy_nt_grid", seq_copy(0, 4, 8192)))
     for rnd in range(3):
         for name, f in fns:
             res.setdefault(name, []).append(timed(f))
