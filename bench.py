@@ -114,6 +114,9 @@ CONFIGS = {
                          workload="C3 reassembly over a 576 B MTU: 4K x 64512 B IPv4/TCP datagrams arriving as 552 B "
                                   "fragments (117 per datagram: past the flat grid's 64 a wave, one workgroup per "
                                   "datagram), otherwise as c3_reasm"),
+    "c3_reasm_retx": dict(kind="frag", frames=4096, frame_bytes=64512, retx=True,
+                          workload="C3 reassembly with retransmissions: as c3_reasm, every datagram's middle "
+                                   "fragment arriving a second time, last (45 fragments, one repeated offset each)"),
     "c3": dict(kind="uniform", frames=262144, frame_bytes=9000,
                workload="C3: 256K x 9000 B jumbo frames, raw pico_checksum per frame"),
     "c3_64k": dict(kind="uniform", frames=16384, frame_bytes=65536,
@@ -215,10 +218,12 @@ FRAG = 1480                 # IPv4 fragment payload (MTU 1500 - 20 B header)
 FRAG6 = 1448                # IPv6 fragment payload (MTU 1500 - 40 B header - 8 B fragment header, 8-aligned)
 
 
-def make_frag(n, tl, device, seed, v6=False, interleave=False, frag_payload=0):
+def make_frag(n, tl, device, seed, v6=False, interleave=False, frag_payload=0, retx=False):
     """n IPv4/TCP (IPv6/TCP) datagrams of tl transport bytes as in-order 1480 B (1448 B)
     fragments (frag_payload: another payload size, a multiple of 8), each behind a 14 B gap, built
     on the device (vectorized); the TCP checksum made valid with one untimed reassembly pass.
+    retx: every datagram's middle fragment arrives a second time, last (a retransmission: the same
+    bytes, a repeated offset the reference's fragment tree rejects).
     Returns (buffer, fragment descriptors, groups, out, out descriptors, fragment count, payload
     bytes)."""
     fr, hl = (FRAG6, 48) if v6 else (FRAG, 20)
@@ -265,8 +270,15 @@ def make_frag(n, tl, device, seed, v6=False, interleave=False, frag_payload=0):
     buf[idx] = torch.from_numpy(hdr.reshape(-1)).to(device)
     crc = torch.from_numpy(np.stack([net[::nf] + hl + 16, net[::nf] + hl + 17], 1).reshape(-1)).to(device)
     buf[crc] = 0                                         # TCP crc of each datagram (first fragment)
-    desc = batch.make_desc(net.astype(np.uint64), np.repeat(tot[None, :], n, 0).reshape(-1))
-    grp = np.stack([np.arange(n) * nf, np.full(n, nf)], 1).astype(np.uint32).reshape(-1)
+    flen = np.repeat(tot[None, :], n, 0)
+    if retx:                                             # + fragment nf // 2 again, last
+        net2 = np.concatenate([net.reshape(n, nf), net.reshape(n, nf)[:, nf // 2:nf // 2 + 1]], 1).reshape(-1)
+        flen = np.concatenate([flen, flen[:, nf // 2:nf // 2 + 1]], 1)
+        desc = batch.make_desc(net2.astype(np.uint64), flen.reshape(-1))
+        grp = np.stack([np.arange(n) * (nf + 1), np.full(n, nf + 1)], 1).astype(np.uint32).reshape(-1)
+    else:
+        desc = batch.make_desc(net.astype(np.uint64), flen.reshape(-1))
+        grp = np.stack([np.arange(n) * nf, np.full(n, nf)], 1).astype(np.uint32).reshape(-1)
     H = 40 if v6 else 20
     cap = (H + tl + 15) // 16 * 16 + 16
     # each reassembled datagram at (16 - H % 16) mod 16, so that its transport (behind the H B
@@ -276,12 +288,13 @@ def make_frag(n, tl, device, seed, v6=False, interleave=False, frag_payload=0):
     d_grp = torch.from_numpy(grp.view(np.int32)).to(device)
     out = torch.empty(n * cap, dtype=torch.uint8, device=device)
     fn = batch.ipv6_reassemble_batch if v6 else batch.ipv4_reassemble_batch
-    _, l4, _ = fn(buf, d_desc, n * nf, d_grp, out, d_od)
+    nfr = n * (nf + 1) if retx else n * nf
+    _, l4, _ = fn(buf, d_desc, nfr, d_grp, out, d_od)
     c = l4.view(torch.int16).to(torch.int32) & 0xFFFF                # value to store: short_be(c)
     buf[crc[0::2]] = (c >> 8).to(torch.uint8)
     buf[crc[1::2]] = (c & 0xFF).to(torch.uint8)
     torch.cuda.synchronize(device)
-    return buf, d_desc, d_grp, out, d_od, n * nf, n * tl
+    return buf, d_desc, d_grp, out, d_od, nfr, n * tl
 
 
 def cpu_model() -> str:
@@ -492,7 +505,7 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
         grp = gr.cpu().numpy().view(np.uint32)[:2 * k]
         nf_used = int(grp[-2] + grp[-1])
         desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
-        hi = int(desc["off"][-1]) + int(desc["len"][-1])
+        hi = int((desc["off"] + desc["len"].astype(np.uint64)).max())     # (retx: the last descriptor is a repeat)
         odh = od.cpu().numpy().view(batch.DESC_DTYPE)[:k]
         outh = np.zeros(int(odh["off"][-1]) + int(odh["len"][-1]), np.uint8)
         v6 = bool(cfg.get("v6"))
@@ -854,8 +867,8 @@ def main():
         n, ln = cfg["frames"], cfg["frame_bytes"]
         rot = a.rotate or max(2, rotation(2 * n * ln))
         v6 = bool(cfg.get("v6"))
-        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6, bool(cfg.get("interleave")), cfg.get("frag_payload", 0))
-                for i in range(rot)]
+        sets = [make_frag(n, ln, dev, 900 + 13 * rank + i, v6, bool(cfg.get("interleave")), cfg.get("frag_payload", 0),
+                          bool(cfg.get("retx"))) for i in range(rot)]
         res = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(rot)]
 

@@ -12,11 +12,11 @@
 // the whole transport again; here one pass reads each fragment's payload once, writes it to
 // its place in the reassembled datagram and adds it to the checksum on the way.
 //
-// Batches of >= 512 datagrams take the flat grid (reasm_flat_kernel, below: the gather spread
-// over ~one wave per four fragments, each datagram finished by the last of its waves to arrive; a
-// datagram of more than 64 fragments is taken by one of its waves on the one-wave path).
-// Otherwise one workgroup (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its
-// fragments are a contiguous descriptor range, in arrival order):
+// Batches of >= 512 datagrams take the flat grid (reasm_flat_kernel + the finish, below:
+// the gather spread over ~one wave per four fragments, the plan and the sums brought together
+// after it).  Otherwise -- and for a flat-grid datagram the plan could not settle -- one workgroup
+// (4 waves; 1 wave in batches of >= 3072 datagrams) per datagram (its fragments are a contiguous
+// descriptor range, in arrival order):
 //   1. all threads parse the fragment headers (IPv4: IHL, total length, MF, offset; IPv6: the
 //      extension-header walk, payload length, M, offset, protocol) into LDS and
 //      mark repeated offsets (pico_tree_insert rejects a repeated key: the earliest arrival
@@ -97,13 +97,22 @@ struct FragArgs {
     uint32_t* o_len;
     uint16_t* o_l4;
     uint8_t* verdict;
-    // flat grid (reasm_flat_kernel): S waves per datagram, one tally per datagram
-    // {waves arrived << 32 | their partial sums}, zero between launches
-    uint64_t* tally;
+    // flat grid (reasm_flat_kernel, then reasm_finish_kernel): S waves per datagram,
+    // one plan per datagram, one partial sum per wave
+    struct ReasmPlan* plan;
+    uint32_t* slot;
     uint32_t S;
 };
 
-constexpr uint32_t FLAT_MAXF = 64u;          // fragments a flat-grid wave holds (one per lane)
+// A datagram's plan, written by its planner: GOOD (complete: the finish adds the waves' partial
+// sums, less corr -- the sums of retransmitted fragments the gather waves gathered a second time),
+// BAD (not reassembled) or SLOW (a repeated offset whose later arrival differs from the kept one,
+// or more than FLAT_MAXF fragments: the finish runs the one-workgroup path over the datagram again).
+struct ReasmPlan {
+    uint32_t state, len, proto, pseudo, w0, w1, corr, pad;
+};
+constexpr uint32_t PLAN_GOOD = 0u, PLAN_BAD = 1u, PLAN_SLOW = 2u;
+constexpr uint32_t FLAT_MAXF = 64u;          // fragments a plan holds (one per lane)
 #ifndef REASM_NP4
 #define REASM_NP4 2u
 #endif
@@ -113,6 +122,14 @@ constexpr uint32_t FLAT_MAXF = 64u;          // fragments a flat-grid wave holds
 // fragment pairs a flat-grid wave gathers at once (their loads in flight together): IPv4 2
 // (3: 113.2 vs 113.4 us, no gain), IPv6 3 (120.9 us; 2: 128.0, 4: 122.2 at 118 VGPRs)
 __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 : REASM_NP4; }
+// Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
+// c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
+// 130.5 / 143.6 -- the planners then end in the launch's tail)
+__host__ __device__ __forceinline__ uint32_t plan_per(uint32_t n_dgram) {
+    const uint32_t q = n_dgram / 512u;
+    return q < 1u ? 1u : (q > 8u ? 8u : q);
+}             // fragment pairs a flat-grid wave gathers at once
+
 struct FragLds {
     uint32_t key[FRAG_MAX];   // offset | MF << 16 | dup << 24
     uint32_t tl[FRAG_MAX];    // transport length
@@ -204,6 +221,35 @@ __device__ __forceinline__ bool frag_parse_pre(const FragArgs& p, const pico_csu
         pr = ((uint32_t)w >> 24) & 0xFFu;
         return (int)(w & 0xFFu) - 1 == WALK_FRAG && hl + tl <= d.len;
     }
+}
+
+// The flat grid's header reads: lane's fragment descriptor p.frag[idx] (in: the lane has one), then
+// its header's first 16 bytes (IPv6: also bytes 40..55) in one load each through a window over
+// the batch from 1 GiB below the wave's first fragment, parsed by frag_parse_pre (a header
+// outside the window: frag_parse's byte loads).  Returns frag_parse's verdict (true without one).
+template <bool V6>
+__device__ __forceinline__ bool parse_lane(const FragArgs& p, bool in, uint32_t idx, uint64_t& off, uint32_t& key,
+                                           uint32_t& tl, uint32_t& hl, uint32_t& pr) {
+    pico_csum_desc_dev d{0, 0, 0};
+    if (in) d = p.frag[idx];
+    off = d.off;
+    key = tl = hl = pr = 0;
+#ifdef REASM_BYTE_PARSE
+    return in ? frag_parse<V6>(p, d, key, tl, hl, pr) : true;
+#else
+    const uint64_t act = __builtin_amdgcn_ballot_w64(in);
+    const int f = act ? __builtin_ffsll((long long)act) - 1 : 0;
+    const uint64_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, f) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), f) << 32);
+    const uint64_t lo = a0 > (1ull << 30) ? (a0 - (1ull << 30)) & ~(uint64_t)15 : 0ull;
+    const uint64_t wsz = p.base_len > lo ? min(p.base_len - lo, (uint64_t)0x7FFFFFF0u) : 0ull;
+    const Window hw = make_window(reinterpret_cast<uint64_t>(p.base) + lo, (uint32_t)wsz);
+    const bool pre = in && off >= lo && off - lo + (V6 ? 56u : 16u) <= wsz;
+    const uint32_t v = pre ? (uint32_t)(off - lo) : WIN_OOB;
+    const uint4 v0 = load_win<false>(hw, v);
+    const uint4 v40 = V6 ? load_win<false>(hw, pre ? v + 40u : WIN_OOB) : make_uint4(0, 0, 0, 0);
+    return in ? frag_parse_pre<V6>(p, d, pre, v0, v40, key, tl, hl, pr) : true;
+#endif
 }
 
 // pico_transport_crc_check on the reassembled frame (ICMPv6: pico_icmp6_process_in): s = the
@@ -575,23 +621,184 @@ __global__ __launch_bounds__(64 * WPD) void reassemble_kernel(FragArgs p) {
     if (blockIdx.x < p.n_dgram) reassemble_one<V6, WPD>(p, blockIdx.x, L);
 }
 
+// The flat grid's finish: a workgroup of 4 waves per 64 datagrams.  Wave 0, one lane per datagram,
+// gives a GOOD or BAD plan its results from the plan and the S partial sums; then all 4 waves run
+// the workgroup path (reassemble_one, 4 waves) over each SLOW datagram of the 64 in turn.  (Round 5:
+// one wave per 64 datagrams, its SLOW datagrams on the one-wave path: a batch whose every datagram
+// held a retransmitted fragment took 2556 us against 228 us for a workgroup per datagram, and that
+// costs c3_reasm ~3 us; profiles/r06/README_reasm.md.)
+#ifndef REASM_FINISH_WAVES
+#define REASM_FINISH_WAVES 4
+#endif
+template <bool V6>
+__global__ __launch_bounds__(64 * REASM_FINISH_WAVES) void reasm_finish_kernel(FragArgs p) {
+    __shared__ FragLds L;
+    __shared__ uint64_t slow_s;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, g0 = blockIdx.x * 64u, g = g0 + lane;
+    if (tid < 64u) {
+        const bool in = g < p.n_dgram;
+        uint32_t state = PLAN_SLOW;
+        if (in) {
+            const ReasmPlan r = p.plan[g];
+            state = r.state;
+            if (state != PLAN_SLOW) {
+                uint32_t sum = 0u - r.corr;
+                for (uint32_t k = 0; k < p.S; ++k) sum += p.slot[(uint64_t)g * p.S + k];
+                uint32_t l4 = 0, v = V_MALFORMED;
+                if (state == PLAN_GOOD) v = reasm_verdict<V6>(p.flags, r.len, r.proto, r.pseudo, sum, r.w0, r.w1, l4);
+                if (p.o_len) p.o_len[g] = state == PLAN_GOOD ? r.len : 0u;
+                if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
+                if (p.verdict) p.verdict[g] = (uint8_t)v;
+            }
+        }
+        const uint64_t slow = __builtin_amdgcn_ballot_w64(in && state == PLAN_SLOW);
+        if (lane == 0) slow_s = slow;
+    }
+    __syncthreads();
+    uint64_t slow = slow_s;
+    while (slow) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(slow);
+        slow &= slow - 1u;
+        reassemble_one<V6, REASM_FINISH_WAVES>(p, g0 + j, L);
+        __syncthreads();                              // L is the next one's
+    }
+}
+
 // ---------------------------------------------------------------- flat grid
 //
-// Large batches: S one-wave workgroups per datagram (S ~ its fragments / 4 for IPv4, / 6 for IPv6),
-// no planner and no second launch.  Every wave of a datagram reads all of the datagram's fragment
-// headers, one per lane (one round trip; the S waves read the same lines), gathers its own
-// fragments at their own offsets -- skipping a repeated offset's later arrivals, as pico_tree_insert
-// does -- and adds {1 << 32 | its partial sum} to the datagram's tally with one 64-bit atomic.  The
-// wave that brings the tally to S is the last arriver: it holds every header in its lanes, so it
-// checks completeness (pico_fragments_check_complete), copies the first fragment's header and
-// writes the results from the total the atomic returned, then zeroes the tally for the next launch.
-// Nobody waits on another wave.  (The transport is < 64 KiB, so the sum of its 16-bit words never
-// reaches bit 32 and cannot carry into the count.)  A datagram of more than FLAT_MAXF fragments
-// takes the one-wave LDS path in its wave s = 0 (the other waves return).
-//
-// Round 5 ran planners dispatched ahead of the gather waves and a finish launch that added the
-// partial sums and re-gathered datagrams with repeated offsets one at a time, 64 per finish wave
-// (c3_reasm 110.1 / c3_reasm6 118.0 us; the finish launch alone 4.9 us of trace time).
+// Large batches: S one-wave workgroups per datagram (S ~ its fragments / 4), each gathering
+// fragments 4 s, ... of its datagram at their own offsets straight from their own headers, so the
+// dispatcher balances the gather over the whole batch instead of one wave walking a whole
+// datagram; planner workgroups dispatched ahead of them plan the datagrams (a datagram's fragments
+// one per lane: dedup, completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
+// (reasm_finish_kernel) adds them.  A datagram with repeated offsets or more than
+// FLAT_MAXF fragments is gathered again there by the one-wave path (its flat-grid bytes may hold
+// a later arrival's copy; the region past the reassembled datagram is unspecified).
+
+// A retransmitted fragment's payload against the kept arrival's (n bytes each from sa / sb, wave-uniform
+// addresses): true when equal; sum = the retransmission's word sum (its payload starts at an even
+// transport offset), which its gather wave added to its slot a second time.  16-byte units through
+// windows over the batch (byte-unaligned loads), the last partial unit by bytes.
+__device__ __forceinline__ bool payload_same(const FragArgs& p, uint64_t sa, uint64_t sb, uint32_t n, uint32_t lane,
+                                             uint32_t& sum) {
+    const uint64_t b0 = reinterpret_cast<uint64_t>(p.base), bend = b0 + p.base_len;
+    const uint64_t wa = sa & ~(uint64_t)15, wb = sb & ~(uint64_t)15;
+    const Window A = make_window(wa, (uint32_t)min(bend - wa, (uint64_t)0x7FFFFFF0u));
+    const Window B = make_window(wb, (uint32_t)min(bend - wb, (uint64_t)0x7FFFFFF0u));
+    const uint32_t full = n >> 4;
+    uint32_t acc = 0;
+    bool diff = false;
+    for (uint32_t u = lane; u < full; u += 64u) {
+        const uint4 x = load_win<false>(A, (uint32_t)(sa - wa) + 16u * u);
+        const uint4 y = load_win<false>(B, (uint32_t)(sb - wb) + 16u * u);
+        diff |= x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+        acc = dot2_add(x.w, dot2_add(x.z, dot2_add(x.y, dot2_add(x.x, acc))));
+    }
+    const uint32_t i = 16u * full + lane;
+    if (lane < (n & 15u)) {
+        const uint32_t x = ld_u8(reinterpret_cast<const uint8_t*>(sa) + i), y = ld_u8(reinterpret_cast<const uint8_t*>(sb) + i);
+        diff |= x != y;
+        acc += x << (8u * (i & 1u));
+    }
+    sum = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
+    return __builtin_amdgcn_ballot_w64(diff) == 0;
+}
+
+// a planner: pico_fragments_check_complete on registers (lane j: fragment j).  A repeated offset's
+// later arrival is not kept (pico_tree_insert rejects a repeated key); the gather waves gathered it
+// too, so it is harmless only when it carries the kept arrival's bytes -- a retransmission: the
+// plan then subtracts its sum (corr) -- else the plan is SLOW.
+template <bool V6>
+__device__ __forceinline__ void plan_datagram(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, bool bad0,
+                                              uint8_t* t, uint32_t cap, uint32_t lane) {
+    constexpr uint32_t HDR = V6 ? 40u : 20u;
+    auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+    uint32_t state = PLAN_BAD, len = 0, proto = 0, pseudo = 0, w0 = 0, w1 = 0, corr = 0;
+    if (!bad0 && cnt > FLAT_MAXF) {
+        state = PLAN_SLOW;
+    } else if (!bad0) {
+        const bool in = lane < cnt;
+        uint32_t key, tl, hl, pr;
+        uint64_t off;
+        const bool ok = parse_lane<V6>(p, in, first + lane, off, key, tl, hl, pr);
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+            const uint32_t o = key & 0xFFFFu;
+            uint32_t P = 0, rank = 0;                 // transport bytes / kept fragments below this offset
+            uint32_t orig = lane;                     // the earliest arrival with this offset
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t kk = rl(key, k) & 0xFFFFu, tk = rl(tl, k);
+                orig = k < orig && kk == o ? k : orig;
+                P += kk < o ? tk : 0u;
+                rank += kk < o ? 1u : 0u;
+            }
+            const bool kept = in && orig == lane;
+            const uint64_t km = __builtin_amdgcn_ballot_w64(kept);
+            const uint64_t dups = __builtin_amdgcn_ballot_w64(in && !kept);
+            if (dups) {                               // (rare) P and rank over the kept arrivals only
+                P = rank = 0;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const uint32_t kk = rl(key, k) & 0xFFFFu, tk = rl(tl, k);
+                    const bool below = ((km >> k) & 1u) && kk < o;
+                    P += below ? tk : 0u;
+                    rank += below ? 1u : 0u;
+                }
+            }
+            // retransmissions: the same length and bytes as the kept arrival, else SLOW
+            bool slow = false;
+            const uint64_t src = reinterpret_cast<uint64_t>(p.base) + off + hl;
+            for (uint64_t dm = dups; dm && !slow; dm &= dm - 1u) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(dm), j = rl(orig, k), n = rl(tl, k);
+                uint32_t sk = 0;
+                slow = n != rl(tl, j) ||
+                       !payload_same(p, ((uint64_t)rl((uint32_t)(src >> 32), k) << 32) | rl((uint32_t)src, k),
+                                     ((uint64_t)rl((uint32_t)(src >> 32), j) << 32) | rl((uint32_t)src, j), n, lane, sk);
+                corr += sk;
+            }
+            const uint32_t m = (uint32_t)__builtin_popcountll(km);
+            if (slow) {
+                state = PLAN_SLOW;
+            } else {
+                // rank = tree position.  Complete: offset == the transport bytes below it up to the
+                // first MF-clear fragment in tree order, which is the last
+                const bool mfc = kept && !(key & (1u << 16));
+                const uint32_t re = 64u - rl(wave_scan_max(mfc ? 64u - rank : 0u), 63);
+                bool b = re >= m || re + 1u != m || __builtin_amdgcn_ballot_w64(kept && rank <= re && o != P) != 0;
+                if (!b) {
+                    const uint32_t le = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(mfc && rank == re));
+                    len = rl(P + tl, le);
+                    b = HDR + len > 0xFFFFu || len > cap;
+                }
+                if (!b) {
+                    // the first fragment's header (pico_fragments.c:332-338), its transport bytes
+                    // 0..7 and the pseudo header's address part (as in reassemble_kernel)
+                    const uint32_t f0 = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kept && o == 0u));
+                    const uint8_t* h0 =
+                        p.base + (((uint64_t)rl((uint32_t)(off >> 32), f0) << 32) | rl((uint32_t)off, f0));
+                    const uint32_t hl0 = rl(hl, f0), tl0 = rl(tl, f0);
+                    const uint32_t hb = lane < HDR ? ld_u8(h0 + lane) : 0u;
+                    if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hb;
+                    const uint32_t tb8 = lane < 8u && lane < tl0 ? ld_u8(h0 + hl0 + lane) : 0u;
+                    w0 = rl(tb8, 0) | (rl(tb8, 1) << 8) | (rl(tb8, 2) << 16) | (rl(tb8, 3) << 24);
+                    w1 = rl(tb8, 4) | (rl(tb8, 5) << 8) | (rl(tb8, 6) << 16) | (rl(tb8, 7) << 24);
+                    if constexpr (!V6) {
+                        proto = (uint32_t)__shfl((int)hb, 9);
+                        const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                        pseudo = rl(group_sum<64>(pw), 63) + (proto << 8) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                    } else {
+                        // the module: the walk's protocol of the latest kept arrival (it completes the
+                        // set, pico_fragments.c:492; reassemble_one's rule)
+                        proto = rl(pr, 63u - (uint32_t)__builtin_clzll(km)) | ((uint32_t)__shfl((int)hb, 9) << 8);
+                        const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                        pseudo = rl(group_sum<64>(pw), 63) + (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) +
+                                 (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                    }
+                    state = PLAN_GOOD;
+                }
+            }
+        }
+    }
+    if (lane == 0) p.plan[g] = ReasmPlan{state, len, proto, pseudo, w0, w1, corr, 0u};
+}
 
 // One or two fragments' payloads gathered into the transport at tb (fragment A: transport bytes
 // [ata, ata + ta) from address srcA; B likewise when nb_on), in 16-byte units on the output's lines
@@ -715,129 +922,71 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
     return acc;
 }
 
-// The flat grid's waves (gather, tally, and for the last arriver the finish).  Payload loads are
-// cached, not non-temporal: the byte-unaligned 16-byte loads of neighbouring units share lines
-// (round 5: 113.8 -> 108.9 us, IPv6 121.3 -> 118.3).  Pairs in flight per wave: IPv4 2, IPv6 3
-// (round 5: IPv6 two 128.0, three 120.9, four 122.2 us).
+// The flat grid: planner workgroups, then S one-wave workgroups per datagram; wave s takes
+// fragments FPI s, ... in groups
+// of FPI = 2 flat_np (its pairs' loads in flight together).  c3_reasm (profiles/r05/ab_reasm_flat.txt):
+// 115.4 us against 124.0 us for one workgroup per datagram; one pair a wave 124.7 us (per wave the
+// descriptor and header round trips come before its loads), four pairs 127 us (124 VGPRs); 5, 6
+// or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
+// 115.7 at 4 (105 VGPRs).  The payload loads are cached, not non-temporal: the byte-unaligned
+// 16-byte loads of neighbouring units share lines (113.8 -> 108.9 us, IPv6 121.3 -> 118.3).
 template <bool V6>
 __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
-    __shared__ FragLds L;                             // the > FLAT_MAXF path only
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.S;
-#ifdef REASM_XCD
-    // blocks b = 8 (q S + s) + x serve datagram g = 8 q + x: blocks b and b + 8 share an XCD (the
-    // dispatcher deals blocks round-robin over the 8 XCDs; speed only), so a datagram's S waves share
-    // one L2 for the headers every one of them reads
-    const uint32_t xb = blockIdx.x & 7u, rb = blockIdx.x >> 3;
-    const uint32_t qg = rb / S, s = rb - qg * S, g = 8u * qg + xb;
-#else
-    const uint32_t g = blockIdx.x / S, s = blockIdx.x - g * S;
-#endif
+    // Workgroups [0, npl) plan plan_per datagrams each and gather nothing -- dispatched first, so
+    // no plan lands in the launch's tail and the planners hold few of the slots (with the plan in
+    // each datagram's wave 0 instead: c3_reasm6 152.9 us, c3_reasm 115.3); the rest gather, S per
+    // datagram.
+    const uint32_t per = plan_per(p.n_dgram), npl = (p.n_dgram + per - 1u) / per;   // planner workgroups
+    if (blockIdx.x < npl) {                           // per datagrams in turn
+        for (uint32_t g = blockIdx.x * per; g < min(p.n_dgram, (blockIdx.x + 1u) * per); ++g) {
+            const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
+            const pico_csum_desc_dev od = p.odesc[g];
+            const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
+                              (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off ||
+                              od.len < HDR;
+            plan_datagram<V6>(p, g, first, cnt, bad0, p.out + od.off + HDR, od.len - HDR, lane);
+        }
+        return;
+    }
+    const uint32_t gb = blockIdx.x - npl;
+    const uint32_t g = gb / S, s = gb - g * S;
     if (g >= p.n_dgram) return;
     const uint32_t first = p.grp[2 * g], cnt = p.grp[2 * g + 1];
     const pico_csum_desc_dev od = p.odesc[g];
     const bool bad0 = cnt == 0 || cnt > FRAG_MAX || first > p.n_frag || cnt > p.n_frag - first ||
                       (od.off & 3u) != 0 || od.off > p.out_len || od.len > p.out_len - od.off || od.len < HDR;
-    auto put = [&](uint32_t len, uint32_t l4, uint32_t v) {
-        if (p.o_len) p.o_len[g] = len;
-        if (p.o_l4) p.o_l4[g] = (uint16_t)l4;
-        if (p.verdict) p.verdict[g] = (uint8_t)v;
-    };
-    if (bad0) {
-        if (s == 0 && lane == 0) put(0u, 0u, V_MALFORMED);
-        return;
-    }
-    if (cnt > FLAT_MAXF) {
-#ifndef REASM_ABL_NOLDS
-        if (s == 0) reassemble_one<V6, 1>(p, g, L);
-#endif
-        return;
-    }
     uint8_t* t = p.out + od.off + HDR;
     const uint32_t cap = od.len - HDR;
-    auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
-
-    // ---- every fragment's header, lane j = fragment j: its first 16 bytes (IPv6 also 40..55) in
-    //      one load each through a window over the batch from 1 GiB below the first fragment
-    //      (a header outside it: frag_parse's byte loads)
-    const bool in = lane < cnt;
-    uint32_t key = 0, tl = 0, hl = 0, pr = 0;
-    uint64_t off = 0;
-    bool ok = true;
-    {
-        pico_csum_desc_dev d{0, 0, 0};
-        if (in) d = p.frag[first + lane];
-        off = d.off;
-        const uint64_t a0 = rl((uint32_t)off, 0) | ((uint64_t)rl((uint32_t)(off >> 32), 0) << 32);
-        const uint64_t lo = a0 > (1ull << 30) ? (a0 - (1ull << 30)) & ~(uint64_t)15 : 0ull;
-        const uint64_t wsz = p.base_len > lo ? min(p.base_len - lo, (uint64_t)0x7FFFFFF0u) : 0ull;
-        const Window hw = make_window(reinterpret_cast<uint64_t>(p.base) + lo, (uint32_t)wsz);
-        const bool pre = in && off >= lo && off - lo + (V6 ? 56u : 16u) <= wsz;
-        const uint32_t v = pre ? (uint32_t)(off - lo) : WIN_OOB;
-        const uint4 v0 = load_win<false>(hw, v);
-        const uint4 v40 = V6 ? load_win<false>(hw, pre ? v + 40u : WIN_OOB) : make_uint4(0, 0, 0, 0);
-        if (in) ok = frag_parse_pre<V6>(p, d, pre, v0, v40, key, tl, hl, pr);
-    }
-    if (__builtin_amdgcn_ballot_w64(!ok)) {           // a malformed fragment: not reassembled
-        if (s == 0 && lane == 0) put(0u, 0u, V_MALFORMED);
-        return;
-    }
-    const uint32_t o = key & 0xFFFFu;
-    const uint64_t src = reinterpret_cast<uint64_t>(p.base) + off + hl;
-    // the first fragment (offset 0; the earliest arrival if repeated): its header bytes and the
-    // transport's bytes 0..7, loaded now for the last arriver (lanes [0, HDR) the header, lanes
-    // [HDR, HDR + 8) the transport bytes), in flight beside the gather
-    const uint64_t z = __builtin_amdgcn_ballot_w64(in && o == 0u);
-    const uint32_t f0 = z ? (uint32_t)__builtin_ctzll(z) : 0u;
-    uint32_t hbt = 0;
-    if (z) {
-        const uint8_t* h0 = p.base + (((uint64_t)rl((uint32_t)(off >> 32), f0) << 32) | rl((uint32_t)off, f0));
-        const uint32_t hl0 = rl(hl, f0), tl0 = rl(tl, f0);
-        if (lane < HDR) hbt = ld_u8(h0 + lane);
-        else if (lane < HDR + 8u && lane - HDR < tl0) hbt = ld_u8(h0 + hl0 + (lane - HDR));
-    }
-
-    // ---- this wave's fragments FPI s, ... (FPI = 2 NP), NP pairs' loads in flight together; the
-    //      tally's atomic goes out before the last step's stores, so the wave waits for its
-    //      return, not for its stores (vmcnt counts both, in issue order)
     uint32_t acc = 0;
-    uint64_t before = 0;
-    auto tally = [&]() {
-        const uint32_t tot = rl(group_sum<64>(acc), 63);
-        acc = tot;
-        if (lane == 0)
-            before = __hip_atomic_fetch_add(p.tally + g, (1ull << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("" ::: "memory");
-    };
-    {
+    if (!bad0 && cnt <= FLAT_MAXF) {
         const uint64_t tb = reinterpret_cast<uintptr_t>(t);
         const Window ow = make_window(tb, cap);
-        constexpr uint32_t NP = flat_np(V6), FPI = 2u * NP;
-        uint32_t j0 = FPI * s;
-        if (j0 >= cnt) tally();
-        for (; j0 < cnt; j0 += FPI * S) {
-            const bool lastit = j0 + FPI * S >= cnt;
-            // gathered: parsed (all are), the first arrival of its offset, held by the output region
-            uint64_t m = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < FPI; ++q) {
-                const uint32_t j = j0 + q;
-                if (j < cnt) {
-                    const uint32_t oj = rl(o, j);
-                    const bool dup = __builtin_amdgcn_ballot_w64(lane < j && o == oj) != 0;
-                    if (!dup && oj + rl(tl, j) <= cap) m |= 1ull << q;
-                }
-            }
+        auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+        constexpr uint32_t NP = flat_np(V6), FPI = 2u * NP;      // pairs / fragments per iteration
+        for (uint32_t j0 = FPI * s; j0 < cnt; j0 += FPI * S) {
+            // lanes 0..FPI-1 read fragments j0, ..., j0 + FPI - 1; a fragment is gathered when it
+            // parses and the output region holds it (repeated offsets too: SLOW plans are gathered
+            // again); the NP pairs' loads are in flight at once
+            const uint32_t j = j0 + lane;
+            uint32_t key, tl, hl, pr;
+            uint64_t off;
+            const bool in = lane < FPI && j < cnt;
+            const bool parsed = parse_lane<V6>(p, in, first + j, off, key, tl, hl, pr);
+            const bool ok = in && parsed && (key & 0xFFFFu) + tl <= cap;
+            const uint64_t src = reinterpret_cast<uint64_t>(p.base + off) + hl;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
             PairStep ps[NP];
             bool one = true;                  // every pair in one step of 3 x 64 units
 #pragma unroll
             for (uint32_t q = 0; q < NP; ++q) {
-                const uint32_t la = min(j0 + 2u * q, 63u), lb = min(j0 + 2u * q + 1u, 63u);
+                const uint32_t la = 2u * q, lb = la + 1u;
                 const uint64_t sA = ((uint64_t)rl((uint32_t)(src >> 32), la) << 32) | rl((uint32_t)src, la);
                 const uint64_t sB = ((uint64_t)rl((uint32_t)(src >> 32), lb) << 32) | rl((uint32_t)src, lb);
-                const uint32_t aA = rl(o, la), aB = rl(o, lb), tA = rl(tl, la), tB = rl(tl, lb);
-                const bool vA = (m >> (2u * q)) & 1u, vB = (m >> (2u * q + 1u)) & 1u;
+                const uint32_t aA = rl(key, la) & 0xFFFFu, aB = rl(key, lb) & 0xFFFFu, tA = rl(tl, la), tB = rl(tl, lb);
+                const bool vA = (m >> la) & 1u, vB = (m >> lb) & 1u;
                 if (vA && vB && max64s(sA + tA, sB + tB) - min64s(sA, sB) < (1ull << 30)) {
                     ps[q] = pair_prep(tb, sA, aA, tA, true, sB, aB, tB);
                 } else if (vA) {
@@ -856,82 +1005,19 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
 #pragma unroll
                 for (uint32_t q = 0; q < NP; ++q) pair_issue<3>(ps[q], lane, 0u, c[q]);
 #pragma unroll
-                for (uint32_t q = 0; q < NP; ++q) acc = pair_sum<3>(ps[q], lane, 0u, c[q], acc);
-                if (lastit) tally();
-#pragma unroll
-                for (uint32_t q = 0; q < NP; ++q) pair_store<3>(ps[q], ow, lane, 0u, c[q]);
+                for (uint32_t q = 0; q < NP; ++q) acc = pair_process<3>(ps[q], ow, lane, 0u, c[q], acc);
             } else {
 #pragma unroll
                 for (uint32_t q = 0; q < NP; ++q) acc = pair_gather(ps[q], ow, lane, acc);
-                if (lastit) tally();
             }
         }
     }
-
-    // ---- the tally: the wave that brings it to S finishes the datagram
-#ifdef REASM_ABL_NOATOM
-    if (lane == 0 && s == 0) p.o_len[g] = (uint32_t)(__builtin_amdgcn_readfirstlane(hbt));
-    return;
-#endif
-    before = ((uint64_t)rl((uint32_t)(before >> 32), 0) << 32) | rl((uint32_t)before, 0);
-    if ((uint32_t)(before >> 32) != S - 1u) return;
-    const uint32_t sum = (uint32_t)before + acc;      // (acc: this wave's total, from tally())
-
-    // ---- the last arriver: pico_fragments_check_complete over the kept fragments (earliest arrival
-    //      of each offset), in tree order by rank; complete when every offset up to the first
-    //      MF-clear fragment equals the transport bytes below it and that fragment is the last
-    bool dup = false;
-    uint32_t P = 0, rank = 0;
-    for (uint32_t k = 0; k < cnt; ++k) dup |= k < lane && rl(o, k) == o;
-    const bool kept = in && !dup;
-    const uint64_t km = __builtin_amdgcn_ballot_w64(kept);
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t ok_ = rl(o, k), tk = rl(tl, k);
-        const bool below = ((km >> k) & 1u) && ok_ < o;
-        P += below ? tk : 0u;
-        rank += below ? 1u : 0u;
-    }
-    const uint32_t mkept = (uint32_t)__builtin_popcountll(km);
-    const bool mfc = kept && !(key & (1u << 16));
-    const uint32_t re = 64u - rl(wave_scan_max(mfc ? 64u - rank : 0u), 63);
-    bool b = !z || re >= mkept || re + 1u != mkept || __builtin_amdgcn_ballot_w64(kept && rank <= re && o != P) != 0;
-    uint32_t len = 0;
-    if (!b) {
-        const uint32_t le = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(mfc && rank == re));
-        len = rl(P + tl, le);
-        b = HDR + len > 0xFFFFu || len > cap;
-    }
-    if (b) {
-        if (lane == 0) put(0u, 0u, V_MALFORMED);
-    } else {
-        // the first fragment's PICO_SIZE_IP4HDR / PICO_SIZE_IP6HDR bytes (pico_fragments.c:332-338),
-        // the transport's bytes 0..7 and the pseudo header's address part (as reassemble_one)
-        if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hbt;
-        const uint32_t w0 = rl(hbt, HDR) | (rl(hbt, HDR + 1u) << 8) | (rl(hbt, HDR + 2u) << 16) | (rl(hbt, HDR + 3u) << 24);
-        const uint32_t w1 = rl(hbt, HDR + 4u) | (rl(hbt, HDR + 5u) << 8) | (rl(hbt, HDR + 6u) << 16) | (rl(hbt, HDR + 7u) << 24);
-        const uint32_t hb = lane < HDR ? hbt : 0u;
-        uint32_t proto, pseudo;
-        if constexpr (!V6) {
-            proto = rl(hb, 9);
-            const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
-            pseudo = rl(group_sum<64>(pw), 63) + (proto << 8) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
-        } else {
-            // the module: the walk's protocol of the latest kept arrival (it completes the set,
-            // pico_fragments.c:492); byte 9 of the copied header rides in bits 8-15
-            proto = rl(pr, 63u - (uint32_t)__builtin_clzll(km)) | (rl(hb, 9) << 8);
-            const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
-            pseudo = rl(group_sum<64>(pw), 63) + (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) +
-                     (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
-        }
-        uint32_t l4 = 0;
-        const uint32_t v = reasm_verdict<V6>(p.flags, len, proto, pseudo, sum, w0, w1, l4);
-        if (lane == 0) put(len, l4, v);
-    }
-    if (lane == 0) p.tally[g] = 0ull;                 // every wave of this launch has arrived
+    acc = (uint32_t)__builtin_amdgcn_readlane((int)group_sum<64>(acc), 63);
+    if (lane == 0) p.slot[(uint64_t)g * S + s] = acc;
 }
 
-// Scratch of the flat grid (one 8-byte tally per datagram, zero between launches: the last
-// arriver of each datagram zeroes its own), never allocated per call (per-call hipMallocAsync /
+// Scratch of the flat grid (plans and partial sums, n_dgram x (32 + 4 S) bytes, every byte written
+// by each launch before it is read), never allocated per call (per-call hipMallocAsync /
 // hipFreeAsync -- alloc / free nodes in a captured graph -- cost c3_reasm ~23 us a call, an event
 // record per call ~24 us: idle device time):
 //  * eager calls: one buffer per calling thread, device and stream, kept across calls and grown
@@ -943,7 +1029,6 @@ __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
 //    on one stream are a chain in the graph), allocated outside the capture's rules and owned by
 //    the graph (a user object; freed by the next eager call, or the next release, after the graph
 //    is destroyed).  Two executable instances of one graph must not run concurrently.
-// A new buffer is zeroed on a private non-blocking stream (no implicit join with a capturing one).
 struct ReasmScratch {
     void* p;
     size_t n;
@@ -1008,23 +1093,6 @@ struct CapScratch {
 thread_local CapScratch t_cap[SCR_SLOTS];
 thread_local int t_cap_next;
 
-int zero_fill(void* p, size_t n) {
-    static std::mutex mu;
-    static hipStream_t zs[64] = {};
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return (int)e;
-    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
-    hipStream_t st;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!zs[dev] && (e = hipStreamCreateWithFlags(&zs[dev], hipStreamNonBlocking)) != hipSuccess) return (int)e;
-        st = zs[dev];
-    }
-    if ((e = hipMemsetAsync(p, 0, n, st)) != hipSuccess) return (int)e;
-    return (int)hipStreamSynchronize(st);
-}
-
 int capture_scratch(hipStream_t s, size_t need, void** out) {
     hipStreamCaptureStatus cs;
     unsigned long long id = 0;
@@ -1042,14 +1110,9 @@ int capture_scratch(hipStream_t s, size_t need, void** out) {
     if ((e = hipThreadExchangeStreamCaptureMode(&mode)) != hipSuccess) return (int)e;
     void* p = nullptr;
     e = hipMalloc(&p, need);
-    int z = e == hipSuccess ? zero_fill(p, need) : 0;
     hipStreamCaptureMode back = mode;
     (void)hipThreadExchangeStreamCaptureMode(&back);
     if (e != hipSuccess) return (int)e;
-    if (z) {
-        scratch_release(p);
-        return z;
-    }
     hipUserObject_t obj;
     if ((e = hipUserObjectCreate(&obj, p, scratch_release, 1, hipUserObjectNoDestructorSync)) != hipSuccess) {
         scratch_release(p);
@@ -1100,12 +1163,6 @@ int reasm_scratch(hipStream_t s, size_t need, void** out) {
             c->p = nullptr;
             return (int)e;
         }
-        int z = zero_fill(c->p, n);
-        if (z) {
-            (void)hipFree(c->p);
-            c->p = nullptr;
-            return z;
-        }
         c->n = n;
         c->stream = s;
         c->dev = dev;
@@ -1136,40 +1193,45 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     if (n_dgram == 0) return (int)hipSuccess;
     FragArgs a{static_cast<const uint8_t*>(base), flags, base_len, static_cast<const pico_csum_desc_dev*>(frag),
                groups, n_dgram, n_frag, static_cast<uint8_t*>(out), out_len,
-               static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict, nullptr, 0u};
+               static_cast<const pico_csum_desc_dev*>(out_desc), o_len, o_l4, verdict, nullptr, nullptr, 0u};
     const hipStream_t s = static_cast<hipStream_t>(stream);
 #ifndef REASM_FLAT_MIN
 #define REASM_FLAT_MIN 512u
 #endif
-    // flat grid from REASM_FLAT_MIN datagrams on (round 5, 64512-byte datagrams, flat vs one
-    // workgroup per datagram: 256 19.2 vs 18.7 us, 512 22.6 vs 23.9, 1024 35.4 vs 36.9;
+    // flat grid from REASM_FLAT_MIN datagrams on (64512-byte datagrams, flat vs one workgroup per
+    // datagram: 256 19.2 vs 18.7 us, 512 22.6 vs 23.9, 1024 35.4 vs 36.9;
     // profiles/r05/ab_reasm_small_batches.txt)
     const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
     // automatic: a batch of more than FLAT_MAXF fragments a datagram on average (64 KiB datagrams
-    // over a small MTU) takes one workgroup per datagram -- the flat grid would give most of its
-    // datagrams to the one-wave path in one of their waves, the others idle
+    // over a small MTU) takes one workgroup per datagram -- on the flat grid most of its datagrams
+    // would be SLOW plans, gathered twice
     if (n_dgram >= fmin && (flat_min || (uint64_t)n_frag <= (uint64_t)FLAT_MAXF * n_dgram)) {
         // S waves per datagram, FPI fragments each on average
         const uint32_t fpi = 2u * flat_np(v6 != 0);
         const uint64_t its = ((uint64_t)n_frag + fpi - 1u) / fpi;
         uint32_t S = (uint32_t)((its + n_dgram - 1u) / n_dgram);
         S = S < 1u ? 1u : (S > 32u ? 32u : S);
-        const size_t need = (size_t)n_dgram * sizeof(uint64_t);
-#ifdef REASM_XCD
-        const uint64_t blocks = (uint64_t)((n_dgram + 7u) / 8u) * 8u * S;
-#else
-        const uint64_t blocks = (uint64_t)n_dgram * S;
-#endif
+        const size_t plan_b = (size_t)n_dgram * sizeof(ReasmPlan), need = plan_b + (size_t)n_dgram * S * 4u;
+        const uint32_t per = plan_per(n_dgram);
+        const uint64_t blocks = (uint64_t)n_dgram * S + (n_dgram + per - 1u) / per;   // planners + gather
         void* scratch = nullptr;
         if (blocks <= 0x7FFFFFFFu && reasm_scratch(s, need, &scratch) == 0) {
-            a.tally = static_cast<uint64_t*>(scratch);
+            a.plan = static_cast<ReasmPlan*>(scratch);
+            a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
             a.S = S;
-            if (v6) hipLaunchKernelGGL((reasm_flat_kernel<true>), dim3((unsigned)blocks), dim3(64), 0, s, a);
-            else hipLaunchKernelGGL((reasm_flat_kernel<false>), dim3((unsigned)blocks), dim3(64), 0, s, a);
+            const dim3 fg((unsigned)blocks), fb(64);
+            if (v6) {
+                hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
+                hipLaunchKernelGGL((reasm_finish_kernel<true>), dim3((n_dgram + 63u) / 64u), dim3(64 * REASM_FINISH_WAVES), 0, s, a);
+            } else {
+                hipLaunchKernelGGL((reasm_flat_kernel<false>), fg, fb, 0, s, a);
+                hipLaunchKernelGGL((reasm_finish_kernel<false>), dim3((n_dgram + 63u) / 64u), dim3(64 * REASM_FINISH_WAVES), 0, s, a);
+            }
             return (int)hipGetLastError();
         }
         // no scratch (out of memory, or a capture state the stream query refuses) or a grid past
-        // 2^31 workgroups: the same results from one workgroup per datagram, which needs none
+        // 2^31 workgroups: the same
+        // results from one workgroup per datagram, which needs none
         (void)hipGetLastError();
     }
     // waves per datagram: 4 each while the batch is small, 1 each once the batch fills the chip's
@@ -1188,3 +1250,4 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
 }
 
 }  // extern "C"
+
