@@ -169,8 +169,8 @@ __device__ __forceinline__ void sorted_rounds(const RawArgs& p, SortedWaveLds& L
 // pico_ethernet.c:180-235) -- IPv4 / IPv6 outputs in the out_net / out_l4 / verdict fields of FlatArgs.
 // Phase 4: lane `lane` finalizes its frame (output index idx) from the LDS state.
 template <int MODE>
-__device__ __forceinline__ uint3 finish_frame(const FlatArgs& p, uint64_t idx, bool tx, uint32_t acc_all,
-                                              uint32_t acc_x, uint32_t acc_opt, uint4 info, uint4 fin, uint32_t xpos) {
+__device__ __forceinline__ void finish_frame(const FlatArgs& p, uint64_t idx, bool tx, uint32_t acc_all,
+                                             uint32_t acc_x, uint32_t acc_opt, uint4 info, uint4 fin, uint32_t xpos) {
     const uint32_t r = info.w & 15u;
     uint8_t* fp = p.base + (((((uint64_t)info.y) << 32) | info.x) + r);
     uint32_t verdict = fin.x & 8u;               // V_MALFORMED from phase 1, or 0
@@ -189,7 +189,6 @@ __device__ __forceinline__ uint3 finish_frame(const FlatArgs& p, uint64_t idx, b
             if ((p.flags & 1u) && xpos != NONE) store_crc(fp + p.crc_off, ret);
         }
         p.out[idx] = (uint16_t)ret;
-        return make_uint3(ret, 0u, 0u);
     } else {
         uint32_t net = 0, l4 = 0;
         if (MODE == 3 && l2v) {
@@ -281,7 +280,6 @@ __device__ __forceinline__ uint3 finish_frame(const FlatArgs& p, uint64_t idx, b
         if (MODE != 2 && p.out_net) p.out_net[idx] = (uint16_t)net;
         if (p.out_l4) p.out_l4[idx] = (uint16_t)l4;
         if (p.verdict) p.verdict[idx] = (uint8_t)verdict;
-        return make_uint3(net, l4, verdict);
     }
 }
 
@@ -1169,80 +1167,13 @@ __device__ __forceinline__ bool stream_finish(const FlatArgs& p, StreamLds& S, u
     // (MODE 3 IPv6: the transport's line and offset; finish stores the field relative to it)
     const uint32_t ri = (r + (eth6 ? 54u : L2)) & 15u;
     const uint64_t a0off = valid ? off + (eth6 ? 54u : L2) - ri : 0u;
-#ifdef PICO_TX_CHUNK_WB
-    // (A/B) MODE 1 TX written in place: the crc fields patched into the frame's head-window chunks
-    // (hw, as the stream read them), each written chunk one aligned 16-byte store -- unless the
-    // chunk holds bytes outside this frame, or the field lies past the head window: then the
-    // field's own 2-byte store
-    constexpr bool WB = !NATM && !ETH;
-    FlatArgs pw = p;
-    if (WB && tx) pw.flags &= ~1u;
-#else
-    constexpr bool WB = false;
-    const FlatArgs& pw = p;
-#endif
-    uint3 res = make_uint3(0u, 0u, 0u);
     if (lane < cnt)
-        res = finish_frame<ETH ? 3 : 1>(pw, f0 + lane, tx, eth6 ? v6sum : hdr20 + opt + tsum, eth6 ? v6x : xp, opt,
+        finish_frame<ETH ? 3 : 1>(p, f0 + lane, tx, eth6 ? v6sum : hdr20 + opt + tsum, eth6 ? v6x : xp, opt,
                         make_uint4((uint32_t)a0off, (uint32_t)(a0off >> 32), 0u, ri),
                         make_uint4(verdict | post | (parsed ? 16u : 0u) | (l4_needed ? 32u : 0u) | (oob ? 64u : 0u) |
                                        (eth6 ? 128u : 0u) | (proto << 8) | (tl << 16),
                                    hl | (l2v << 8) | (ipcrc << 16), pseudo, hdr20),
                         NONE);
-    if (WB && tx && (p.flags & 1u)) {
-        // the fields finish_frame would store (positions in the head window, 2 bytes each)
-        const uint32_t net = res.x, l4 = res.y, vd = res.z;
-        const bool mine = lane < cnt && valid;
-        uint32_t pa = NONE, va = 0u, pb = NONE, vb = 0u;
-        if (mine && (vd == V_ACCEPT || vd == V_FRAG)) { pa = r + 10u; va = net; }
-        if (mine && vd == V_ACCEPT) {
-            if ((proto == 6u || proto == 1u) && l4_needed) { pb = r + hl + (proto == 6u ? 16u : 2u); vb = l4; }
-            else if (proto == 17u && tl >= 8u) { pb = r + hl + 6u; vb = 0u; }
-        }
-        // chunks written (bit c: window chunk c = span chunk hq + c); a field past the window stores alone
-        const bool ina = pa != NONE && pa + 2u <= 16u * HS, inb = pb != NONE && pb + 2u <= 16u * HS;
-        uint32_t dm = (ina ? (1u << (pa >> 4)) | (1u << ((pa + 1u) >> 4)) : 0u) |
-                      (inb ? (1u << (pb >> 4)) | (1u << ((pb + 1u) >> 4)) : 0u);
-        // a chunk is stored whole only when it lies inside this frame: no other frame's bytes in it
-        // (frames do not overlap), so no other lane or wave writes into it
-        const uint32_t fe = r + len;                  // frame end in window bytes
-        uint32_t conflict = 0u;
-#pragma unroll
-        for (uint32_t c = 0; c < HS; ++c)
-            if (16u * c < r || 16u * c + 16u > fe) conflict |= 1u << c;
-        uint32_t W[4 * HS];
-#pragma unroll
-        for (uint32_t i = 0; i < HS; ++i) {
-            W[4 * i] = hw[i].x; W[4 * i + 1] = hw[i].y; W[4 * i + 2] = hw[i].z; W[4 * i + 3] = hw[i].w;
-        }
-        auto patch = [&](uint32_t pos, uint32_t v) {   // short_be(v) at window byte pos
-#pragma unroll
-            for (uint32_t k = 0; k < 4 * HS; ++k) {
-                const uint32_t b0 = 4u * k;
-                uint32_t w = W[k];
-                if (pos >= b0 && pos < b0 + 4u) {
-                    const uint32_t sh = 8u * (pos - b0);
-                    w = (w & ~(0xFFu << sh)) | (((v >> 8) & 0xFFu) << sh);
-                }
-                if (pos + 1u >= b0 && pos + 1u < b0 + 4u) {
-                    const uint32_t sh = 8u * (pos + 1u - b0);
-                    w = (w & ~(0xFFu << sh)) | ((v & 0xFFu) << sh);
-                }
-                W[k] = w;
-            }
-        };
-        const bool ca = ina && ((conflict >> (pa >> 4)) & 1u || (conflict >> ((pa + 1u) >> 4)) & 1u);
-        const bool cb = inb && ((conflict >> (pb >> 4)) & 1u || (conflict >> ((pb + 1u) >> 4)) & 1u);
-        if (ina && !ca) patch(pa, va);
-        if (inb && !cb) patch(pb, vb);
-        uint8_t* const fpw = p.base + off - r;          // window byte 0 (16-byte aligned)
-#pragma unroll
-        for (uint32_t c = 0; c < HS; ++c)
-            if (((dm & ~conflict) >> c) & 1u)
-                *reinterpret_cast<uint4*>(fpw + 16u * c) = make_uint4(W[4 * c], W[4 * c + 1], W[4 * c + 2], W[4 * c + 3]);
-        if (pa != NONE && (!ina || ca)) store_crc(fpw + pa, va);
-        if (pb != NONE && (!inb || cb)) store_crc(fpw + pb, vb);
-    }
     STAMP(3);
     return true;
 }
