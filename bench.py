@@ -577,6 +577,9 @@ def seq_copy_lib():
 # (variant, units per lane, workgroups): 0 non-temporal loads + stores, 1 cached, 2 nt loads + cached
 # stores; workgroups 0 = one trip each, else a striding grid (8192 = 32 per CU)
 SEQ_COPY_SHAPES = ((0, 4, 0), (0, 8, 0), (1, 4, 0), (2, 4, 0), (0, 4, 8192), (2, 8, 8192))
+# the same copy with its loads 2 bytes off the 16-byte grid (as the reassembly's payload loads), reported
+# beside the ceiling, not as it
+SEQ_COPY_UNALIGNED = ((3, 4, 0), (4, 4, 0))
 
 
 def copy_ceiling(nbytes: int, dev) -> dict:
@@ -608,6 +611,12 @@ def copy_ceiling(nbytes: int, dev) -> dict:
             def f(i, var=var, u=u, blocks=blocks):
                 assert lib.seq_copy_launch(var, u, blocks, dst[i % rot].data_ptr(), src[i % rot].data_ptr(), nbytes, h) == 0
             shapes[f"v{var}_u{u}_g{blocks}"] = round(timed(f), 2)
+    unal = {}
+    if lib is not None:
+        for var, u, blocks in SEQ_COPY_UNALIGNED:
+            def f(i, var=var, u=u, blocks=blocks):
+                assert lib.seq_copy_launch(var, u, blocks, dst[i % rot].data_ptr(), src[i % rot].data_ptr(), nbytes, h) == 0
+            unal[f"v{var}_u{u}_g{blocks}"] = round(timed(f), 2)
     torch_us = timed(lambda i: dst[i % rot].copy_(src[i % rot]))
     if shapes:
         best = min(shapes, key=shapes.get)
@@ -618,7 +627,7 @@ def copy_ceiling(nbytes: int, dev) -> dict:
         us = torch_us
         what = f"torch copy_ of {nbytes} B (read + write), {rot} rotating buffers, HIP events (seq_copy not built)"
     return {"copy_us": round(us, 2), "copy_GBs": round(2 * nbytes / us / 1e3, 1), "what": what,
-            "shapes_us": shapes, "torch_copy_us": round(torch_us, 2)}
+            "shapes_us": shapes, "unaligned_source_us": unal, "torch_copy_us": round(torch_us, 2)}
 
 
 def e2e_rate_desc(host):

@@ -103,23 +103,38 @@ extern "C" int gather_ceiling_launch(int mode, const void* src, uint64_t src_len
 // 6.29 TB/s).  Each lane moves U 16-byte units per trip, a wave 1 KiB a unit row, all U loads issued
 // before the stores; a grid of `blocks` workgroups of 256 threads strides over the buffer.
 // VARIANT: 0 non-temporal loads and stores, 1 cached loads and stores, 2 non-temporal loads with
-// cached stores.  n must be a multiple of 16 (the caller copies the tail, if any, itself).
+// cached stores, 3 cached loads 2 bytes off the 16-byte grid (byte-unaligned buffer loads, as the
+// reassembly's payload loads: a fragment's payload sits 34 bytes past its 16-byte-aligned frame) with
+// cached aligned stores, 4 the same with non-temporal loads.  n must be a multiple of 16 (the caller
+// copies the tail, if any, itself).
 template <int U, int VARIANT>
 __global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u * U;
     for (uint64_t b = (uint64_t)blockIdx.x * 256u * U + threadIdx.x; b < n16; b += stride) {
         u32x4 v[U];
+        __amdgpu_buffer_rsrc_t sr;
+        if constexpr (VARIANT >= 3) {                   // a window over this trip's source bytes, + 2
+            const uint64_t b0 = b - threadIdx.x;       // the trip's first unit; the window stops at the buffer's end
+            const uint64_t left = (n16 - b0) * 16u;
+            sr = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(src + b0), 0,
+                                                   (int)min((uint64_t)(256u * U * 16u + 16u), left), 0x00020000);
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint64_t i = b + 256u * k;
-            if (i < n16) v[k] = VARIANT == 1 ? src[i] : __builtin_nontemporal_load(src + i);
+            if constexpr (VARIANT >= 3) {
+                const uint32_t o = (uint32_t)(threadIdx.x + 256u * k) * 16u + 2u;
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(i < n16 ? o : 0x80000000u), 0, VARIANT == 4 ? 2 : 0);
+            } else if (i < n16) {
+                v[k] = VARIANT == 1 ? src[i] : __builtin_nontemporal_load(src + i);
+            }
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint64_t i = b + 256u * k;
             if (i < n16) {
                 if (VARIANT == 0) __builtin_nontemporal_store(v[k], dst + i);
-                else dst[i] = v[k];
+                else dst[i] = v[k];                  // (VARIANT 3 / 4: the source's last unit reads 2 bytes past it)
             }
         }
     }
@@ -136,9 +151,11 @@ extern "C" int seq_copy_launch(int variant, int u, uint32_t blocks, void* dst, c
     const u32x4* sr = static_cast<const u32x4*>(src);
 #define SC(UU, VV) hipLaunchKernelGGL((seq_copy<UU, VV>), dim3(g), dim3(256), 0, s, d, sr, n16)
     if (u == 8) {
-        if (variant == 0) SC(8, 0); else if (variant == 1) SC(8, 1); else SC(8, 2);
+        if (variant == 0) SC(8, 0); else if (variant == 1) SC(8, 1); else if (variant == 2) SC(8, 2);
+        else if (variant == 3) SC(8, 3); else SC(8, 4);
     } else {
-        if (variant == 0) SC(4, 0); else if (variant == 1) SC(4, 1); else SC(4, 2);
+        if (variant == 0) SC(4, 0); else if (variant == 1) SC(4, 1); else if (variant == 2) SC(4, 2);
+        else if (variant == 3) SC(4, 3); else SC(4, 4);
     }
 #undef SC
     return (int)hipGetLastError();
