@@ -443,7 +443,7 @@ def cpu_baseline_frag(st, target_s: float, v6: bool = False):
     grp = gr.cpu().numpy().view(np.uint32)[:2 * k]
     nf_used = int(grp[-2] + grp[-1])
     desc = d.cpu().numpy().view(batch.DESC_DTYPE)[:nf_used]
-    hi = int(desc["off"][-1]) + int(desc["len"][-1])
+    hi = int((desc["off"] + desc["len"].astype(np.uint64)).max())   # (retx: the last descriptor is a repeat)
     host = b[:hi].cpu().numpy()
     nbytes = payload // n * k
     if O.ref_reasm_available():
