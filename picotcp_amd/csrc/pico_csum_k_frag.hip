@@ -639,11 +639,22 @@ __global__ __launch_bounds__(64 * REASM_FINISH_WAVES) void reasm_finish_kernel(F
         const bool in = g < p.n_dgram;
         uint32_t state = PLAN_SLOW;
         if (in) {
+            // the plan and the S slots in one round trip (the slots are read whatever the plan says):
+            // 8 slot loads in flight before the adds
             const ReasmPlan r = p.plan[g];
+            const uint32_t* sl = p.slot + (uint64_t)g * p.S;
+            uint32_t sum = 0u, k = 0;
+            for (; k + 8u <= p.S; k += 8u) {
+                uint32_t v[8];
+#pragma unroll
+                for (uint32_t i = 0; i < 8u; ++i) v[i] = sl[k + i];
+#pragma unroll
+                for (uint32_t i = 0; i < 8u; ++i) sum += v[i];
+            }
+            for (; k < p.S; ++k) sum += sl[k];
             state = r.state;
             if (state != PLAN_SLOW) {
-                uint32_t sum = 0u - r.corr;
-                for (uint32_t k = 0; k < p.S; ++k) sum += p.slot[(uint64_t)g * p.S + k];
+                sum -= r.corr;
                 uint32_t l4 = 0, v = V_MALFORMED;
                 if (state == PLAN_GOOD) v = reasm_verdict<V6>(p.flags, r.len, r.proto, r.pseudo, sum, r.w0, r.w1, l4);
                 if (p.o_len) p.o_len[g] = state == PLAN_GOOD ? r.len : 0u;

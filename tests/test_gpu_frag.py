@@ -298,10 +298,11 @@ def test_flat_grid_streams_and_sizes():
         _check_flat(r, o, od, want, out_o)
 
 
-def _with_retransmits(buf, off, flen, grp, seed, per=(1, 3)):
+def _with_retransmits(buf, off, flen, grp, seed, per=(1, 3), same=0.0, hdr=20):
     """Every datagram gets per[0]..per[1] retransmitted fragments: a copy of one of its fragments
-    (same header, different payload bytes) at a random place in its arrival order -- before the
-    original (the copy is then the kept one) or after it (rejected by pico_tree_insert)."""
+    at a random place in its arrival order -- before the original (the copy is then the kept one)
+    or after it (rejected by pico_tree_insert).  A copy carries the original's bytes with
+    probability `same` (a true retransmission), else different payload bytes (behind `hdr`)."""
     rng = np.random.default_rng(seed)
     extra, new_off, new_len, new_grp = [], [], [], []
     pos = buf.size
@@ -311,7 +312,8 @@ def _with_retransmits(buf, off, flen, grp, seed, per=(1, 3)):
         for _ in range(int(rng.integers(per[0], per[1] + 1)) if cnt else 0):
             o, n = orig[int(rng.integers(0, cnt))]
             f = buf[o:o + n].copy()
-            f[20:] = rng.integers(0, 256, n - 20, dtype=np.uint8)     # (IPv4: the payload behind 20 B)
+            if rng.random() >= same:
+                f[hdr:] = rng.integers(0, 256, n - hdr, dtype=np.uint8)
             extra.append(f)
             order.insert(int(rng.integers(0, len(order) + 1)), (pos, n))
             pos += n
@@ -335,3 +337,28 @@ def test_flat_grid_retransmits(payload):
     od, size = layout(lens, shift=4)
     wl, wv = check(buf, d, grp, od, size)
     assert (wv != 8).mean() > 0.9
+
+
+@pytest.mark.parametrize("v6", [False, True])
+@pytest.mark.parametrize("same", [1.0, 0.7])
+def test_flat_grid_true_retransmits(v6, same):
+    """Retransmissions carrying the original's bytes (all of them, or 70 % mixed with altered
+    copies) on 800 datagrams: the flat grid's planner keeps such a plan GOOD and subtracts the
+    copy's sum; an altered copy sends its datagram to the finish's workgroup path.  Every
+    verdict, checksum and reassembled byte against the oracle (both fixture settings)."""
+    rng = np.random.default_rng(17 + v6)
+    lens = rng.integers(1, 24000, 800).tolist()
+    if v6:
+        lens = [x // 8 * 8 + 8 for x in lens]
+        buf, off, flen, grp = synth.ipv6_fragments(lens, seed=31, proto=6, frag_payload=1448)
+    else:
+        buf, off, flen, grp = synth.ipv4_fragments(lens, seed=31, proto=6, frag_payload=1480)
+    buf, off, flen, grp = _with_retransmits(buf, off, flen, grp, seed=32 + v6, per=(0, 2), same=same,
+                                            hdr=48 if v6 else 20)
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=8 if v6 else 4, hdr=40 if v6 else 20)
+    wl, wv = check(buf, d, grp, od, size, v6=v6)
+    ok = wv != 8
+    assert ok.mean() > 0.9
+    if same == 1.0:
+        assert (wv == 1).mean() > 0.99                   # the kept bytes are the originals: valid TCP
