@@ -682,9 +682,10 @@ __global__ __launch_bounds__(64 * REASM_FINISH_WAVES) void reasm_finish_kernel(F
 // dispatcher balances the gather over the whole batch instead of one wave walking a whole
 // datagram; planner workgroups dispatched ahead of them plan the datagrams (a datagram's fragments
 // one per lane: dedup, completeness, header copy).  Every wave leaves its partial sum in its slot; the finish
-// (reasm_finish_kernel) adds them.  A datagram with repeated offsets or more than
-// FLAT_MAXF fragments is gathered again there by the one-wave path (its flat-grid bytes may hold
-// a later arrival's copy; the region past the reassembled datagram is unspecified).
+// (reasm_finish_kernel) adds them, less the sums of retransmitted fragments (a repeated offset whose
+// later arrival carries the same bytes).  A datagram with a repeated offset of different bytes, or
+// more than FLAT_MAXF fragments, is gathered again there by the workgroup path (its flat-grid bytes
+// may hold a later arrival's copy); the region past the reassembled datagram is unspecified.
 
 // A retransmitted fragment's payload against the kept arrival's (n bytes each from sa / sb, wave-uniform
 // addresses): true when equal; sum = the retransmission's word sum (its payload starts at an even
