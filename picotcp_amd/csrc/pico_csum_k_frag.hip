@@ -112,7 +112,7 @@ struct ReasmPlan {
     uint32_t state, len, proto, pseudo, w0, w1, corr, pad;
 };
 constexpr uint32_t PLAN_GOOD = 0u, PLAN_BAD = 1u, PLAN_SLOW = 2u;
-constexpr uint32_t FLAT_MAXF = 64u;          // fragments a plan holds (one per lane)
+constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a lane)
 #ifndef REASM_NP4
 #define REASM_NP4 2u
 #endif
@@ -716,100 +716,166 @@ __device__ __forceinline__ bool payload_same(const FragArgs& p, uint64_t sa, uin
     return __builtin_amdgcn_ballot_w64(diff) == 0;
 }
 
-// a planner: pico_fragments_check_complete on registers (lane j: fragment j).  A repeated offset's
-// later arrival is not kept (pico_tree_insert rejects a repeated key); the gather waves gathered it
-// too, so it is harmless only when it carries the kept arrival's bytes -- a retransmission: the
-// plan then subtracts its sum (corr) -- else the plan is SLOW.
-template <bool V6>
-__device__ __forceinline__ void plan_datagram(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, bool bad0,
-                                              uint8_t* t, uint32_t cap, uint32_t lane) {
+// a planner: pico_fragments_check_complete on registers, NS fragments a lane (lane j: fragments j,
+// j + 64).  A repeated offset's later arrival is not kept (pico_tree_insert rejects a repeated key);
+// the gather waves gathered it too, so it is harmless only when it carries the kept arrival's bytes --
+// a retransmission: the plan then subtracts its sum (corr) -- else the plan is SLOW.
+template <bool V6, int NS>
+__device__ __forceinline__ void plan_sets(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, uint8_t* t,
+                                          uint32_t cap, uint32_t lane) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
+    constexpr uint32_t W = 64u * NS;                  // fragments the planner holds
     auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+    // fragment k's field from set k / 64 (k wave-uniform)
+    auto rk = [&](const uint32_t (&v)[NS], uint32_t k) {
+        uint32_t x = rl(v[0], k & 63u);
+        if constexpr (NS > 1) x = (k >> 6) ? rl(v[1], k & 63u) : x;
+        return x;
+    };
     uint32_t state = PLAN_BAD, len = 0, proto = 0, pseudo = 0, w0 = 0, w1 = 0, corr = 0;
-    if (!bad0 && cnt > FLAT_MAXF) {
-        state = PLAN_SLOW;
-    } else if (!bad0) {
-        const bool in = lane < cnt;
-        uint32_t key, tl, hl, pr;
+    bool in[NS], ok = true;
+    uint32_t key[NS], tl[NS], hl[NS], pr[NS], o[NS], offl[NS], offh[NS], srcl[NS], srch[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        in[s] = lane + 64u * s < cnt;
         uint64_t off;
-        const bool ok = parse_lane<V6>(p, in, first + lane, off, key, tl, hl, pr);
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
-            const uint32_t o = key & 0xFFFFu;
-            uint32_t P = 0, rank = 0;                 // transport bytes / kept fragments below this offset
-            uint32_t orig = lane;                     // the earliest arrival with this offset
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const uint32_t kk = rl(key, k) & 0xFFFFu, tk = rl(tl, k);
-                orig = k < orig && kk == o ? k : orig;
-                P += kk < o ? tk : 0u;
-                rank += kk < o ? 1u : 0u;
+        ok = parse_lane<V6>(p, in[s], first + lane + 64u * s, off, key[s], tl[s], hl[s], pr[s]) && ok;
+        o[s] = key[s] & 0xFFFFu;
+        offl[s] = (uint32_t)off;
+        offh[s] = (uint32_t)(off >> 32);
+        const uint64_t src = reinterpret_cast<uint64_t>(p.base) + off + hl[s];
+        srcl[s] = (uint32_t)src;
+        srch[s] = (uint32_t)(src >> 32);
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+        uint32_t P[NS], rank[NS], orig[NS];           // transport bytes / kept fragments below; earliest same offset
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { P[s] = rank[s] = 0; orig[s] = lane + 64u * s; }
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t kk = rk(key, k) & 0xFFFFu, tk = rk(tl, k);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                orig[s] = k < orig[s] && kk == o[s] ? k : orig[s];
+                P[s] += kk < o[s] ? tk : 0u;
+                rank[s] += kk < o[s] ? 1u : 0u;
             }
-            const bool kept = in && orig == lane;
-            const uint64_t km = __builtin_amdgcn_ballot_w64(kept);
-            const uint64_t dups = __builtin_amdgcn_ballot_w64(in && !kept);
-            if (dups) {                               // (rare) P and rank over the kept arrivals only
-                P = rank = 0;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const uint32_t kk = rl(key, k) & 0xFFFFu, tk = rl(tl, k);
-                    const bool below = ((km >> k) & 1u) && kk < o;
-                    P += below ? tk : 0u;
-                    rank += below ? 1u : 0u;
+        }
+        bool kept[NS];
+        uint64_t km[NS], dups[NS];
+        bool anydup = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            kept[s] = in[s] && orig[s] == lane + 64u * s;
+            km[s] = __builtin_amdgcn_ballot_w64(kept[s]);
+            dups[s] = __builtin_amdgcn_ballot_w64(in[s] && !kept[s]);
+            anydup |= dups[s] != 0;
+        }
+        if (anydup) {                                 // (rare) P and rank over the kept arrivals only
+#pragma unroll
+            for (int s = 0; s < NS; ++s) P[s] = rank[s] = 0;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t kk = rk(key, k) & 0xFFFFu, tk = rk(tl, k);
+                const uint64_t kmk = NS > 1 && (k >> 6) ? km[NS - 1] : km[0];
+                const bool kk_kept = (kmk >> (k & 63u)) & 1u;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const bool below = kk_kept && kk < o[s];
+                    P[s] += below ? tk : 0u;
+                    rank[s] += below ? 1u : 0u;
                 }
             }
-            // retransmissions: the same length and bytes as the kept arrival, else SLOW
-            bool slow = false;
-            const uint64_t src = reinterpret_cast<uint64_t>(p.base) + off + hl;
-            for (uint64_t dm = dups; dm && !slow; dm &= dm - 1u) {
-                const uint32_t k = (uint32_t)__builtin_ctzll(dm), j = rl(orig, k), n = rl(tl, k);
+        }
+        // retransmissions: the same length and bytes as the kept arrival, else SLOW
+        bool slow = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            for (uint64_t dm = dups[s]; dm && !slow; dm &= dm - 1u) {
+                const uint32_t k = 64u * s + (uint32_t)__builtin_ctzll(dm), j = rk(orig, k), n = rk(tl, k);
                 uint32_t sk = 0;
-                slow = n != rl(tl, j) ||
-                       !payload_same(p, ((uint64_t)rl((uint32_t)(src >> 32), k) << 32) | rl((uint32_t)src, k),
-                                     ((uint64_t)rl((uint32_t)(src >> 32), j) << 32) | rl((uint32_t)src, j), n, lane, sk);
+                slow = n != rk(tl, j) ||
+                       !payload_same(p, ((uint64_t)rk(srch, k) << 32) | rk(srcl, k), ((uint64_t)rk(srch, j) << 32) | rk(srcl, j),
+                                     n, lane, sk);
                 corr += sk;
             }
-            const uint32_t m = (uint32_t)__builtin_popcountll(km);
-            if (slow) {
-                state = PLAN_SLOW;
-            } else {
-                // rank = tree position.  Complete: offset == the transport bytes below it up to the
-                // first MF-clear fragment in tree order, which is the last
-                const bool mfc = kept && !(key & (1u << 16));
-                const uint32_t re = 64u - rl(wave_scan_max(mfc ? 64u - rank : 0u), 63);
-                bool b = re >= m || re + 1u != m || __builtin_amdgcn_ballot_w64(kept && rank <= re && o != P) != 0;
-                if (!b) {
-                    const uint32_t le = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(mfc && rank == re));
-                    len = rl(P + tl, le);
-                    b = HDR + len > 0xFFFFu || len > cap;
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) m += (uint32_t)__builtin_popcountll(km[s]);
+        if (slow) {
+            state = PLAN_SLOW;
+        } else {
+            // rank = tree position.  Complete: offset == the transport bytes below it up to the
+            // first MF-clear fragment in tree order, which is the last
+            bool mfc[NS];
+            uint32_t top = 0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                mfc[s] = kept[s] && !(key[s] & (1u << 16));
+                top = max(top, rl(wave_scan_max(mfc[s] ? W - rank[s] : 0u), 63));
+            }
+            const uint32_t re = W - top;
+            bool b = re >= m || re + 1u != m;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) b = b || __builtin_amdgcn_ballot_w64(kept[s] && rank[s] <= re && o[s] != P[s]) != 0;
+            if (!b) {
+#pragma unroll
+                for (int s = NS - 1; s >= 0; --s) {
+                    const uint64_t e = __builtin_amdgcn_ballot_w64(mfc[s] && rank[s] == re);
+                    if (e) len = rl(P[s] + tl[s], (uint32_t)__builtin_ctzll(e));
                 }
-                if (!b) {
-                    // the first fragment's header (pico_fragments.c:332-338), its transport bytes
-                    // 0..7 and the pseudo header's address part (as in reassemble_kernel)
-                    const uint32_t f0 = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kept && o == 0u));
-                    const uint8_t* h0 =
-                        p.base + (((uint64_t)rl((uint32_t)(off >> 32), f0) << 32) | rl((uint32_t)off, f0));
-                    const uint32_t hl0 = rl(hl, f0), tl0 = rl(tl, f0);
-                    const uint32_t hb = lane < HDR ? ld_u8(h0 + lane) : 0u;
-                    if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hb;
-                    const uint32_t tb8 = lane < 8u && lane < tl0 ? ld_u8(h0 + hl0 + lane) : 0u;
-                    w0 = rl(tb8, 0) | (rl(tb8, 1) << 8) | (rl(tb8, 2) << 16) | (rl(tb8, 3) << 24);
-                    w1 = rl(tb8, 4) | (rl(tb8, 5) << 8) | (rl(tb8, 6) << 16) | (rl(tb8, 7) << 24);
-                    if constexpr (!V6) {
-                        proto = (uint32_t)__shfl((int)hb, 9);
-                        const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
-                        pseudo = rl(group_sum<64>(pw), 63) + (proto << 8) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
-                    } else {
-                        // the module: the walk's protocol of the latest kept arrival (it completes the
-                        // set, pico_fragments.c:492; reassemble_one's rule)
-                        proto = rl(pr, 63u - (uint32_t)__builtin_clzll(km)) | ((uint32_t)__shfl((int)hb, 9) << 8);
-                        const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
-                        pseudo = rl(group_sum<64>(pw), 63) + (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) +
-                                 (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
-                    }
-                    state = PLAN_GOOD;
+                b = HDR + len > 0xFFFFu || len > cap;
+            }
+            if (!b) {
+                // the first fragment's header (pico_fragments.c:332-338), its transport bytes
+                // 0..7 and the pseudo header's address part (as in reassemble_kernel)
+                uint32_t f0 = 0;
+#pragma unroll
+                for (int s = NS - 1; s >= 0; --s) {
+                    const uint64_t z = __builtin_amdgcn_ballot_w64(kept[s] && o[s] == 0u);
+                    if (z) f0 = 64u * s + (uint32_t)__builtin_ctzll(z);
                 }
+                const uint8_t* h0 = p.base + (((uint64_t)rk(offh, f0) << 32) | rk(offl, f0));
+                const uint32_t hl0 = rk(hl, f0), tl0 = rk(tl, f0);
+                const uint32_t hb = lane < HDR ? ld_u8(h0 + lane) : 0u;
+                if (lane < HDR) t[(int)lane - (int)HDR] = (uint8_t)hb;
+                const uint32_t tb8 = lane < 8u && lane < tl0 ? ld_u8(h0 + hl0 + lane) : 0u;
+                w0 = rl(tb8, 0) | (rl(tb8, 1) << 8) | (rl(tb8, 2) << 16) | (rl(tb8, 3) << 24);
+                w1 = rl(tb8, 4) | (rl(tb8, 5) << 8) | (rl(tb8, 6) << 16) | (rl(tb8, 7) << 24);
+                if constexpr (!V6) {
+                    proto = (uint32_t)__shfl((int)hb, 9);
+                    const uint32_t pw = lane >= 12u && lane < 20u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                    pseudo = rl(group_sum<64>(pw), 63) + (proto << 8) + (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                } else {
+                    // the module: the walk's protocol of the latest kept arrival (it completes the
+                    // set, pico_fragments.c:492; reassemble_one's rule)
+                    uint32_t last = 0;
+#pragma unroll
+                    for (int s = 0; s < NS; ++s)
+                        if (km[s]) last = 64u * s + 63u - (uint32_t)__builtin_clzll(km[s]);
+                    proto = rk(pr, last) | ((uint32_t)__shfl((int)hb, 9) << 8);
+                    const uint32_t pw = lane >= 8u && lane < 40u ? (lane & 1u ? hb << 8 : hb) : 0u;
+                    pseudo = rl(group_sum<64>(pw), 63) + (((len >> 24) & 0xFFu) | ((len >> 8) & 0xFF00u)) +
+                             (((len & 0xFFu) << 8) | ((len >> 8) & 0xFFu));
+                }
+                state = PLAN_GOOD;
             }
         }
     }
     if (lane == 0) p.plan[g] = ReasmPlan{state, len, proto, pseudo, w0, w1, corr, 0u};
+}
+
+template <bool V6>
+__device__ __forceinline__ void plan_datagram(const FragArgs& p, uint32_t g, uint32_t first, uint32_t cnt, bool bad0,
+                                              uint8_t* t, uint32_t cap, uint32_t lane) {
+    if (bad0) {
+        if (lane == 0) p.plan[g] = ReasmPlan{PLAN_BAD, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    } else if (cnt <= 64u) {
+        plan_sets<V6, 1>(p, g, first, cnt, t, cap, lane);
+    } else if (cnt <= FLAT_MAXF) {
+        plan_sets<V6, 2>(p, g, first, cnt, t, cap, lane);
+    } else if (lane == 0) {
+        p.plan[g] = ReasmPlan{PLAN_SLOW, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    }
 }
 
 // One or two fragments' payloads gathered into the transport at tb (fragment A: transport bytes
@@ -1214,10 +1280,11 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     // datagram: 256 19.2 vs 18.7 us, 512 22.6 vs 23.9, 1024 35.4 vs 36.9;
     // profiles/r05/ab_reasm_small_batches.txt)
     const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
-    // automatic: a batch of more than FLAT_MAXF fragments a datagram on average (64 KiB datagrams
-    // over a small MTU) takes one workgroup per datagram -- on the flat grid most of its datagrams
-    // would be SLOW plans, gathered twice
-    if (n_dgram >= fmin && (flat_min || (uint64_t)n_frag <= (uint64_t)FLAT_MAXF * n_dgram)) {
+    // automatic: a batch of more than 64 fragments a datagram on average (64 KiB datagrams over a
+    // small MTU) takes one workgroup per datagram.  (The flat grid plans up to FLAT_MAXF = 128 a
+    // datagram, but on c3_reasm_576 -- 117 fragments of 552 B -- it measured 221 us, and 217 us with
+    // four pairs a gather wave, against 217 us here: profiles/r06/ab_reasm_128*.txt.)
+    if (n_dgram >= fmin && (flat_min || (uint64_t)n_frag <= 64ull * n_dgram)) {
         // S waves per datagram, FPI fragments each on average
         const uint32_t fpi = 2u * flat_np(v6 != 0);
         const uint64_t its = ((uint64_t)n_frag + fpi - 1u) / fpi;

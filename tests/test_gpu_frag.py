@@ -362,3 +362,27 @@ def test_flat_grid_true_retransmits(v6, same):
     assert ok.mean() > 0.9
     if same == 1.0:
         assert (wv == 1).mean() > 0.99                   # the kept bytes are the originals: valid TCP
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_flat_grid_two_fragments_a_lane(v6):
+    """Datagrams of 65-128 fragments (64 KiB over 552 / 520-byte fragments: the planner holds two
+    fragments a lane), some with retransmitted fragments -- the same bytes or altered, in either
+    half of the arrival order -- on 600 datagrams: every verdict, checksum and reassembled byte
+    against the oracle.  (More than 128 fragments: test_batch_shapes.)"""
+    rng = np.random.default_rng(23 + v6)
+    pl = 520 if v6 else 552
+    lens = rng.integers(34000, 65000, 600)
+    lens[rng.integers(0, 600, 20)] = rng.integers(0, 3000, 20)            # and a few short ones
+    lens = [int(x) // 8 * 8 + 8 if v6 else int(x) for x in lens]
+    if v6:
+        buf, off, flen, grp = synth.ipv6_fragments(lens, seed=41, proto=6, frag_payload=pl)
+    else:
+        buf, off, flen, grp = synth.ipv4_fragments(lens, seed=41, proto=6, frag_payload=pl)
+    buf, off, flen, grp = _with_retransmits(buf, off, flen, grp, seed=42 + v6, per=(0, 3), same=0.6,
+                                            hdr=48 if v6 else 20)
+    assert ((grp[:, 1] > 64) & (grp[:, 1] <= 128)).mean() > 0.8
+    d = G.ipv4_desc(off, flen)
+    od, size = layout(lens, shift=8 if v6 else 4, hdr=40 if v6 else 20)
+    wl, wv = check(buf, d, grp, od, size, v6=v6)
+    assert (wv != 8).mean() > 0.9
