@@ -198,6 +198,12 @@ int main(int argc, char **argv)
     fails += cmp16("scalar", u_out, u_want, u_n);
     pico_csum_host_unregister(frames);
 
+    /* ---- 4. (ABI 4) this thread has run no reassembly: the release has nothing to free */
+    if ((rc = pico_csum_release_thread_scratch()) != 0) {
+        fprintf(stderr, "release_thread_scratch: %d %s\n", rc, pico_csum_last_error());
+        fails++;
+    }
+
     hipFree(d_buf); hipFree(d_desc); hipFree(d_net); hipFree(d_l4); hipFree(d_v);
     printf("abi_check: %u datagrams TX+RX, %u host frames, scalar: %s\n", n, u_n, fails ? "MISMATCH" : "ok");
     return fails ? 1 : 0;

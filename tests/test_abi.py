@@ -164,6 +164,8 @@ def test_batch_path_fails_loudly_without_gpu():
     from picotcp_amd import batch
     with pytest.raises(ValueError):
         batch.checksum_uniform(torch.zeros(6000, dtype=torch.uint8), 1500, 1500, 4)
+    # (ABI 4) the scratch release has nothing to free and says why
+    assert lib.pico_csum_release_thread_scratch() == -_lib.ENODEV
 
 
 def test_kernel_image_is_gfx950():
