@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident checksummed GiB/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2slot|c2tx|c2tx_nw|c2nat|c2v6|c2eth|c2ethmix|c3|c3_64k|c3_frag|c3_reasm|c3_reasm6|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config <one of the configs below>]
   torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 A step = one pass of the hot path over one batch resident in HBM:
   c1 (default, the metric's config): 256K x 1500 B frames, raw pico_checksum per frame
+  c1_s1536: the same frames at stride 1536 (each on a 128 B line)
   c2: 256K simple-IMIX {64,576,1500} IPv4/TCP datagrams, fused header + pseudo-header RX verify
   c2slot: the same datagrams each in its own 2 KiB slot (a driver's slot ring), RX verify
   c2tx: the same datagrams, fused TX (checksums computed and written in place)
@@ -17,6 +18,8 @@ A step = one pass of the hot path over one batch resident in HBM:
   c3_frag: 16K x 64512 B IPv4/TCP datagrams (reassembly maximum), fused RX verify
   c3_reasm: 4K x 64512 B datagrams reassembled from 1480 B fragments + TCP check in the same pass
   c3_reasm6: the same for IPv6 (1448 B fragments behind a fragment header)
+  c3_reasm_il / _retx / _576: c3_reasm with the fragments interleaved across datagrams / a
+      retransmitted fragment in every datagram / 552 B fragments (a 576 B MTU)
   c3: 256K x 9000 B jumbo frames;  c3_64k: 16K x 64 KiB reassembled buffers
   c4: 4M x 1500 B frames sharded over the ranks (strong scaling)
 c1/c2/c3 are weak-scaled: every rank checksums its own batch of that size (frame batches
@@ -63,6 +66,9 @@ GIB = float(1 << 30)
 CONFIGS = {
     "c1": dict(kind="uniform", frames=262144, frame_bytes=1500,
                workload="C1: 256K x 1500 B (Ethernet MTU) frames, raw pico_checksum per frame, packed stride 1500"),
+    "c1_s1536": dict(kind="uniform", frames=262144, frame_bytes=1500, stride=1536,
+                     workload="C1, the aligned variant (SURVEY 8d): 256K x 1500 B frames at stride 1536 (every "
+                              "frame on a 128 B line), raw pico_checksum per frame"),
     "c2": dict(kind="ipv4", frames=262144,
                workload="C2: 256K simple-IMIX {64,576,1500} B IPv4/TCP datagrams (14 B Ethernet header in front), "
                         "fused IPv4 header + TCP pseudo-header RX verify"),
@@ -326,30 +332,32 @@ def cgroup_cpu() -> str | None:
         return None
 
 
-def cpu_baseline(sample: np.ndarray, ln: int, target_s: float):
+def cpu_baseline(sample: np.ndarray, ln: int, target_s: float, stride: int = 0):
     """The reference's pico_checksum (oracle/_ref: stack/pico_frame.c built -O3 = the
     reference's PERF=1, and -Os = its release default) over a bounded sample of the same
     frames, on 1 thread and on the job's host-core share."""
     from oracle import oracle as O
     kind = "reference" if O.ref_available() else "port"
-    n = sample.size // ln
+    stride = stride or ln
+    n = (sample.size - ln) // stride + 1
     threads, cores = cpu_threads()
     res = {}
     legs = [(1, False), (threads, False)]
     if kind == "reference" and O.ref_available(os_flags=True):
         legs += [(1, True), (threads, True)]
     for t, osf in legs:
-        secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind, os_flags=osf)   # page-in / warm
+        secs, _ = O.uniform_mt(sample, stride, ln, n, t, kind=kind, os_flags=osf)   # page-in / warm
         reps = max(1, int(target_s / max(secs, 1e-3)))
         tot = 0.0
         for _ in range(reps):
-            secs, _ = O.uniform_mt(sample, ln, ln, n, t, kind=kind, os_flags=osf)
+            secs, _ = O.uniform_mt(sample, stride, ln, n, t, kind=kind, os_flags=osf)
             tot += secs
         res[(t, osf)] = (n * ln * reps / tot / GIB, reps)
     out = {
         "value": round(res[(threads, False)][0], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "single_core_value": round(res[(1, False)][0], 3),
-        "sample": f"{n} x {ln} B frames ({n * ln / 2**20:.0f} MiB, DRAM-resident), reference stack/pico_frame.c "
+        "sample": f"{n} x {ln} B frames{f' at stride {stride}' if stride != ln else ''} ({n * ln / 2**20:.0f} MiB, "
+                  f"DRAM-resident), reference stack/pico_frame.c "
                   f"pico_checksum built -O3 (PERF=1), pthreads over contiguous frame ranges; "
                   f"{res[(threads, False)][1]} passes on {threads} threads, {res[(1, False)][1]} on 1 thread",
         "cpu_model": cpu_model(), "usable_cores": cores, "cgroup_cpu_max": cgroup_cpu(),
@@ -493,8 +501,9 @@ def verify(kind: str, cfg: dict, slot, out, host, threads: int) -> dict:
     t0 = time.perf_counter()
     if kind == "uniform":
         b, ln, n = slot
+        stride = cfg.get("stride", ln)
         hb = b.cpu().numpy()
-        _, want = O.uniform_mt(hb, ln, ln, n, threads, kind="port")
+        _, want = O.uniform_mt(hb, stride, ln, n, threads, kind="port")
         got = out.cpu().numpy().view(np.uint16)
         frames, bad = n, int((got != want).sum())
         what = f"every frame, oracle_checksum on {threads} threads"
@@ -812,17 +821,18 @@ def main():
     # ---- batches resident in HBM (rotated so the 256 MiB MALL cannot serve repeats)
     if cfg["kind"] == "uniform":
         ln = cfg["frame_bytes"]
+        stride = cfg.get("stride", ln)
         if cfg.get("strong"):
             first, n = shard_range(cfg["frames"], rank, world)
         else:
             first, n = rank * cfg["frames"], cfg["frames"]
         per = n * ln
-        rot = a.rotate or rotation(per)
-        bufs = [make_uniform(n, ln, dev, 1000 + 17 * rank + i) for i in range(rot)]
+        rot = a.rotate or rotation(n * stride)
+        bufs = [make_uniform(n, stride, dev, 1000 + 17 * rank + i) for i in range(rot)]
         outs = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(rot)]
 
         def step(i):
-            batch.checksum_uniform(bufs[i % rot], ln, ln, n, out=outs[i % rot])
+            batch.checksum_uniform(bufs[i % rot], stride, ln, n, out=outs[i % rot])
         frame_bytes = per
         algo_bytes = per + 2 * n                            # frames read + uint16 results written
     elif cfg["kind"] == "ipv4":
@@ -1010,9 +1020,9 @@ def main():
     if rank == 0 and world == 1 and cfg["kind"] == "uniform":
         if not a.no_cpu:
             sample_frames = min(n, 262144)
-            sample = bufs[0][: sample_frames * ln].cpu().numpy()
-            out["cpu_baseline"] = cpu_baseline(sample, ln, a.cpu_seconds)
-        if not a.no_e2e:
+            sample = bufs[0][: (sample_frames - 1) * stride + ln].cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(sample, ln, a.cpu_seconds, stride)
+        if not a.no_e2e and stride == ln:
             out["e2e_host_to_host"] = e2e_rate(n, ln)
     elif rank == 0 and world == 1 and cfg["kind"] in ("ipv4", "ipv6", "eth"):
         if not a.no_cpu:
