@@ -17,7 +17,7 @@ import shutil
 import statistics
 import sys
 
-CFGS = ("c1", "c2", "c2slot", "c2ethmix", "c2tx", "c2tx_nw", "c2nat", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3_reasm_il",
+CFGS = ("c1", "c1_s1536", "c2", "c2slot", "c2ethmix", "c2tx", "c2tx_nw", "c2nat", "c2v6", "c2eth", "c3_reasm", "c3_reasm6", "c3_reasm_il",
         "c3_reasm_retx", "c3_reasm_576", "c3", "c3_64k", "c3_frag", "c4")
 
 
