@@ -587,8 +587,9 @@ def seq_copy_lib():
 # stores; workgroups 0 = one trip each, else a striding grid (8192 = 32 per CU)
 SEQ_COPY_SHAPES = ((0, 4, 0), (0, 8, 0), (1, 4, 0), (2, 4, 0), (0, 4, 8192), (2, 8, 8192))
 # the same copy with its loads 2 bytes off the 16-byte grid (as the reassembly's payload loads), reported
-# beside the ceiling, not as it
-SEQ_COPY_UNALIGNED = ((3, 4, 0), (4, 4, 0))
+# beside the ceiling, not as it: 3 cached loads + stores, 4 nt loads + cached stores, 5 cached loads + nt
+# stores (the reassembly's policy)
+SEQ_COPY_UNALIGNED = ((3, 4, 0), (4, 4, 0), (5, 4, 0))
 
 
 def copy_ceiling(nbytes: int, dev) -> dict:

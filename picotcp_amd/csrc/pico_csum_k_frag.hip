@@ -119,6 +119,16 @@ constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a la
 #ifndef REASM_NP6
 #define REASM_NP6 3u
 #endif
+// The gathers' whole 16-byte unit stores are non-temporal (aux 2, `nt`): c3_reasm 105.5-107.4 us
+// against 110.0-110.8 cached, c3_reasm6 111.2-112.1 against 117.9-118.8; the edge units' partial
+// stores the same either way (profiles/r06/ab_reasm_nts.txt).  The payload loads stay cached
+// (reasm_flat_kernel).
+#ifndef REASM_STORE_AUX
+#define REASM_STORE_AUX 2
+#endif
+#ifndef REASM_EDGE_AUX
+#define REASM_EDGE_AUX 0
+#endif
 // fragment pairs a flat-grid wave gathers at once (their loads in flight together): IPv4 2
 // (3: 113.2 vs 113.4 us, no gain), IPv6 3 (120.9 us; 2: 128.0, 4: 122.2 at 118 VGPRs)
 __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 : REASM_NP4; }
@@ -542,7 +552,7 @@ __device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, Fr
                 const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
                 const uint32_t nr = hi > lo ? hi & 3u : 0u;
                 __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
-                                                       (int)(whole ? so : WIN_OOB), 0, 0);
+                                                       (int)(whole ? so : WIN_OOB), 0, REASM_STORE_AUX);
                 const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
                 __builtin_amdgcn_raw_buffer_store_b64(
                     (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
@@ -968,18 +978,18 @@ __device__ __forceinline__ void pair_store(const PairStep& q, const Window& ow, 
         const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
         const uint32_t nr = hi > lo ? hi & 3u : 0u;
         __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
-                                               (int)(whole ? so : WIN_OOB), 0, 0);
+                                               (int)(whole ? so : WIN_OOB), 0, REASM_STORE_AUX);
         const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
         __builtin_amdgcn_raw_buffer_store_b64(
             (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
-            (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, 0);
+            (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, REASM_EDGE_AUX);
         __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc,
-                                              (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, 0);
+                                              (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, REASM_EDGE_AUX);
         const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc,
-                                              (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, 0);
+                                              (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, REASM_EDGE_AUX);
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
-                                             (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, 0);
+                                             (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, REASM_EDGE_AUX);
     }
 }
 

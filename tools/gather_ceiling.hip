@@ -39,7 +39,7 @@ __device__ __forceinline__ void copy_pair(__amdgpu_buffer_rsrc_t sr, __amdgpu_bu
             const uint32_t x = x0 + 64u * k + lane;
             const bool b = x >= na;
             const uint64_t o = (b ? db : da) + 16u * (b ? x - na : x);
-            __builtin_amdgcn_raw_buffer_store_b128(v[k], dr, (int)(x < nt ? (uint32_t)o : 0x80000000u), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v[k], dr, (int)(x < nt ? (uint32_t)o : 0x80000000u), 0, 2);   // nt (as the product)
         }
     }
 }
@@ -105,7 +105,8 @@ extern "C" int gather_ceiling_launch(int mode, const void* src, uint64_t src_len
 // VARIANT: 0 non-temporal loads and stores, 1 cached loads and stores, 2 non-temporal loads with
 // cached stores, 3 cached loads 2 bytes off the 16-byte grid (byte-unaligned buffer loads, as the
 // reassembly's payload loads: a fragment's payload sits 34 bytes past its 16-byte-aligned frame) with
-// cached aligned stores, 4 the same with non-temporal loads.  n must be a multiple of 16 (the caller
+// cached aligned stores, 4 the same with non-temporal loads, 5 variant 3's loads with non-temporal
+// stores.  n must be a multiple of 16 (the caller
 // copies the tail, if any, itself).
 template <int U, int VARIANT>
 __global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u
         for (int k = 0; k < U; ++k) {
             const uint64_t i = b + 256u * k;
             if (i < n16) {
-                if (VARIANT == 0) __builtin_nontemporal_store(v[k], dst + i);
+                if (VARIANT == 0 || VARIANT == 5) __builtin_nontemporal_store(v[k], dst + i);
                 else dst[i] = v[k];                  // (VARIANT 3 / 4: the source's last unit reads 2 bytes past it)
             }
         }
@@ -152,10 +153,10 @@ extern "C" int seq_copy_launch(int variant, int u, uint32_t blocks, void* dst, c
 #define SC(UU, VV) hipLaunchKernelGGL((seq_copy<UU, VV>), dim3(g), dim3(256), 0, s, d, sr, n16)
     if (u == 8) {
         if (variant == 0) SC(8, 0); else if (variant == 1) SC(8, 1); else if (variant == 2) SC(8, 2);
-        else if (variant == 3) SC(8, 3); else SC(8, 4);
+        else if (variant == 3) SC(8, 3); else if (variant == 4) SC(8, 4); else SC(8, 5);
     } else {
         if (variant == 0) SC(4, 0); else if (variant == 1) SC(4, 1); else if (variant == 2) SC(4, 2);
-        else if (variant == 3) SC(4, 3); else SC(4, 4);
+        else if (variant == 3) SC(4, 3); else if (variant == 4) SC(4, 4); else SC(4, 5);
     }
 #undef SC
     return (int)hipGetLastError();

@@ -111,7 +111,8 @@ def main():
         ("bare_gather_4waves", gather(2)), ("bare_gather_flat", gather(3)), ("sequential_copy_torch", copy),
         ("sequential_copy_nt", seq_copy(0, 4, 0)), ("sequential_copy_cached", seq_copy(1, 4, 0)),
         ("sequential_copy_nt_grid", seq_copy(0, 4, 8192)), ("sequential_copy_unaligned_src", seq_copy(3, 4, 0)),
-        ("sequential_copy_unaligned_src_nt", seq_copy(4, 4, 0)))
+        ("sequential_copy_unaligned_src_nt", seq_copy(4, 4, 0)),
+        ("sequential_copy_unaligned_src_nt_stores", seq_copy(5, 4, 0)))
     for rnd in range(3):
         for name, f in fns:
             res.setdefault(name, []).append(timed(f))
