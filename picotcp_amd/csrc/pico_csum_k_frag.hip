@@ -121,8 +121,10 @@ constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a la
 #endif
 // The gathers' whole 16-byte unit stores are non-temporal (aux 2, `nt`): c3_reasm 105.5-107.4 us
 // against 110.0-110.8 cached, c3_reasm6 111.2-112.1 against 117.9-118.8; the edge units' partial
-// stores the same either way (profiles/r06/ab_reasm_nts.txt).  The payload loads stay cached
-// (reasm_flat_kernel).
+// stores the same either way (profiles/r06/ab_reasm_nts.txt).  Write-through `sc1` (16), `sc1 nt`
+// (18) or `sc0 sc1` (17) whole-unit stores: c3_reasm 116.4-117.2 / 112.9-114.3 / 116.5-116.8 us,
+// c3_reasm6 125.6-125.9 / 123.2-123.7 / 125.7-125.9 (ab_reasm_sc1.txt).  The payload loads stay
+// cached (reasm_flat_kernel).
 #ifndef REASM_STORE_AUX
 #define REASM_STORE_AUX 2
 #endif
