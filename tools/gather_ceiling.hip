@@ -106,7 +106,9 @@ extern "C" int gather_ceiling_launch(int mode, const void* src, uint64_t src_len
 // cached stores, 3 cached loads 2 bytes off the 16-byte grid (byte-unaligned buffer loads, as the
 // reassembly's payload loads: a fragment's payload sits 34 bytes past its 16-byte-aligned frame) with
 // cached aligned stores, 4 the same with non-temporal loads, 5 variant 3's loads with non-temporal
-// stores.  n must be a multiple of 16 (the caller
+// stores, 6 variant 3's bytes from ALIGNED non-temporal loads: each lane loads its own 16-byte chunk,
+// takes the next lane's through ds_bpermute (lane 63 loads it) and shifts the pair 2 bytes with
+// v_alignbyte, non-temporal stores.  n must be a multiple of 16 (the caller
 // copies the tail, if any, itself).
 template <int U, int VARIANT>
 __global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, uint64_t n16) {
@@ -123,18 +125,36 @@ __global__ __launch_bounds__(256) void seq_copy(u32x4* __restrict__ dst, const u
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint64_t i = b + 256u * k;
-            if constexpr (VARIANT >= 3) {
+            if constexpr (VARIANT == 6) {
+                const uint32_t o = (uint32_t)(threadIdx.x + 256u * k) * 16u;
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(i < n16 ? o : 0x80000000u), 0, 2);
+            } else if constexpr (VARIANT >= 3) {
                 const uint32_t o = (uint32_t)(threadIdx.x + 256u * k) * 16u + 2u;
                 v[k] = __builtin_amdgcn_raw_buffer_load_b128(sr, (int)(i < n16 ? o : 0x80000000u), 0, VARIANT == 4 ? 2 : 0);
             } else if (i < n16) {
                 v[k] = VARIANT == 1 ? src[i] : __builtin_nontemporal_load(src + i);
             }
         }
+        if constexpr (VARIANT == 6) {                  // the unit = bytes 2..17 of (own chunk, next lane's chunk)
+            const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const uint64_t i = b + 256u * k;
+                const int src_lane = (int)((lane + 1u) & 63u) * 4;
+                uint32_t nx = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane, (int)v[k].x);
+                if (lane == 63u) {
+                    const uint32_t o = (uint32_t)(threadIdx.x + 256u * k + 1u) * 16u;
+                    nx = __builtin_amdgcn_raw_buffer_load_b32(sr, (int)(i < n16 ? o : 0x80000000u), 0, 0);
+                }
+                v[k] = (u32x4){__builtin_amdgcn_alignbyte(v[k].y, v[k].x, 2u), __builtin_amdgcn_alignbyte(v[k].z, v[k].y, 2u),
+                               __builtin_amdgcn_alignbyte(v[k].w, v[k].z, 2u), __builtin_amdgcn_alignbyte(nx, v[k].w, 2u)};
+            }
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const uint64_t i = b + 256u * k;
             if (i < n16) {
-                if (VARIANT == 0 || VARIANT == 5) __builtin_nontemporal_store(v[k], dst + i);
+                if (VARIANT == 0 || VARIANT == 5 || VARIANT == 6) __builtin_nontemporal_store(v[k], dst + i);
                 else dst[i] = v[k];                  // (VARIANT 3 / 4: the source's last unit reads 2 bytes past it)
             }
         }
@@ -153,10 +173,10 @@ extern "C" int seq_copy_launch(int variant, int u, uint32_t blocks, void* dst, c
 #define SC(UU, VV) hipLaunchKernelGGL((seq_copy<UU, VV>), dim3(g), dim3(256), 0, s, d, sr, n16)
     if (u == 8) {
         if (variant == 0) SC(8, 0); else if (variant == 1) SC(8, 1); else if (variant == 2) SC(8, 2);
-        else if (variant == 3) SC(8, 3); else if (variant == 4) SC(8, 4); else SC(8, 5);
+        else if (variant == 3) SC(8, 3); else if (variant == 4) SC(8, 4); else if (variant == 5) SC(8, 5); else SC(8, 6);
     } else {
         if (variant == 0) SC(4, 0); else if (variant == 1) SC(4, 1); else if (variant == 2) SC(4, 2);
-        else if (variant == 3) SC(4, 3); else if (variant == 4) SC(4, 4); else SC(4, 5);
+        else if (variant == 3) SC(4, 3); else if (variant == 4) SC(4, 4); else if (variant == 5) SC(4, 5); else SC(4, 6);
     }
 #undef SC
     return (int)hipGetLastError();

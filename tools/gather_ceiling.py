@@ -112,7 +112,17 @@ def main():
         ("sequential_copy_nt", seq_copy(0, 4, 0)), ("sequential_copy_cached", seq_copy(1, 4, 0)),
         ("sequential_copy_nt_grid", seq_copy(0, 4, 8192)), ("sequential_copy_unaligned_src", seq_copy(3, 4, 0)),
         ("sequential_copy_unaligned_src_nt", seq_copy(4, 4, 0)),
-        ("sequential_copy_unaligned_src_nt_stores", seq_copy(5, 4, 0)))
+        ("sequential_copy_unaligned_src_nt_stores", seq_copy(5, 4, 0)),
+        ("sequential_copy_aligned_nt_shifted", seq_copy(6, 4, 0)))
+    if not a.only_reasm:                      # variant 6 moves the same bytes as variant 3
+        (buf, d_desc, d_grp, out, d_od, nfr, payload), _, _ = sets[0]
+        n = (payload & ~15) - 16
+        seq_copy(3, 4, 0)(0)
+        ref = out[:n].clone()
+        out[:n].zero_()
+        seq_copy(6, 4, 0)(0)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(ref, out[:n]), "seq_copy variant 6 differs from variant 3"
     for rnd in range(3):
         for name, f in fns:
             res.setdefault(name, []).append(timed(f))
