@@ -1020,6 +1020,12 @@ __device__ __forceinline__ uint32_t pair_gather(const PairStep& q, const Window&
 // or 8 waves per SIMD forced (96 / 75 / 60 VGPRs, no spills) 116.1 / 116.1 / 117.8 us against
 // 115.7 at 4 (105 VGPRs).  The payload loads are cached, not non-temporal: the byte-unaligned
 // 16-byte loads of neighbouring units share lines (113.8 -> 108.9 us, IPv6 121.3 -> 118.3).
+// Fewer, longer waves measured slower, with the next iteration's descriptor and header loads
+// issued under this iteration's payload loads (2 / 3 / 4 iterations a wave: c3_reasm 115.6-115.9 /
+// 119.5-119.8 / 118.1-118.4 us against 103.4-104.6, c3_reasm6 120.1-120.5 / 122.1-122.6 /
+// 126.4-126.5 against 110.1-111.2; profiles/r06/ab_reasm_iters.txt).  Where the time goes
+// (ab_reasm_ablate_finish_plan.txt): without the finish launch 101.6-103.1 / 109.4-109.7 us,
+// without planners and finish 99.5-99.9 / 105.2-106.0.
 template <bool V6>
 __global__ __launch_bounds__(64) void reasm_flat_kernel(FragArgs p) {
     constexpr uint32_t HDR = V6 ? 40u : 20u;
