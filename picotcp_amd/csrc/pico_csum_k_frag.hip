@@ -137,6 +137,11 @@ __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 
 // Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
 // c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
 // 130.5 / 143.6 -- the planners then end in the launch's tail)
+// A planner that loads the next datagram's descriptors before planning this one and its headers
+// before this one's header copy measured no better: c3_reasm 102.7-104.1 against 104.4-105.1 us,
+// c3_reasm6 112.6-113.7 against 110.2-111.2, c3_reasm_retx 119.3-119.8 against 111.6-113.4; with
+// the gather's occupancy held at 4 / 5 / 5.5 waves a SIMD (LDS) slower still
+// (profiles/r06/ab_reasm_plan_pipelined.txt, ab_reasm_plan_occupancy.txt).
 __host__ __device__ __forceinline__ uint32_t plan_per(uint32_t n_dgram) {
     const uint32_t q = n_dgram / 512u;
     return q < 1u ? 1u : (q > 8u ? 8u : q);
