@@ -145,6 +145,9 @@ __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 
 // the gather's occupancy held at 4 / 5 / 5.5 waves a SIMD (LDS) slower still
 // (profiles/r06/ab_reasm_plan_pipelined.txt, ab_reasm_plan_occupancy.txt).
 __host__ __device__ __forceinline__ uint32_t plan_per(uint32_t n_dgram) {
+#ifdef REASM_PLAN_PER
+    return REASM_PLAN_PER;
+#endif
     const uint32_t q = n_dgram / 512u;
     return q < 1u ? 1u : (q > 8u ? 8u : q);
 }             // fragment pairs a flat-grid wave gathers at once
@@ -160,6 +163,32 @@ struct FragLds {
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t* p) { return (uint32_t)*p; }
+
+// One masked unit's stores into the output window at so (16-byte aligned): the whole unit as one
+// aligned 16-byte store; else, by the edge lanes alone (exec-masked), its whole dwords [a, a + c)
+// as a b64 and / or a b32, then its last partial dword's bytes as a b16 and / or a b8.  The whole
+// units' stores are non-temporal (REASM_STORE_AUX).
+__device__ __forceinline__ void edge_store(const Window& ow, const uint32_t (&xw)[4], uint32_t lo, uint32_t hi, uint32_t so) {
+    const bool whole = lo == 0u && hi == 16u;
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc, (int)(whole ? so : WIN_OOB), 0,
+                                           REASM_STORE_AUX);
+    if (!whole && hi > lo) {
+        const uint32_t a = lo >> 2, bq = hi >> 2, c = bq <= a ? 0u : bq - a, nr = hi & 3u;
+        const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
+        const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
+        if (c >= 2u)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
+                (int)(so + 4u * a), 0, REASM_EDGE_AUX);
+        if (c & 1u)
+            __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc, (int)(so + 4u * a2),
+                                                  0, REASM_EDGE_AUX);
+        if (nr >= 2u) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc, (int)(so + 4u * bq), 0, REASM_EDGE_AUX);
+        if (nr & 1u)
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
+                                                 (int)(so + 4u * bq + (nr & 2u)), 0, REASM_EDGE_AUX);
+    }
+}
 
 // One fragment's header.  IPv4 as pico_ipv4_process_in hands a fragment on (net_len,
 // transport_len = tot - net_len, frag); IPv6 as pico_ipv6_extension_headers does (the walk must
@@ -552,27 +581,9 @@ __device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, Fr
                     const uint32_t kb = 4u * w < lo ? 0u : min((uint32_t)max((int)hi - 4 * w, 0), 4u);
                     xw[w] &= (uint32_t)(0xFFFFFFFFull >> (32u - 8u * kb));
                 }
-                // stores, a fixed sequence of 5 per slot (out-of-range ones void): the whole unit as
-                // one aligned 16-byte store; else its whole dwords [a, a + c) as a b64 and / or a b32,
-                // then a last partial dword's bytes as a b16 and / or a b8
-                const uint32_t ou = at + 16u * u - o;       // the unit's place (16-byte aligned in t)
-                const uint32_t so = ou;
-                const bool whole = lo == 0u && hi == 16u;
-                const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
-                const uint32_t nr = hi > lo ? hi & 3u : 0u;
-                __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
-                                                       (int)(whole ? so : WIN_OOB), 0, REASM_STORE_AUX);
-                const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
-                __builtin_amdgcn_raw_buffer_store_b64(
-                    (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
-                    (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc,
-                                                      (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, 0);
-                const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
-                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc,
-                                                      (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
-                                                     (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, 0);
+                // stores: edge_store (the whole unit, or an edge unit's bytes by its lane alone)
+                const uint32_t so = at + 16u * u - o;       // the unit's place (16-byte aligned in t)
+                edge_store(ow, xw, lo, hi, so);
                 acc = dot2_add(xw[3], dot2_add(xw[2], dot2_add(xw[1], dot2_add(xw[0], acc))));   // even offset
                 if (ok && at + 16u * u <= o + 4u) {         // transport bytes 0..3 (ICMPv6 type), 4..7 (UDP crc)
 #pragma unroll
@@ -972,33 +983,23 @@ __device__ __forceinline__ uint32_t pair_sum(const PairStep& q, uint32_t lane, u
     return acc;
 }
 
-// The masked units' stores, a fixed sequence of 5 per slot (out-of-range ones void): the whole unit
-// as one aligned 16-byte store; else its whole dwords [a, a + c) as a b64 and / or a b32, then a
-// last partial dword's bytes as a b16 and / or a b8.
+// The masked units' stores: the whole units as one aligned 16-byte store (the other lanes void);
+// an edge unit's whole dwords [a, a + c) as a b64 and / or a b32, then its last partial dword's
+// bytes as a b16 and / or a b8, by the edge lanes alone (exec-masked), and nothing for a row past
+// the pair's units.  Against a fixed sequence of 5 stores a row, the edge ones void by offset
+// (profiles/r06/ab_reasm_edge_exec.txt): c3_reasm 102.6-103.4 vs 103.4-104.3 us, c3_reasm6
+// 109.3 vs 110.3-111.0, c3_reasm_576 on the flat grid 169.8-170.1 vs 217.9-219.2 (the edge stores
+// issued only when a lane needs them by a wave ballot: 173.7-173.9; no edge stores at all, a
+// timing-only build: c3_reasm 98.0, c3_reasm_576 161.3-161.8, ab_reasm*_edge_stores.txt).
 template <int U>
 __device__ __forceinline__ void pair_store(const PairStep& q, const Window& ow, uint32_t lane, uint32_t u0,
                                            const uint4 (&c0)[U]) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
+        if (u0 + 64u * k >= q.nt) continue;             // (wave-uniform) a row past the pair's units
         const UnitSpan us = unit_span(q, u0 + 64u * k + lane);
         const uint32_t xw[4] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w};
-        const uint32_t lo = us.lo, hi = us.hi, so = us.so;
-        const bool whole = lo == 0u && hi == 16u;
-        const uint32_t a = lo >> 2, bq = hi >> 2, c = whole || bq <= a ? 0u : bq - a;
-        const uint32_t nr = hi > lo ? hi & 3u : 0u;
-        __builtin_amdgcn_raw_buffer_store_b128((u32x4){xw[0], xw[1], xw[2], xw[3]}, ow.rsrc,
-                                               (int)(whole ? so : WIN_OOB), 0, REASM_STORE_AUX);
-        const uint32_t a1 = min(a + 1u, 3u), a2 = c >= 2u ? a + 2u : a;
-        __builtin_amdgcn_raw_buffer_store_b64(
-            (u32x2){sel4s(a & 3u, xw[0], xw[1], xw[2], xw[3]), sel4s(a1, xw[0], xw[1], xw[2], xw[3])}, ow.rsrc,
-            (int)(c >= 2u ? so + 4u * a : WIN_OOB), 0, REASM_EDGE_AUX);
-        __builtin_amdgcn_raw_buffer_store_b32(sel4s(a2 & 3u, xw[0], xw[1], xw[2], xw[3]), ow.rsrc,
-                                              (int)(c & 1u ? so + 4u * a2 : WIN_OOB), 0, REASM_EDGE_AUX);
-        const uint32_t tw = sel4s(bq & 3u, xw[0], xw[1], xw[2], xw[3]);
-        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)tw, ow.rsrc,
-                                              (int)(nr >= 2u ? so + 4u * bq : WIN_OOB), 0, REASM_EDGE_AUX);
-        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tw >> (8u * (nr & 2u))), ow.rsrc,
-                                             (int)(nr & 1u ? so + 4u * bq + (nr & 2u) : WIN_OOB), 0, REASM_EDGE_AUX);
+        edge_store(ow, xw, us.lo, us.hi, us.so);
     }
 }
 
@@ -1305,11 +1306,12 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
     // datagram: 256 19.2 vs 18.7 us, 512 22.6 vs 23.9, 1024 35.4 vs 36.9;
     // profiles/r05/ab_reasm_small_batches.txt)
     const uint32_t fmin = flat_min ? flat_min : REASM_FLAT_MIN;
-    // automatic: a batch of more than 64 fragments a datagram on average (64 KiB datagrams over a
-    // small MTU) takes one workgroup per datagram.  (The flat grid plans up to FLAT_MAXF = 128 a
-    // datagram, but on c3_reasm_576 -- 117 fragments of 552 B -- it measured 221 us, and 217 us with
-    // four pairs a gather wave, against 217 us here: profiles/r06/ab_reasm_128*.txt.)
-    if (n_dgram >= fmin && (flat_min || (uint64_t)n_frag <= 64ull * n_dgram)) {
+    // automatic: a batch of more than FLAT_MAXF = 128 fragments a datagram on average takes one
+    // workgroup per datagram (the planners hold 128).  c3_reasm_576 -- 117 fragments of 552 B --
+    // takes 170 us on the flat grid with the exec-masked edge stores (pair_store), against 210 us
+    // here; with the edge stores void by offset the flat grid took 218-221 us and this threshold
+    // was 64 (profiles/r06/ab_reasm_128*.txt, ab_reasm576_edge_exec.txt).
+    if (n_dgram >= fmin && (flat_min || (uint64_t)n_frag <= (uint64_t)FLAT_MAXF * n_dgram)) {
         // S waves per datagram, FPI fragments each on average
         const uint32_t fpi = 2u * flat_np(v6 != 0);
         const uint64_t its = ((uint64_t)n_frag + fpi - 1u) / fpi;

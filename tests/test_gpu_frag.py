@@ -365,11 +365,12 @@ def test_flat_grid_true_retransmits(v6, same):
 
 
 @pytest.mark.parametrize("v6", [False, True])
-def test_flat_grid_two_fragments_a_lane(v6):
+def test_flat_grid_two_fragments_a_lane(v6, reasm_path):
     """Datagrams of 65-128 fragments (64 KiB over 552 / 520-byte fragments: the planner holds two
-    fragments a lane), some with retransmitted fragments -- the same bytes or altered, in either
-    half of the arrival order -- on 600 datagrams: every verdict, checksum and reassembled byte
-    against the oracle.  (More than 128 fragments: test_batch_shapes.)"""
+    fragments a lane; the launcher's automatic choice is the flat grid up to 128 a datagram on
+    average), some with retransmitted fragments -- the same bytes or altered, in either half of the
+    arrival order -- on 600 datagrams: every verdict, checksum and reassembled byte against the
+    oracle, and again on one workgroup per datagram.  (More than 128 fragments: test_batch_shapes.)"""
     rng = np.random.default_rng(23 + v6)
     pl = 520 if v6 else 552
     lens = rng.integers(34000, 65000, 600)
@@ -386,3 +387,7 @@ def test_flat_grid_two_fragments_a_lane(v6):
     od, size = layout(lens, shift=8 if v6 else 4, hdr=40 if v6 else 20)
     wl, wv = check(buf, d, grp, od, size, v6=v6)
     assert (wv != 8).mean() > 0.9
+    if reasm_path == "auto":                             # and one workgroup per datagram
+        batch.set_reasm_flat(2)
+        wl2, wv2 = check(buf, d, grp, od, size, v6=v6)
+        assert (wv2 == wv).all() and (wl2 == wl).all()
