@@ -418,7 +418,8 @@ const char *pico_csum_last_error(void);   /* thread-local, "" when none */
  *   group 2: descriptor batches (the sorted-rounds kernel) with fpw frames per wave (1..64);
  *            the other arguments are ignored.
  *   group 4..64 (power of 2): uniform rings -- lanes per frame; cpl = 16-byte chunks per lane
- *            per pass (1,2,4,8); unroll = frames in flight per group (1,2,4; cpl*unroll <= 8);
+ *            per pass (1,2,4,8; 3 and 5-7 with group >= 8 and pipeline != 1: the pipelined
+ *            kernel, frames past its one pass round cpl up to 4 / 8); unroll = frames in flight per group (1,2,4; cpl*unroll <= 8);
  *            fpw = frames per wave (multiple of 64/group, <= 64); nt = 0 auto / 1 plain /
  *            2 non-temporal loads; pipeline = 0 auto / 1 off / 2 on / 3 on with global instead
  *            of buffer-window loads (frames that fit one pass: double-buffered frame sets).

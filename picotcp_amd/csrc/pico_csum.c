@@ -206,8 +206,8 @@ int pico_csum_set_launch_override(uint32_t group, uint32_t cpl, uint32_t unroll,
                                         "instead of the buffer window)");
     if (!(group == 4 || group == 8 || group == 16 || group == 32 || group == 64))
         return fail(PICO_CSUM_EINVAL, "group must be 2 (descriptor batches) or 4, 8, 16, 32, 64 (uniform rings)");
-    if (!(cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8))
-        return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8");
+    if (!(cpl >= 1 && cpl <= 8) || ((cpl == 3 || cpl >= 5) && cpl != 8 && (group < 8 || pipeline == 1)))
+        return fail(PICO_CSUM_EINVAL, "cpl must be 1, 2, 4 or 8, or 3 / 5-7 with group >= 8 on the pipelined kernel");
     if (!(unroll == 1 || unroll == 2 || unroll == 4) || cpl * unroll > 8)
         return fail(PICO_CSUM_EINVAL, "unroll must be 1, 2 or 4 with cpl*unroll <= 8");
     if (fpw == 0 || fpw > 64 || fpw % (64 / group) != 0)
@@ -241,6 +241,15 @@ static struct shape uniform_shape(uint32_t n, uint32_t len)
     s.nt = len >= 1024u;
     ng = 64u / s.G;
     s.pipe = (uint64_t)s.G * s.CPL * 16u >= (uint64_t)len + 15u;
+    if (s.pipe && s.G >= 8) {
+        /* the pipelined kernel takes exactly the chunks a lane needs (3, 5-7 besides the powers of
+         * two), so no chunk slot is void in every frame: C1 (1500 B, G 16) 59.2-59.4 us at 6 a lane
+         * against 61.3 at 8 (profiles/r06/c1_cpl_sweep.txt) */
+        const uint32_t need = (uint32_t)(((uint64_t)len + 15u + 15u) / 16u);
+        const uint32_t exact = (need + s.G - 1) / s.G;
+        if (exact == 3 || (exact >= 5 && exact < s.CPL))
+            s.CPL = exact;
+    }
     if (s.pipe) {
         f = n / 32768u;
         f -= f % ng;
@@ -407,6 +416,11 @@ int pico_checksum_batch_uniform_dev(const void *d_base, uint64_t base_len, uint6
         return launch_status(pico_csum_launch_uniform_pf(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL,
                                                          s.nt, s.fpw, g_ovr_pipe != 3, stream),
                              "pico_checksum_batch_uniform_dev");
+    if (s.CPL == 3 || (s.CPL >= 5 && s.CPL <= 7)) {   /* the multi-pass kernel: power-of-two passes */
+        s.CPL = s.CPL == 3 ? 4 : 8;
+        if (s.CPL * s.U > 8)
+            s.U = 1;
+    }
     return launch_status(pico_csum_launch_raw(d_base, base_len, stride, len, n, seed, d_out, s.G, s.CPL, s.U, s.nt,
                                               s.fpw, stream),
                          "pico_checksum_batch_uniform_dev");

@@ -481,9 +481,17 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 #define PICO_FOR_RAW(Y) PICO_FOR_CU(Y, 64) PICO_FOR_CU(Y, 32) PICO_FOR_CU(Y, 16) PICO_FOR_CU(Y, 8) PICO_FOR_CU(Y, 4)
 
-inline bool shape_ok(uint32_t G, uint32_t CPL, uint32_t fpw) {
+// The software-pipelined uniform kernel also takes 3 and 5-7 chunks a lane (G >= 8): a frame then
+// fills its lane group's one pass without whole void chunk slots (1500 B at G = 16: 6 chunks a
+// lane, where CPL 8 left chunk slots 96-127 void in every frame).
+#define PICO_FOR_PF_SHAPES(X) \
+    PICO_FOR_SHAPES(X) \
+    X(64, 3) X(64, 5) X(64, 6) X(64, 7) X(32, 3) X(32, 5) X(32, 6) X(32, 7) \
+    X(16, 3) X(16, 5) X(16, 6) X(16, 7) X(8, 3)  X(8, 5)  X(8, 6)  X(8, 7)
+
+inline bool shape_ok(uint32_t G, uint32_t CPL, uint32_t fpw, bool pf = false) {
     if (!(G == 4 || G == 8 || G == 16 || G == 32 || G == 64)) return false;
-    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8)) return false;
+    if (!(CPL == 1 || CPL == 2 || CPL == 4 || CPL == 8 || (pf && G >= 8 && (CPL == 3 || (CPL >= 5 && CPL <= 7))))) return false;
     return fpw >= 1 && fpw <= 64 && fpw % (64 / G) == 0;
 }
 

@@ -948,6 +948,10 @@ __device__ __forceinline__ void pair_issue(const PairStep& q, uint32_t lane, uin
         const uint32_t x = u0 + 64u * k + lane;
         const bool inb = x >= q.na;
         const uint32_t u = inb ? x - q.na : x, v = inb ? q.vb : q.va;
+        if (u0 + 64u * k >= q.nt) {                     // (wave-uniform) a row past the pair's units:
+            c0[k] = make_uint4(0, 0, 0, 0);             // no load (c3_reasm 98.6-98.7 vs 102.3-103.1 us,
+            continue;                                   // c3_reasm6 105.8-106.3 vs 109.2-109.5,
+        }                                               // c3_reasm_576 158.8-159.4 vs 165.5-166.3)
         c0[k] = load_win<false>(win, x < q.nt ? v + 16u * u : WIN_OOB);   // (cached: see reasm_flat_kernel)
     }
 }

@@ -229,7 +229,7 @@ extern "C" {
 int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t stride, uint32_t len, uint32_t n,
                                 uint32_t seed, uint16_t* out, uint32_t G, uint32_t CPL, uint32_t nt, uint32_t fpw,
                                 uint32_t win, void* stream) {
-    if (!shape_ok(G, CPL, fpw) || (uint64_t)G * CPL * 16u < (uint64_t)len + 15u) return (int)hipErrorInvalidValue;
+    if (!shape_ok(G, CPL, fpw, true) || (uint64_t)G * CPL * 16u < (uint64_t)len + 15u) return (int)hipErrorInvalidValue;
     if (n == 0) return (int)hipSuccess;
     RawArgs a{static_cast<uint8_t*>(const_cast<void*>(base)), base_len, nullptr, stride, len, n, seed, -1, 0u, fpw,
               out, nullptr};
@@ -247,7 +247,7 @@ int pico_csum_launch_uniform_pf(const void* base, uint64_t base_len, uint64_t st
         else hipLaunchKernelGGL((csum_uniform_pf_kernel<g, c, 0>), grid, block, 0, s, a);               \
         return (int)hipGetLastError();                                                                   \
     }
-    PICO_FOR_SHAPES(X)
+    PICO_FOR_PF_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }

@@ -135,7 +135,12 @@ def test_launch_override_validation():
     lib = _lib.load()
     # uniform rings: group 4..64
     assert lib.pico_csum_set_launch_override(12, 2, 1, 16, 0, 0) == -_lib.EINVAL
-    assert lib.pico_csum_set_launch_override(16, 3, 1, 16, 0, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 3, 1, 16, 0, 1) == -_lib.EINVAL   # 3 / 5-7: pipelined only
+    assert lib.pico_csum_set_launch_override(4, 6, 1, 16, 0, 0) == -_lib.EINVAL    # ... and group >= 8
+    assert lib.pico_csum_set_launch_override(16, 6, 2, 16, 0, 0) == -_lib.EINVAL   # cpl * unroll <= 8
+    assert lib.pico_csum_set_launch_override(16, 9, 1, 16, 0, 0) == -_lib.EINVAL
+    assert lib.pico_csum_set_launch_override(16, 6, 1, 16, 2, 2) == 0
+    assert lib.pico_csum_set_launch_override(32, 3, 1, 16, 2, 0) == 0
     assert lib.pico_csum_set_launch_override(16, 2, 1, 6, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 4, 4, 16, 0, 0) == -_lib.EINVAL
     assert lib.pico_csum_set_launch_override(16, 2, 1, 16, 4, 0) == -_lib.EINVAL

@@ -13,7 +13,8 @@ from tests import golden_data as G
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
-SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)]
+SHAPES = [(g, c) for g in (4, 8, 16, 32, 64) for c in (1, 2, 4, 8)] + \
+    [(g, c) for g in (8, 16, 32, 64) for c in (3, 5, 6, 7)]     # (the pipelined kernel's extra shapes)
 # descriptor batches: the sorted-rounds kernel, automatic or with a forced frames-per-wave
 # (1: a wave per frame; 5 / 7 / 13: ragged waves; 64: full waves whatever the batch size)
 FPWS = (1, 5, 7, 13, 64)
@@ -67,7 +68,7 @@ def test_uniform_every_shape(g, c):
         want = O.batch_uniform(buf, stride, ln, n, seed)
         d = to_dev(buf)
         for fpw in sorted({64 // g, 64, (64 // g) * 3 if (64 // g) * 3 <= 64 else 64}):
-            for pipe in (1, 2):
+            for pipe in ((2,) if c in (3, 5, 6, 7) else (1, 2)):   # (frames past one pass: multi-pass)
                 batch.set_launch_override(g, c, fpw, 1, 2 if pipe == 2 else 1, pipe)
                 got = u16(batch.checksum_uniform(d, stride, ln, n, seed=seed))
                 np.testing.assert_array_equal(got, want, err_msg=f"g={g} c={c} fpw={fpw} pipe={pipe} len={ln} "
