@@ -553,6 +553,9 @@ __device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, Fr
             else n = make_pair((c.i2 == c.i ? c.i : c.i2) + 1u);
             return n;
         };
+        // (rows past a pair's units load through the void offset: skipping them by a uniform
+        // branch, as the flat grid's pair_issue does, measured slower here -- c3_reasm_576 on this
+        // path 190.8 vs 180.0 us, c3_reasm 128.4-129.5 vs 124.3-125.1; ab_reasm_wg_void_rows.txt)
         auto issue = [&](const Step& st, uint4 (&c0)[U]) {
             const Window win = make_window(st.wlo, st.wsz);   // empty for an invalid step
 #pragma unroll
