@@ -564,17 +564,12 @@ __device__ __forceinline__ void reassemble_one(const FragArgs& p, uint32_t g, Fr
                 const bool inb = x >= st.na;
                 const uint32_t u = inb ? x - st.na : x, v = inb ? st.vb : st.va;
                 const bool ok = st.valid && x < st.nt;
-                if (!st.valid || st.u0 + 64u * k >= st.nt) {   // (uniform) a row past the pair: no load
-                    c0[k] = make_uint4(0, 0, 0, 0);
-                    continue;
-                }
                 c0[k] = load_win<false>(win, ok ? v + 16u * u : WIN_OOB);   // byte-unaligned: the unit's 16 bytes
             }
         };
         auto process = [&](const Step& st, const uint4 (&c0)[U]) {
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                if (st.u0 + 64u * k >= st.nt) continue;     // (uniform) a row past the pair: nothing
                 const uint32_t x = st.u0 + 64u * k + lane;
                 const bool ok = x < st.nt;
                 const bool inb = x >= st.na;
