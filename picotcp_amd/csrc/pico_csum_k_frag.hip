@@ -125,6 +125,14 @@ constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a la
 // (18) or `sc0 sc1` (17) whole-unit stores: c3_reasm 116.4-117.2 / 112.9-114.3 / 116.5-116.8 us,
 // c3_reasm6 125.6-125.9 / 123.2-123.7 / 125.7-125.9 (ab_reasm_sc1.txt).  The payload loads stay
 // cached (reasm_flat_kernel).
+#ifndef REASM_FLAT_LDS
+// LDS a flat-grid wave reserves when its datagrams average <= 64 fragments: 8 KiB holds the grid
+// at 5 waves a SIMD (20 a CU; the IPv4 kernel's 62 VGPRs would allow 8).  c3_reasm_retx 111.9-112.0
+// against 119.0-119.3 us, c3_reasm and c3_reasm6 the same (99.3-99.5 / 105.8-106.4); smaller
+// fragments want every wave: c3_reasm_576 186.4-186.7 capped against 159.0-159.3
+// (profiles/r06/ab_reasm_flat_occupancy.txt).
+#define REASM_FLAT_LDS 8192u
+#endif
 #ifndef REASM_STORE_AUX
 #define REASM_STORE_AUX 2
 #endif
@@ -1333,11 +1341,12 @@ int pico_csum_launch_reassemble(int v6, const void* base, uint64_t base_len, con
             a.slot = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + plan_b);
             a.S = S;
             const dim3 fg((unsigned)blocks), fb(64);
+            const uint32_t lds = (uint64_t)n_frag <= 64ull * n_dgram ? REASM_FLAT_LDS : 0u;
             if (v6) {
-                hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, 0, s, a);
+                hipLaunchKernelGGL((reasm_flat_kernel<true>), fg, fb, lds, s, a);
                 hipLaunchKernelGGL((reasm_finish_kernel<true>), dim3((n_dgram + 63u) / 64u), dim3(64 * REASM_FINISH_WAVES), 0, s, a);
             } else {
-                hipLaunchKernelGGL((reasm_flat_kernel<false>), fg, fb, 0, s, a);
+                hipLaunchKernelGGL((reasm_flat_kernel<false>), fg, fb, lds, s, a);
                 hipLaunchKernelGGL((reasm_finish_kernel<false>), dim3((n_dgram + 63u) / 64u), dim3(64 * REASM_FINISH_WAVES), 0, s, a);
             }
             return (int)hipGetLastError();
