@@ -67,6 +67,9 @@ struct SortedWaveLds {
 // (profiles/r03s3/README.md): 8 chunks per lane per step (8 KiB; StreamLds 10 KiB a wave, 4
 // workgroups of 4 waves per CU), two steps in flight, non-temporal loads.
 constexpr uint32_t SCPL = 8;                 // chunks per lane per step
+#ifndef STREAM_LAST_NOPF
+#define STREAM_LAST_NOPF 1
+#endif
 constexpr uint32_t SQ = 64u * SCPL;          // chunks per step
 struct StreamLds {
     uint4 raw[SQ];           // the step's bytes, chunk slots swizzled (sslot)
@@ -1290,9 +1293,14 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
     if (!ETH || lo != lo0) load_step(0u, v);             // MODE 3: the span starts elsewhere
     STAMP(1);
     // one step: cur is staged and summed while nxt's loads (step st + 1) are in flight
-    auto step = [&](uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
+    auto step = [&](auto pf, uint32_t st, uint4 (&cur)[SCPL], uint4 (&nxt)[SCPL]) {
         const uint32_t qb = st * SQ;
+#if STREAM_LAST_NOPF
+        if constexpr (decltype(pf)::value) load_step(qb + SQ, nxt);
+#else
+        (void)pf;
         load_step(qb + SQ, nxt);
+#endif
         asm volatile("" ::: "memory");
 #pragma unroll
         for (uint32_t c = 0; c < SCPL; ++c) S.raw[sslot(64u * c + lane)] = cur[c];
@@ -1372,16 +1380,36 @@ __device__ __forceinline__ bool stream_batch(const FlatArgs& p, StreamLds& S, ui
         // two steps a trip, the register sets swapping roles: each step's wait covers only its own
         // loads (a copy of the next set into this one at the end of a trip would wait on them too,
         // leaving one step in flight across the wait)
-        for (uint32_t st = 0; st < nsteps; st += 2) {
-            step(st, v, vn);
-            if (st + 1u >= nsteps) break;
-            step(st + 1u, vn, v);
+#if STREAM_LAST_NOPF
+        // the last step loads nothing ahead (its next step would be past the span: 8 void loads):
+        // c2v6 22.3-22.7 vs 22.9-23.5 us, c2nat 30.9-31.4 vs 31.2-31.7, c2 and c2tx the same
+        // (profiles/r06/ab_stream_last_nopf.txt)
+        uint32_t st = 0;
+        for (; st + 2u < nsteps; st += 2) {
+            step(std::true_type{}, st, v, vn);
+            step(std::true_type{}, st + 1u, vn, v);
         }
+        if (st + 1u < nsteps) {
+            step(std::true_type{}, st, v, vn);
+            step(std::false_type{}, st + 1u, vn, v);
+        } else if (st < nsteps) {
+            step(std::false_type{}, st, v, vn);
+        }
+#else
+        for (uint32_t st = 0; st < nsteps; st += 2) {
+            step(std::true_type{}, st, v, vn);
+            if (st + 1u >= nsteps) break;
+            step(std::true_type{}, st + 1u, vn, v);
+        }
+#endif
     } else {
         // MODE 3 (both families' parse in the loop): one step a trip, the sets copied -- the
         // two-step trip spills there
+        // (every step loads ahead here: the last step without its void loads measured slower on
+        // MODE 3, c2eth 25.5-25.8 vs 23.5-23.8 us, c2ethmix 28.2-29.0 vs 26.4-27.3;
+        // profiles/r06/ab_stream_last_nopf.txt)
         for (uint32_t st = 0; st < nsteps; ++st) {
-            step(st, v, vn);
+            step(std::true_type{}, st, v, vn);
 #pragma unroll
             for (uint32_t c = 0; c < SCPL; ++c) v[c] = vn[c];
         }
