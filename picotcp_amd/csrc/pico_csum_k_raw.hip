@@ -209,6 +209,9 @@ __global__ __launch_bounds__(256) void csum_uniform_pf_kernel(RawArgs p) {
     uint4 va[CPL], vb[CPL];
     Frame fa = frame(0), fb;
     issue(fa, va);
+    // (the wave's last trip issues one set past its frames, all void loads at C1's 8 frames a
+    // wave; skipping it measured mixed: c1 57.2-57.3 vs 57.6-57.8 us, c1_s1536 59.5-60.0 vs
+    // 58.7-58.8 -- profiles/r06/ab_c1_notail.txt; not kept)
     for (uint32_t i = 0; i < cnt; i += 2 * NG) {
         fb = frame(i + NG);
         issue(fb, vb);                                   // set i+NG in flight
