@@ -142,7 +142,9 @@ constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a la
 // fragment pairs a flat-grid wave gathers at once (their loads in flight together): IPv4 2
 // (3: 113.2 vs 113.4 us, no gain), IPv6 3 (120.9 us; 2: 128.0, 4: 122.2 at 118 VGPRs); again
 // with the nt stores (profiles/r06/ab_reasm_np.txt): IPv4 3 pairs 106.5-107.7 against 103.2-103.8,
-// IPv6 2 / 4 pairs 114.7-115.4 / 114.2-114.6 against 110.7-111.1
+// IPv6 2 / 4 pairs 114.7-115.4 / 114.2-114.6 against 110.7-111.1; on c3_reasm_576 (552 B fragments) IPv4
+// 3 / 4 pairs 155.3-155.6 / 154.4-155.2 against 158.9-159.3, c3_reasm 102.8-102.9 / 111.1 against
+// 98.4-99.7 (ab_reasm576_np.txt: not worth a second instantiation)
 __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 : REASM_NP4; }
 // Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
 // c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
