@@ -75,6 +75,21 @@ def test_uniform_every_shape(g, c):
                                                                  f"stride={stride}")
 
 
+def test_uniform_automatic_shapes_every_length_class():
+    """The launcher's own shape (no override) over frame lengths that land on every lane-group
+    width and every exact chunk count of the pipelined kernel (3, 5-7 chunks a lane as well as the
+    powers of two), odd strides and a seed -- against the oracle."""
+    rng = np.random.default_rng(77)
+    for ln in list(range(1, 200, 13)) + list(range(200, 2200, 37)) + [1500, 1520, 1521, 1522, 4000, 8170]:
+        stride = ln + int(rng.integers(0, 9))
+        n = int(rng.integers(100, 1500))
+        buf = synth.uniform_batch(n, ln, stride, seed=ln)
+        seed = int(rng.integers(0, 1 << 32))
+        want = O.batch_uniform(buf, stride, ln, n, seed)
+        got = u16(batch.checksum_uniform(to_dev(buf), stride, ln, n, seed=seed))
+        np.testing.assert_array_equal(got, want, err_msg=f"len={ln} stride={stride} n={n}")
+
+
 def test_uniform_c1_full_size():
     """C1 at its full size: 256K x 1500 B, bit-exact against the oracle on every frame."""
     n, ln = 262144, 1500
