@@ -148,7 +148,9 @@ constexpr uint32_t FLAT_MAXF = 128u;         // fragments a plan holds (two a la
 __host__ __device__ constexpr uint32_t flat_np(bool v6) { return v6 ? REASM_NP6 : REASM_NP4; }
 // Datagrams a planner workgroup plans in turn: 512 planners, at most 8 datagrams each (c3_reasm /
 // c3_reasm6, 4096 datagrams: 8 a planner 113.7 / 127.3 us, 4 127.4 (IPv6), 1 118.0 / 130.0, 16
-// 130.5 / 143.6 -- the planners then end in the launch's tail)
+// 130.5 / 143.6 -- the planners then end in the launch's tail).  Again on the final gather
+// (profiles/r06/ab_reasm_plan_per_final.txt): 4 a planner c3_reasm 98.6-99.3 vs 97.7-98.1 us,
+// c3_reasm6 104.8-106.1 vs 104.6, c3_reasm_retx 105.9-106.8 vs 110.1-110.3; 16: 114.5 / 130.2 / 169
 // A planner that loads the next datagram's descriptors before planning this one and its headers
 // before this one's header copy measured no better: c3_reasm 102.7-104.1 against 104.4-105.1 us,
 // c3_reasm6 112.6-113.7 against 110.2-111.2, c3_reasm_retx 119.3-119.8 against 111.6-113.4; with
