@@ -166,6 +166,8 @@ __device__ __forceinline__ uint32_t collect(uint32_t res, uint32_t val, uint32_t
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
+// (generic pointer: flat loads.  As global-address-space loads -- vmcnt only -- c2slot, c2eth,
+// c3_frag measured the same: profiles/r06/ab_global_chunks.txt)
 template <bool NT>
 __device__ __forceinline__ uint4 load_chunk_t(const uint8_t* a0, uint32_t k) {
     const u32x4* q = reinterpret_cast<const u32x4*>(a0 + ((uint64_t)k << 4));
